@@ -1,0 +1,126 @@
+"""Headline benchmark: whole-node training tokens/sec, GPT-2 124M bf16 DDP.
+
+BASELINE.json metric/config: GPT-2 124M, nanoGPT semantics — micro-batch 12 x
+block 1024, 40 micro-steps per optimizer step divided over the ranks
+(491,520 tokens per step regardless of N, i.e. strong scaling of a fixed
+global batch), synthetic tokens, random init.  One timed "step" is a full
+optimizer iteration: grad_accum x (fwd + bwd) with the bucketed RCCL
+all-reduce overlapped on the last micro-step, global-norm clip, fused AdamW.
+
+    python bench.py --gpus 1 --steps 5 --warmup 2
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8 --steps 10 --warmup 3
+
+Rank 0 prints exactly one JSON line on stdout (everything else goes to stderr).
+"""
+
+from __future__ import annotations
+
+import argparse
+import contextlib
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+GLOBAL_MICRO_STEPS = 40  # nanoGPT train_gpt2: 5 * 8
+METRIC = "tokens/sec (whole node) GPT-2 124M DDP"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--micro-batch", type=int, default=12)
+    ap.add_argument("--block-size", type=int, default=1024)
+    ap.add_argument("--model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl"])
+    ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
+    ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--grad-ckpt", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N bench.py ...")
+        raise SystemExit(f"--gpus {args.gpus} does not match WORLD_SIZE {world}")
+
+    from nanosandbox_amd.config import TRAIN_DEFAULTS
+    from nanosandbox_amd.train import Trainer
+
+    dims = {"gpt2": (12, 12, 768), "gpt2-medium": (24, 16, 1024), "gpt2-large": (36, 20, 1280),
+            "gpt2-xl": (48, 25, 1600)}[args.model]
+    tokens_per_micro = args.micro_batch * args.block_size
+    # keep nanoGPT's 491,520 tokens/step even when the micro-batch is changed
+    total_micro = GLOBAL_MICRO_STEPS * 12 // args.micro_batch
+    assert total_micro % world == 0, "global micro-steps must divide over the ranks"
+    cfg = dict(TRAIN_DEFAULTS)
+    cfg.update(dataset="synthetic", batch_size=args.micro_batch, block_size=args.block_size,
+               gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
+               dropout=0.0, bias=False, compile=False, device="cuda", dtype="bfloat16", backend="nccl",
+               ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
+               out_dir="/tmp/nsa_bench_out", metrics_jsonl=False, learning_rate=6e-4, warmup_iters=0,
+               decay_lr=False)
+
+    with contextlib.redirect_stdout(sys.stderr):
+        tr = Trainer(cfg)
+        for g in tr.optimizer.param_groups:
+            g["lr"] = cfg["learning_rate"]
+        X, Y = tr.batches.get_batch("train")
+        for _ in range(args.warmup):
+            loss, _, X, Y = tr.train_step(X, Y)
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss, _, X, Y = tr.train_step(X, Y)
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        dt_t = torch.tensor([dt], device=tr.device, dtype=torch.float64)
+        if dist.is_initialized():
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        dt = float(dt_t.item())
+        lossf = float(loss.item()) * tr.gas
+
+    tokens_per_step = tokens_per_micro * tr.gas * world
+    value = tokens_per_step * args.steps / dt
+    ms = dt / args.steps * 1000.0
+    flops_per_token = tr.raw_model.flops_per_token(args.block_size)
+    mfu = value * flops_per_token / (world * 2.5e15)
+    if tr.info.rank == 0:
+        print(json.dumps({
+            "metric": METRIC if args.model == "gpt2" else f"tokens/sec (whole node) {args.model} DDP",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random tokens, vocab 50304); random-init weights",
+            "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,
+                       "global_batch": tokens_per_step // args.block_size, "seq_len": args.block_size,
+                       "tokens_per_step": tokens_per_step, "micro_batch": args.micro_batch,
+                       "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
+                       "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb},
+            "mfu_vs_2.5PF": round(mfu, 4),
+            "loss": round(lossf, 4),
+        }), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernel library.
+//
+// Conventions used by every kernel in this directory:
+//  * bf16 tensors are stored as raw 16-bit words (bf16_t) and moved in 16-byte
+//    vectors (8 elements per lane) — hipcc does not vectorise scalar bf16 loads
+//    (cdna_hip_programming.md Guideline 13);
+//  * math is fp32; f32 -> bf16 uses the compiler cast, which lowers to
+//    v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN-preserving);
+//  * waves are 64 lanes; block sizes are multiples of 64;
+//  * every launch takes the caller's hipStream_t and returns hipError_t.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define NSA_API extern "C" __attribute__((visibility("default")))
+
+#define NSA_LAUNCH_CHECK() \
+  do {                     \
+    return hipGetLastError(); \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// 8 x bf16 in one 16-byte vector
+struct __attribute__((aligned(16))) bf16v8 {
+  bf16_t v[8];
+};
+
+__device__ __forceinline__ void load8(const bf16_t* p, float (&f)[8]) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  f[0] = __uint_as_float(u.x << 16);
+  f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16);
+  f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16);
+  f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16);
+  f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ void store8(bf16_t* p, const float (&f)[8]) {
+  uint4 u;
+  u.x = pack2(f[0], f[1]);
+  u.y = pack2(f[2], f[3]);
+  u.z = pack2(f[4], f[5]);
+  u.w = pack2(f[6], f[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based dropout RNG: keep(seed, i) is a pure function of (seed, index),
+// so backward regenerates the forward mask without storing it.
+__device__ __forceinline__ uint32_t nsa_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+__device__ __forceinline__ bool nsa_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return nsa_hash(seed, idx) >= thresh;
+}
+
+static inline uint32_t nsa_drop_thresh(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) return 0xffffffffu;
+  if (t <= 0.0) return 0u;
+  return (uint32_t)t;
+}

@@ -1,0 +1,128 @@
+// Memory-bound elementwise kernels: exact-erf GELU fwd/bwd, hash dropout,
+// fp32 -> bf16 cast.  16-byte vector access per lane (8 bf16), grid capped at
+// 256 CUs x 8 blocks and grid-strided (cdna_hip_programming.md Guideline 11).
+//
+// nanoGPT MLP uses nn.GELU() — the exact erf form, not the tanh approximation
+// (SURVEY.md §2.3 U-M3, K4).
+#include "common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t n_vec) {
+  int64_t g = (n_vec + kBlock - 1) / kBlock;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
+  return cdf + x * pdf;
+}
+
+__global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         int64_t n) {
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+    store8(y + i * 8, f);
+  }
+  // scalar tail
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    y[i] = f2bf(gelu_f(bf2f(x[i])));
+}
+
+__global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                         bf16_t* __restrict__ dx, int64_t n) {
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    float g[8], f[8];
+    load8(dy + i * 8, g);
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = g[j] * gelu_grad(f[j]);
+    store8(dx + i * 8, f);
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    dx[i] = f2bf(bf2f(dy[i]) * gelu_grad(bf2f(x[i])));
+}
+
+__global__ __launch_bounds__(kBlock) void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                        int64_t n, uint32_t thresh, float scale, uint64_t seed) {
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = nsa_keep(seed, (uint64_t)(i * 8 + j), thresh) ? f[j] * scale : 0.0f;
+    store8(y + i * 8, f);
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    y[i] = f2bf(nsa_keep(seed, (uint64_t)i, thresh) ? bf2f(x[i]) * scale : 0.0f);
+}
+
+__global__ __launch_bounds__(kBlock) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                              int64_t n) {
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    const float4 a = reinterpret_cast<const float4*>(x)[2 * i];
+    const float4 b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    store8(y + i * 8, f);
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    y[i] = f2bf(x[i]);
+}
+
+// y[i] *= s[0]  (bf16 tensor scaled by a device scalar; no host sync)
+__global__ __launch_bounds__(kBlock) void scale_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                           const float* __restrict__ s, int64_t n) {
+  const float sc = s[0];
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= sc;
+    store8(y + i * 8, f);
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    y[i] = f2bf(bf2f(x[i]) * sc);
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
+  gelu_fwd_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
+  gelu_bwd_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t s) {
+  const float scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
+  dropout_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, nsa_drop_thresh(p), scale,
+                                                    seed);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_cast_f32_bf16(const void* x, void* y, int64_t n, hipStream_t s) {
+  cast_f32_bf16_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const float*)x, (bf16_t*)y, n);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_scale_rows_bf16(const void* x, void* y, const void* scale, int64_t n, hipStream_t s) {
+  scale_bf16_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, (const float*)scale, n);
+  NSA_LAUNCH_CHECK();
+}

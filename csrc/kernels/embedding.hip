@@ -1,0 +1,133 @@
+// Token + position embedding forward/backward (SURVEY.md §2.7 K11/K12;
+// nanoGPT: x = drop(wte(idx) + wpe(arange(T)))).
+//
+// forward : one wave per token row; 16-byte gathers of the wte row and the wpe
+//           row, fp32 add, optional hash dropout, bf16 store.
+// backward: dwte — the tied wte/lm_head gradient lives in the fp32 flat
+//           gradient buffer; each wave stages its token's dx row in LDS and
+//           issues fp32 atomics so that every wave-instruction covers 256
+//           contiguous bytes (the full-rate atomic shape, MI355X_MICROARCH.md
+//           "Global float atomics").  B*T*C*4 bytes of atomics per micro-step
+//           (38 MB for GPT-2 124M) ≈ 30 us at the ~1.3 TB/s chip atomic rate.
+//           dwpe — owned per (t, column-octet): the thread sums over the batch
+//           and read-modify-writes the flat buffer, no atomics.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx, const bf16_t* __restrict__ wte,
+                                                     const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int N,
+                                                     int T, int C, uint32_t thresh, float scale, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int t = row % T;
+  const int64_t tok = idx[row];
+  const bf16_t* a = wte + tok * C;
+  const bf16_t* p = wpe + (int64_t)t * C;
+  bf16_t* o = out + (int64_t)row * C;
+  for (int c = lane * 8; c < C; c += 512) {
+    float fa[8], fp[8];
+    load8(a + c, fa);
+    load8(p + c, fp);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fa[j] + fp[j];
+      if (thresh) v = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? v * scale : 0.0f;
+      fa[j] = v;
+    }
+    store8(o + c, fa);
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restrict__ idx,
+                                                         const bf16_t* __restrict__ dx, float* __restrict__ dwte, int N,
+                                                         int C, uint32_t thresh, float scale, uint64_t seed) {
+  extern __shared__ __attribute__((aligned(16))) float stage[];  // [4][C]
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  float* srow = stage + wv * C;
+  for (int row = blockIdx.x * 4 + wv; row < N; row += gridDim.x * 4) {
+    const bf16_t* d = dx + (int64_t)row * C;
+    for (int c = lane * 8; c < C; c += 512) {
+      float f[8];
+      load8(d + c, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = f[j];
+        if (thresh) v = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? v * scale : 0.0f;
+        srow[c + j] = v;
+      }
+    }
+    // wave-private LDS row: order the row's writes before the cross-lane reads
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    float* g = dwte + idx[row] * C;
+    for (int c = lane; c < C; c += 64) atomicAdd(g + c, srow[c]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const bf16_t* __restrict__ dx, float* __restrict__ dwpe,
+                                                         int B, int T, int C, uint32_t thresh, float scale,
+                                                         uint64_t seed) {
+  const int octs = C / 8;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= T * octs) return;
+  const int t = i / octs;
+  const int c = (i % octs) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b = 0; b < B; ++b) {
+    const int64_t row = (int64_t)b * T + t;
+    float f[8];
+    load8(dx + row * C + c, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j];
+      if (thresh) v = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? v * scale : 0.0f;
+      acc[j] += v;
+    }
+  }
+  float4* g = reinterpret_cast<float4*>(dwpe + (int64_t)t * C + c);
+  float4 g0 = g[0], g1 = g[1];
+  g0.x += acc[0];
+  g0.y += acc[1];
+  g0.z += acc[2];
+  g0.w += acc[3];
+  g1.x += acc[4];
+  g1.y += acc[5];
+  g1.z += acc[6];
+  g1.w += acc[7];
+  g[0] = g0;
+  g[1] = g1;
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_embedding_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
+                                     int C, float p, uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  emb_fwd_kernel<<<(N + 3) / 4, 256, 0, s>>>((const int64_t*)idx, (const bf16_t*)wte, (const bf16_t*)wpe,
+                                             (bf16_t*)out, N, T, C, th, scale, seed);
+  return hipGetLastError();
+}
+
+NSA_API hipError_t nsa_embedding_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T, int C,
+                                     float p, uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int N = B * T;
+  int grid = (N + 3) / 4;
+  if (grid > 2048) grid = 2048;
+  emb_bwd_wte_kernel<<<grid, 256, 4 * C * sizeof(float), s>>>((const int64_t*)idx, (const bf16_t*)dx,
+                                                               (float*)dwte, N, C, th, scale, seed);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int work = T * (C / 8);
+  emb_bwd_wpe_kernel<<<(work + 255) / 256, 256, 0, s>>>((const bf16_t*)dx, (float*)dwpe, B, T, C, th, scale, seed);
+  return hipGetLastError();
+}

@@ -1,0 +1,622 @@
+// Causal flash attention forward + backward for gfx950.
+//
+// nanoGPT's CausalSelfAttention calls
+//   F.scaled_dot_product_attention(q, k, v, dropout_p, is_causal=True)
+// on q,k,v split out of the packed c_attn output.  Our kernels read the packed
+// activation qkv[B, T, 3C] (q | k | v, head h at columns h*D) directly and write
+// y[B, T, C] / dqkv[B, T, 3C] directly, so there are no transposes or splits
+// around the kernel at all.
+//
+// Matrix work is v_mfma_f32_32x32x16_bf16 on 64-lane waves.  Layout choices
+// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"):
+//
+// forward, per wave = 32 queries, per KV tile = 64 keys (2 sub-blocks of 32):
+//   S^T[key][q] = K · Q^T         A = K   (LDS, ds_read_b128), B = Q^T (registers)
+//     -> the query is the MFMA column = the lane: running max / sum / rescale
+//        are lane-local (+ one xor-32 exchange), no LDS round trip.
+//   O^T[d][q] += V^T · P^T        A = V^T (LDS, ds_read_b64_tr_b16 transposed
+//        read of the row-major V tile), B = P^T straight from the S^T
+//        accumulator registers (bf16-converted, permuted k order).
+// backward, per wave = 32 keys (workgroup = 128 keys), loop over 64-query blocks:
+//   S = Q·K^T, dP = dO·V^T        key on the lane; K, V fragments live in registers
+//   dV^T += dO^T · P,  dK^T += Q^T · dS      accumulators as B operands, A by tr reads
+//   dQ   += dS · K                dS crosses LDS once (as dS^T), fp32 atomics whose
+//        wave-instructions are two 128-B row segments (full atomic rate).
+//
+// LDS images are XOR-swizzled per 16-byte chunk with a bit-reversed row key:
+//   phys_chunk = chunk ^ bitrev((row / rows_per_bank_row) mod chunks_per_row)
+// which is conflict-free both for the 16-row ds_read_b128 groups and for the
+// 4-row x 4-chunk blocks of ds_read_b64_tr_b16 (checked for D = 32, 64, 128).
+//
+// Softmax uses exp2 with log2(e)/sqrt(D) folded into one multiplier; the LSE
+// (natural log) is saved per query for the backward recompute of P.
+// Dropout (char config, p = 0.2) uses the counter-based hash of common.h on
+// (b*H+h, q, k), so the backward regenerates the mask.
+#include "common.h"
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+struct Geo {
+  static constexpr int CPR = D / 8;                         // 16-byte chunks per row
+  static constexpr int RPB = CPR >= 16 ? 1 : 16 / CPR;      // rows per 256-byte bank row
+  static constexpr int BITS = CPR == 4 ? 2 : CPR == 8 ? 3 : 4;
+};
+
+template <int BITS>
+__device__ __forceinline__ int bitrev(int k) {
+  if constexpr (BITS == 2) return ((k & 1) << 1) | ((k >> 1) & 1);
+  else if constexpr (BITS == 3) return ((k & 1) << 2) | (k & 2) | ((k >> 2) & 1);
+  else return (int)(__builtin_bitreverse32((uint32_t)k) >> 28);
+}
+
+// byte offset of (row, chunk) inside a swizzled [rows][D] bf16 tile
+template <int D>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  using G = Geo<D>;
+  const int key = bitrev<G::BITS>((row / G::RPB) & (G::CPR - 1));
+  return row * (D * 2) + ((chunk ^ key) << 4);
+}
+
+__device__ __forceinline__ uint4 lds_b128(const char* base, int off) {
+  return *reinterpret_cast<const uint4*>(base + off);
+}
+
+__device__ __forceinline__ s16x4 lds_tr(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + off));
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 a, s16x4 b) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 as_frag(uint4 u) { return __builtin_bit_cast(bf16x8, u); }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// accumulator register i of a 32x32 tile holds row (i&3) + 8*(i>>2) + 4*h
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Transposed-read address for an MFMA operand whose 8 elements are 4+4 consecutive
+// rows of a row-major tile:  first read rows r0+0..3, second read rows r1+0..3;
+// the lane's column is col_base + (lane & 31) where col_base is this 32-column tile.
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int r1, int col_base, int lane) {
+  const int g = lane >> 4, ig = lane & 15;
+  const int q = ig >> 2, p = ig & 3;
+  const int col = col_base + 16 * (g & 1) + 4 * p;
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  const s16x4 a = lds_tr(tile, swz<D>(r0 + q, chunk) + half * 8);
+  const s16x4 b = lds_tr(tile, swz<D>(r1 + q, chunk) + half * 8);
+  return cat_tr(a, b);
+}
+
+// tr-read fragment for a tile with a different row width W (elements) than D
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag_w(const char* tile, int r0, int r1, int col_base, int lane) {
+  return tr_frag<W>(tile, r0, r1, col_base, lane);
+}
+
+// =============================================================================
+// forward
+// =============================================================================
+template <int D>
+__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                          float* __restrict__ lse_out, int B, int T, int H,
+                                                          float scale_log2, uint32_t drop_thresh, float drop_scale,
+                                                          uint64_t seed) {
+  constexpr int BN = 64;
+  constexpr int TILE_BYTES = BN * D * 2;
+  constexpr int CPR = D / 8;
+  constexpr int CHUNKS_PER_THREAD = BN * CPR / 256;  // 16-byte chunks of one K (or V) tile per thread
+  constexpr int NKS = D / 16;                       // k-steps over the head dim
+  constexpr int NDT = D / 32;                       // 32-wide output tiles over the head dim
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K[2], V[2]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 127) / 128;
+  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int q0 = qt * 128;
+  const int q0w = q0 + 32 * w;
+  const int qpos = q0w + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+  const bf16_t* vbase = base + 2 * C + hh * D;
+
+  // Q^T fragments (B operand): lane holds Q[qpos][16ks + 8h .. +8]
+  bf16x8 qf[NKS];
+  {
+    const int qc = qpos < T ? qpos : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
+  }
+
+  f32x16 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
+  float m_i = -1e30f, l_i = 0.0f;
+
+  const int kv_end = min(T, q0 + 128);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+
+  uint4 kst[CHUNKS_PER_THREAD], vst[CHUNKS_PER_THREAD];
+  auto stage_load = [&](int j) {
+#pragma unroll
+    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
+      const int e = tid + 256 * c;
+      const int row = e / CPR, ch = e % CPR;
+      int key = j * BN + row;
+      key = key < T ? key : T - 1;
+      kst[c] = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);
+      vst[c] = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * row_stride + ch * 8);
+    }
+  };
+  auto stage_write = [&](int buf) {
+    char* kt = smem + buf * TILE_BYTES;
+    char* vt = smem + (2 + buf) * TILE_BYTES;
+#pragma unroll
+    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
+      const int e = tid + 256 * c;
+      const int row = e / CPR, ch = e % CPR;
+      *reinterpret_cast<uint4*>(kt + swz<D>(row, ch)) = kst[c];
+      *reinterpret_cast<uint4*>(vt + swz<D>(row, ch)) = vst[c];
+    }
+  };
+
+  stage_load(0);
+  stage_write(0);
+  __syncthreads();
+
+  for (int j = 0; j < n_tiles; ++j) {
+    const int cur = j & 1;
+    const int kv0 = j * BN;
+    if (j + 1 < n_tiles) stage_load(j + 1);
+    if (kv0 <= q0w + 31) {  // wave-uniform: tile has at least one visible key for this wave
+      const char* kt = smem + cur * TILE_BYTES;
+      const char* vt = smem + (2 + cur) * TILE_BYTES;
+      f32x16 st[2];
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        st[sb] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
+          st[sb] = mfma(kf, qf[ks], st[sb]);
+        }
+      }
+      // causal mask + tile max
+      const bool diag = kv0 + BN - 1 > q0w;
+      float mt = -1e30f;
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float s = st[sb][i];
+          if (diag) {
+            const int kpos = kv0 + 32 * sb + acc_row(i, h);
+            if (kpos > qpos) s = -INFINITY;
+          }
+          st[sb][i] = s;
+          mt = fmaxf(mt, s);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_i, mt);
+      const float alpha = fast_exp2((m_i - m_new) * scale_log2);
+      const float mc = m_new * scale_log2;
+      float rs = 0.0f;
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(st[sb][i] * scale_log2 - mc);
+          rs += p;
+          float pv = p;
+          if (drop_thresh) {
+            const int kpos = kv0 + 32 * sb + acc_row(i, h);
+            const uint64_t id = ((uint64_t)bh * T + (uint64_t)qpos) * (uint64_t)T + (uint64_t)kpos;
+            pv = nsa_keep(seed, id, drop_thresh) ? p * drop_scale : 0.0f;
+          }
+          pf[sb][i >> 3][i & 7] = (__bf16)pv;
+        }
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l_i = l_i * alpha + rs;
+      m_i = m_new;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
+      // O^T += V^T · P^T
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
+            o[dt] = mfma(vf, pf[sb][s], o[dt]);
+          }
+        }
+      }
+    }
+    if (j + 1 < n_tiles) stage_write(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: O = O^T / l ; lane owns query qpos, registers hold d
+  if (qpos < T) {
+    const float inv_l = 1.0f / l_i;
+    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = pack2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
+        u.y = pack2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
+        *reinterpret_cast<uint2*>(orow + d) = u;
+      }
+    }
+    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
+  }
+}
+
+// =============================================================================
+// backward preprocessing: delta = rowsum(dO * O)   ([B, H, T] fp32)
+// =============================================================================
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+                                                           float* __restrict__ delta, int B, int T, int H) {
+  constexpr int LPR = D / 8;  // lanes per (b, t, h) row
+  const int C = H * D;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / LPR;  // row = (b*T + t)*H + h
+  const int sub = gid % LPR;
+  if (row >= (int64_t)B * T * H) return;
+  const int hh = row % H;
+  const int64_t bt = row / H;
+  const int t = bt % T, b = bt / T;
+  float a[8], g[8];
+  load8(o + bt * C + hh * D + sub * 8, a);
+  load8(dout + bt * C + hh * D + sub * 8, g);
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += a[j] * g[j];
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (sub == 0) delta[((int64_t)b * H + hh) * T + t] = s;
+}
+
+// =============================================================================
+// backward main kernel: one workgroup = 128 keys (4 waves x 32) of one (b, h)
+// =============================================================================
+template <int D>
+__global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B,
+                                                          int T, int H, float scale, float scale_log2,
+                                                          uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+  constexpr int QB = 64;                    // queries per block iteration
+  constexpr int KB = 128;                   // keys per workgroup
+  constexpr int CPR = D / 8;
+  constexpr int NKS = D / 16;
+  constexpr int NDT = D / 32;
+  constexpr int QT_BYTES = QB * D * 2;      // one Q (or dO) tile
+  constexpr int K_BYTES = KB * D * 2;       // workgroup's K tile (for dQ)
+  constexpr int DS_BYTES = KB * QB * 2;     // dS^T [128 keys][64 q]
+  constexpr int QCH = QB * CPR / 256;       // 16-byte chunks per thread per Q (or dO) tile
+  constexpr int KCH = KB * CPR / 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * QT_BYTES + K_BYTES + DS_BYTES + 4 * QB * 4];
+  char* const qs_lds = smem;                            // Q[2]
+  char* const do_lds = smem + 2 * QT_BYTES;             // dO[2]
+  char* const k_lds = smem + 4 * QT_BYTES;              // K (workgroup keys)
+  char* const ds_lds = k_lds + K_BYTES;                 // dS^T
+  float* const ld_lds = reinterpret_cast<float*>(ds_lds + DS_BYTES);  // lse2[2][QB], delta[2][QB]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int kb = blockIdx.x / BH;  // key blocks near 0 see the most queries: launched first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int k0 = kb * KB;
+  const int kw0 = k0 + 32 * w;
+  const int kpos = kw0 + r;  // this lane's key (S / dP / dK / dV column)
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+  const bf16_t* vbase = base + 2 * C + hh * D;
+  const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
+  const float* lse_bh = lse + (int64_t)bh * T;
+  const float* delta_bh = delta + (int64_t)bh * T;
+
+  // K^T / V^T fragments for S = Q·K^T and dP = dO·V^T (B operands): K[kpos][16ks+8h..]
+  bf16x8 kf[NKS], vf[NKS];
+  {
+    const int kc = kpos < T ? kpos : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      kf[ks] = as_frag(*reinterpret_cast<const uint4*>(kbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+      vf[ks] = as_frag(*reinterpret_cast<const uint4*>(vbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+    }
+  }
+  // workgroup K tile -> LDS (B operand of dQ = dS·K by transposed reads)
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const int e = tid + 256 * c;
+    const int row = e / CPR, ch = e % CPR;
+    int key = k0 + row;
+    key = key < T ? key : T - 1;
+    *reinterpret_cast<uint4*>(k_lds + swz<D>(row, ch)) =
+        *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);
+  }
+
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    dk[dt] = f32x16{};
+    dv[dt] = f32x16{};
+  }
+
+  const int qb_first = k0 / QB;
+  const int n_qb = (T + QB - 1) / QB;
+
+  uint4 qst[QCH], dost[QCH];
+  float lst = 0.0f, dst = 0.0f;
+  auto stage_load = [&](int qb) {
+#pragma unroll
+    for (int c = 0; c < QCH; ++c) {
+      const int e = tid + 256 * c;
+      const int row = e / CPR, ch = e % CPR;
+      int q = qb * QB + row;
+      q = q < T ? q : T - 1;
+      qst[c] = *reinterpret_cast<const uint4*>(qbase + (int64_t)q * row_stride + ch * 8);
+      dost[c] = *reinterpret_cast<const uint4*>(dobase + (int64_t)q * C + ch * 8);
+    }
+    if (tid < QB) {
+      int q = qb * QB + tid;
+      q = q < T ? q : T - 1;
+      lst = lse_bh[q] * kLog2e;
+      dst = delta_bh[q];
+    }
+  };
+  auto stage_write = [&](int buf) {
+    char* qt = qs_lds + buf * QT_BYTES;
+    char* dt_ = do_lds + buf * QT_BYTES;
+#pragma unroll
+    for (int c = 0; c < QCH; ++c) {
+      const int e = tid + 256 * c;
+      const int row = e / CPR, ch = e % CPR;
+      *reinterpret_cast<uint4*>(qt + swz<D>(row, ch)) = qst[c];
+      *reinterpret_cast<uint4*>(dt_ + swz<D>(row, ch)) = dost[c];
+    }
+    if (tid < QB) {
+      ld_lds[buf * QB + tid] = lst;
+      ld_lds[2 * QB + buf * QB + tid] = dst;
+    }
+  };
+
+  stage_load(qb_first);
+  stage_write(0);
+  __syncthreads();
+
+  // dQ tiles of the 64 x D output per q-block: (q-half, d-tile) pairs spread over the 4 waves
+  constexpr int NTILES = 2 * NDT;
+  constexpr int TPW = NTILES >= 4 ? NTILES / 4 : 1;
+
+  for (int qb = qb_first; qb < n_qb; ++qb) {
+    const int cur = (qb - qb_first) & 1;
+    const char* qt = qs_lds + cur * QT_BYTES;
+    const char* dot = do_lds + cur * QT_BYTES;
+    const float* lse2_s = ld_lds + cur * QB;
+    const float* delta_s = ld_lds + 2 * QB + cur * QB;
+    if (qb + 1 < n_qb) stage_load(qb + 1);
+
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qbase_pos = qb * QB + qs * 32;
+      // S = Q · K^T  (rows = queries in registers, column = this lane's key)
+      f32x16 sacc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 qa = as_frag(lds_b128(qt, swz<D>(qs * 32 + r, 2 * ks + h)));
+        sacc = mfma(qa, kf[ks], sacc);
+      }
+      f32x16 dpacc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 da = as_frag(lds_b128(dot, swz<D>(qs * 32 + r, 2 * ks + h)));
+        dpacc = mfma(da, vf[ks], dpacc);
+      }
+      bf16x8 pfr[2], dsfr[2];
+      float dsv[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *reinterpret_cast<const float4*>(lse2_s + qs * 32 + 8 * g + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qs * 32 + 8 * g + 4 * h);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dlv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          const int q = qbase_pos + 8 * g + 4 * h + e;
+          float p = fast_exp2(sacc[i] * scale_log2 - lv[e]);
+          if (kpos > q || q >= T) p = 0.0f;
+          float dp = dpacc[i];
+          float pd = p;
+          if (drop_thresh) {
+            const uint64_t id = ((uint64_t)bh * T + (uint64_t)q) * (uint64_t)T + (uint64_t)kpos;
+            const bool keep = nsa_keep(seed, id, drop_thresh);
+            pd = keep ? p * drop_scale : 0.0f;
+            dp = keep ? dp * drop_scale : 0.0f;
+          }
+          const float ds = p * (dp - dlv[e]);
+          dsv[i] = ds;
+          pfr[i >> 3][i & 7] = (__bf16)pd;
+          dsfr[i >> 3][i & 7] = (__bf16)ds;
+        }
+      }
+      // dV^T += dO^T · P  and  dK^T += Q^T · dS   (accumulators as B operands)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = qs * 32 + 16 * s + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const bf16x8 doa = tr_frag<D>(dot, r0, r0 + 8, 32 * dt, lane);
+          dv[dt] = mfma(doa, pfr[s], dv[dt]);
+          const bf16x8 qa = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);
+          dk[dt] = mfma(qa, dsfr[s], dk[dt]);
+        }
+      }
+      // dS^T -> LDS: row = key (32w + r), columns = q (qs*32 + 8g + 4h + 0..3)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qcol = qs * 32 + 8 * g + 4 * h;
+        uint2 u;
+        u.x = pack2(dsv[4 * g + 0], dsv[4 * g + 1]);
+        u.y = pack2(dsv[4 * g + 2], dsv[4 * g + 3]);
+        *reinterpret_cast<uint2*>(ds_lds + swz<QB>(32 * w + r, qcol >> 3) + ((qcol >> 2) & 1) * 8) = u;
+      }
+    }
+    __syncthreads();
+    // stage the next Q/dO tile now: buffer cur^1 was last read before the previous
+    // barrier, and doing it before the dQ atomics keeps their vmcnt out of its wait
+    if (qb + 1 < n_qb) stage_write(cur ^ 1);
+
+    // dQ[64 x D] += dS[64 x 128] · K[128 x D]  (scaled), fp32 atomics
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tile = w + 4 * t;
+      if (tile < NTILES) {
+        const int qh = tile & 1, dt = tile >> 1;
+        f32x16 dqa = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KB / 16; ++ks) {
+          const int kr = 16 * ks + 8 * h;
+          const bf16x8 a = tr_frag<QB>(ds_lds, kr, kr + 4, qh * 32, lane);
+          const bf16x8 bk = tr_frag<D>(k_lds, kr, kr + 4, 32 * dt, lane);
+          dqa = mfma(a, bk, dqa);
+        }
+        float* dqrow = dq_acc + (int64_t)b * T * C + hh * D + 32 * dt + r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = qb * QB + qh * 32 + acc_row(i, h);
+          if (q < T) atomicAdd(dqrow + (int64_t)q * C, dqa[i] * scale);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: dK = scale * dK^T^T, dV = dV^T^T  -> dqkv[:, :, C + ...] and [2C + ...]
+  if (kpos < T) {
+    bf16_t* krow = dqkv + ((int64_t)b * T + kpos) * row_stride + C + hh * D;
+    bf16_t* vrow = krow + C;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 uk, uv;
+        uk.x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+        uk.y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        uv.x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+        uv.y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(krow + d) = uk;
+        *reinterpret_cast<uint2*>(vrow + d) = uv;
+      }
+    }
+  }
+}
+
+// dq_acc (fp32 [B, T, C]) -> dqkv[:, :, 0:C] (bf16)
+__global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv,
+                                                        int64_t rows, int C) {
+  const int octs = C / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * octs) return;
+  const int64_t row = i / octs;
+  const int c = (int)(i % octs) * 8;
+  const float4 a = *reinterpret_cast<const float4*>(dq + row * C + c);
+  const float4 bq = *reinterpret_cast<const float4*>(dq + row * C + c + 4);
+  const float f[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
+  store8(dqkv + row * 3 * C + c, f);
+}
+
+template <int D>
+hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H, float scale, float p,
+                      uint64_t seed, hipStream_t s) {
+  const int n_qt = (T + 127) / 128;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  flash_fwd_kernel<D><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+                                                   scale * kLog2e, th, dscale, seed);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const void* lse, void* delta, void* dq_acc,
+                      void* dqkv, int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
+  const int64_t rows = (int64_t)B * T * H;
+  const int64_t threads = rows * (D / 8);
+  flash_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)dout,
+                                                                            (float*)delta, B, T, H);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int n_kb = (T + 127) / 128;
+  flash_bwd_kernel<D><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse,
+                                                   (const float*)delta, (float*)dq_acc, (bf16_t*)dqkv, B, T, H, scale,
+                                                   scale * kLog2e, th, dscale, seed);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int C = H * D;
+  const int64_t work = (int64_t)B * T * (C / 8);
+  dq_convert_kernel<<<(unsigned)((work + 255) / 256), 256, 0, s>>>((const float*)dq_acc, (bf16_t*)dqkv,
+                                                                   (int64_t)B * T, C);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
+                                 float p, uint64_t seed, hipStream_t s) {
+  switch (D) {
+    case 32: return fwd_launch<32>(qkv, out, lse, B, T, H, scale, p, seed, s);
+    case 64: return fwd_launch<64>(qkv, out, lse, B, T, H, scale, p, seed, s);
+    case 128: return fwd_launch<128>(qkv, out, lse, B, T, H, scale, p, seed, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+NSA_API hipError_t nsa_flash_bwd(const void* qkv, const void* o, const void* dout, const void* lse, void* delta,
+                                 void* dq_acc, void* dqkv, int B, int T, int H, int D, float scale, float p,
+                                 uint64_t seed, hipStream_t s) {
+  switch (D) {
+    case 32: return bwd_launch<32>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
+    case 64: return bwd_launch<64>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
+    case 128: return bwd_launch<128>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
+    default: return hipErrorInvalidValue;
+  }
+}

@@ -1,0 +1,149 @@
+// Fused flat AdamW + global gradient-norm clipping.
+//
+// One optimizer step over ALL parameters is three launches, independent of
+// the tensor count (torch's multi-tensor path chunks per tensor list):
+//   nsa_sumsq_partial : per-block sum of squares of the flat fp32 grad
+//   nsa_clip_coef     : one block -> global norm + combined grad multiplier
+//   nsa_adamw_step    : one HBM-bound pass, 16 B/lane vectors:
+//                       reads p,g,m,v (16 B/elt), writes p,m,v (12 B) + bf16 p (2 B)
+// Everything stays on the device (no host sync), so the step is capturable.
+//
+// Math = torch.optim.AdamW (decoupled weight decay):
+//   p *= 1 - lr*wd ; m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+//   p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+// where g = grad * coef and coef = grad_scale * min(1, max_norm/(norm+1e-6)).
+#include "common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      bf16_t* __restrict__ pb, const uint8_t* __restrict__ wd_mask,
+                                                      int64_t n4, float lr, float b1, float b2, float eps, float wd,
+                                                      float step_size, float inv_bc2_sqrt,
+                                                      const float* __restrict__ coef_ptr) {
+  const float coef = coef_ptr[0];
+  const float decay = 1.0f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    const float d = wd_mask[(i * 4) >> 6] ? decay : 1.0f;  // 64-element chunks never straddle params
+    float* pa = &pp.x;
+    const float* ga = &gg.x;
+    float* ma = &mm.x;
+    float* va = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = ga[j] * coef;
+      ma[j] = b1 * ma[j] + (1.0f - b1) * gj;
+      va[j] = b2 * va[j] + (1.0f - b2) * gj * gj;
+      const float denom = sqrtf(va[j]) * inv_bc2_sqrt + eps;
+      pa[j] = pa[j] * d - step_size * ma[j] / denom;
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (pb) {
+      uint2 o;
+      o.x = pack2(pp.x, pp.y);
+      o.y = pack2(pp.z, pp.w);
+      reinterpret_cast<uint2*>(pb)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void sumsq_partial_kernel(const float* __restrict__ g, int64_t n4,
+                                                              float* __restrict__ partial) {
+  float acc = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
+    const float4 x = reinterpret_cast<const float4*>(g)[i];
+    acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  acc = wave_sum(acc);
+  __shared__ float red[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+    partial[blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict__ partial, int nparts, float scale,
+                                                        float max_norm, float* __restrict__ norm_out,
+                                                        float* __restrict__ coef_out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 1024) acc += (double)partial[i];
+  __shared__ double red[1024];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(red[0]) * scale;
+    norm_out[0] = norm;
+    float c = 1.0f;
+    if (max_norm > 0.0f) {
+      c = max_norm / (norm + 1e-6f);
+      if (c > 1.0f) c = 1.0f;
+    }
+    coef_out[0] = scale * c;
+  }
+}
+
+// out[c] += sum_r partial[r][c]   (LayerNorm dW/db second-stage reduction)
+__global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict__ partial, float* __restrict__ out,
+                                                       int rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float acc = 0.0f;
+  if (c < C) {
+    for (int r = w; r < rows; r += 4) acc += partial[(int64_t)r * C + c];
+  }
+  __shared__ float red[4][64];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < C) out[c] += red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_adamw_step(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask,
+                                  int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,
+                                  float bc2_sqrt, const void* coef, hipStream_t s) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  int64_t grid = (n4 + kBlock - 1) / kBlock;
+  if (grid > 4096) grid = 4096;
+  adamw_kernel<<<(int)grid, kBlock, 0, s>>>((float*)p, (const float*)g, (float*)m, (float*)v, (bf16_t*)p_bf16,
+                                            (const uint8_t*)wd_mask, n4, lr, beta1, beta2, eps, wd, lr / bc1,
+                                            1.0f / bc2_sqrt, (const float*)coef);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_sumsq_partial(const void* g, int64_t n, void* partial, int nblocks, hipStream_t s) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  sumsq_partial_kernel<<<nblocks, kBlock, 0, s>>>((const float*)g, n / 4, (float*)partial);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_clip_coef(const void* partial, int nparts, float scale, float max_norm, void* norm_out,
+                                 void* coef_out, hipStream_t s) {
+  clip_coef_kernel<<<1, 1024, 0, s>>>((const float*)partial, nparts, scale, max_norm, (float*)norm_out,
+                                      (float*)coef_out);
+  NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_colsum_accum(const void* partial, void* out, int rows, int C, hipStream_t s) {
+  colsum_kernel<<<(C + 63) / 64, kBlock, 0, s>>>((const float*)partial, (float*)out, rows, C);
+  NSA_LAUNCH_CHECK();
+}

@@ -1,0 +1,108 @@
+// Fused cross-entropy forward + logits-gradient.
+//
+// nanoGPT: F.cross_entropy(logits.view(-1, V), targets.view(-1), ignore_index=-1)
+// over logits [N, V] (V = 50304 for GPT-2: 1.2 GB of bf16 logits per 124M
+// micro-step).  One 256-thread block per row:
+//   pass 1: online (max, sum-exp) over the row with 16-byte loads,
+//           block-combined through LDS;
+//   pass 2: re-read the row (L2/Infinity-Cache resident) and overwrite it IN
+//           PLACE with softmax - onehot(target) in bf16 (the unnormalised
+//           dL/dlogits; the 1/n_valid * grad_out factor is applied later on the
+//           small [N, C] side of the lm_head GEMMs).
+// row_loss[r] = logsumexp - logit[target] (0 for ignored rows, whose gradient
+// row is zeroed).  The [N, V] fp32 softmax never exists.
+#include "common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  if (m2 > m) {
+    s = s * __expf(m - m2) + s2;
+    m = m2;
+  } else {
+    s = s + s2 * __expf(m2 - m);
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
+                                                     float* __restrict__ row_loss, int V, int write_grad) {
+  const int row = blockIdx.x;
+  bf16_t* lr = logits + (int64_t)row * V;
+  const int64_t tgt = targets[row];
+  float m = -INFINITY, s = 0.0f;
+  if (VEC) {
+    const int nv = V / 8;
+    for (int i = threadIdx.x; i < nv; i += kBlock) {
+      float f[8];
+      load8(lr + i * 8, f);
+      float bm = f[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) bm = fmaxf(bm, f[j]);
+      float bs = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bs += __expf(f[j] - bm);
+      online_merge(m, s, bm, bs);
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += kBlock) online_merge(m, s, bf2f(lr[i]), 1.0f);
+  }
+  // wave reduce of (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const float s2 = __shfl_xor(s, o, 64);
+    if (m2 != -INFINITY) online_merge(m, s, m2, s2);
+  }
+  __shared__ float sm[kBlock / 64], ss[kBlock / 64];
+  __shared__ float tgt_logit;
+  if ((threadIdx.x & 63) == 0) {
+    sm[threadIdx.x >> 6] = m;
+    ss[threadIdx.x >> 6] = s;
+  }
+  if (threadIdx.x == 0) tgt_logit = (tgt >= 0 && tgt < V) ? bf2f(lr[tgt]) : 0.0f;
+  __syncthreads();
+  float M = sm[0], S = ss[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) online_merge(M, S, sm[w], ss[w]);
+  const float lse = M + __logf(S);
+  const bool valid = tgt >= 0 && tgt < V;
+  if (threadIdx.x == 0) row_loss[row] = valid ? lse - tgt_logit : 0.0f;
+  if (!write_grad) return;
+  const float invS = 1.0f / S;
+  if (VEC) {
+    const int nv = V / 8;
+    for (int i = threadIdx.x; i < nv; i += kBlock) {
+      float f[8];
+      load8(lr + i * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = i * 8 + j;
+        float p = valid ? __expf(f[j] - M) * invS : 0.0f;
+        if (valid && col == tgt) p -= 1.0f;
+        f[j] = p;
+      }
+      store8(lr + i * 8, f);
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += kBlock) {
+      float p = valid ? __expf(bf2f(lr[i]) - M) * invS : 0.0f;
+      if (valid && i == tgt) p -= 1.0f;
+      lr[i] = f2bf(p);
+    }
+  }
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int write_grad,
+                                hipStream_t s) {
+  if (V % 8 == 0)
+    xent_kernel<true><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
+  else
+    xent_kernel<false><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V,
+                                            write_grad);
+  return hipGetLastError();
+}

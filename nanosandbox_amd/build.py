@@ -1,0 +1,112 @@
+"""Build the native libraries in-tree (no JIT cache, so they travel with the repo).
+
+* ``lib/libnsa_kernels.so`` — every ``csrc/kernels/*.hip`` compiled by
+  ``hipcc --offload-arch=gfx950 -O3`` (CDNA4 only; no CUDA / multi-arch paths)
+* ``lib/libnsa_runtime.so`` — the C++ host runtime (``csrc/runtime/*.cpp``:
+  prefetching data loader), built with g++
+
+Usage: ``python -m nanosandbox_amd.build [--force] [--jobs N]``.
+Objects are rebuilt only when a source or header is newer than the library.
+"""
+
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+LIB_DIR = os.path.join(ROOT, "nanosandbox_amd", "lib")
+BUILD_DIR = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("NSA_OFFLOAD_ARCH", "gfx950")
+
+KERNEL_LIB = os.path.join(LIB_DIR, "libnsa_kernels.so")
+RUNTIME_LIB = os.path.join(LIB_DIR, "libnsa_runtime.so")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise FileNotFoundError("hipcc not found (ROCm 7.x expected under /opt/rocm)")
+
+
+def _newer(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_kernels(force=False, jobs=8, verbose=True):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    if not force and not _newer(KERNEL_LIB, srcs + headers):
+        return KERNEL_LIB
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+             "-munsafe-fp-atomics", "-I", os.path.join(CSRC, "kernels")]
+
+    def compile_one(src):
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        if force or _newer(obj, [src] + headers):
+            _run([hipcc, *flags, "-c", src, "-o", obj])
+            if verbose:
+                print(f"  [hipcc {ARCH}] {os.path.relpath(src, ROOT)}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = KERNEL_LIB + ".tmp"
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
+    os.replace(tmp, KERNEL_LIB)
+    if verbose:
+        print(f"built {os.path.relpath(KERNEL_LIB, ROOT)}")
+    return KERNEL_LIB
+
+
+def build_runtime(force=False, verbose=True):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    if not srcs:
+        return None
+    if not force and not _newer(RUNTIME_LIB, srcs):
+        return RUNTIME_LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    tmp = RUNTIME_LIB + ".tmp"
+    _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *srcs, "-o", tmp])
+    os.replace(tmp, RUNTIME_LIB)
+    if verbose:
+        print(f"built {os.path.relpath(RUNTIME_LIB, ROOT)}")
+    return RUNTIME_LIB
+
+
+def build_all(force=False, jobs=8, verbose=True):
+    build_runtime(force=force, verbose=verbose)
+    return build_kernels(force=force, jobs=jobs, verbose=verbose)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args(argv)
+    build_all(force=a.force, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,305 @@
+"""GPT-2 family model with nanoGPT's module names, init and API.
+
+Behavioural contract: SURVEY.md §2.3 rows U-M1..U-M11 (upstream nanoGPT
+``model.py``, executed by reference ``notebooks/colab_nanoGPT_companion.ipynb:39,70``).
+State-dict keys, weight tying (``transformer.wte.weight is lm_head.weight``),
+init (N(0, 0.02), zero biases, ``*c_proj.weight`` at 0.02/sqrt(2·n_layer)),
+``configure_optimizers``/``estimate_mfu``/``generate``/``crop_block_size``/
+``from_pretrained`` all follow that contract so nanoGPT checkpoints load.
+
+What differs is the execution: ``nn.Linear``/``nn.Embedding`` are used only
+as parameter containers; ``forward`` runs our fused ops
+(``nanosandbox_amd.ops``): HIP LayerNorm / GELU / flash attention / embedding
+/ fused lm_head+cross-entropy kernels on gfx950, residual adds folded into
+the projection GEMMs, and weight gradients accumulated in fp32 straight into
+the flat gradient buffer.
+"""
+
+from __future__ import annotations
+
+import inspect
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+from torch.utils.checkpoint import checkpoint
+
+from .. import ops
+
+# MI355X dense bf16 peak (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA ~2.5 PF dense").
+MI355X_BF16_PEAK_FLOPS = 2.5e15
+
+
+@dataclass
+class GPTConfig:
+    block_size: int = 1024
+    vocab_size: int = 50304  # GPT-2 vocab_size of 50257, padded up to nearest multiple of 64 for efficiency
+    n_layer: int = 12
+    n_head: int = 12
+    n_embd: int = 768
+    dropout: float = 0.0
+    bias: bool = True  # True: bias in Linears and LayerNorms, like GPT-2. False: a bit better and faster
+
+
+class LayerNorm(nn.Module):
+    """LayerNorm with an optional bias (PyTorch's lacks ``bias=False`` in old versions)."""
+
+    def __init__(self, ndim, bias):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(ndim))
+        self.bias = nn.Parameter(torch.zeros(ndim)) if bias else None
+
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        assert config.n_embd % config.n_head == 0
+        # key, query, value projections for all heads, packed: [q | k | v]
+        self.c_attn = nn.Linear(config.n_embd, 3 * config.n_embd, bias=config.bias)
+        # output projection
+        self.c_proj = nn.Linear(config.n_embd, config.n_embd, bias=config.bias)
+        self.n_head = config.n_head
+        self.n_embd = config.n_embd
+        self.dropout = config.dropout
+        self.flash = True  # always: our flash kernel (gfx950) / fp32 reference on CPU
+
+    def forward(self, x, residual=None):
+        """Returns ``residual + c_proj(attn(x))`` (residual folded into the GEMM when no dropout)."""
+        qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)
+        y = ops.attention(qkv, self.n_head, self.dropout, self.training)
+        if self.training and self.dropout > 0:
+            y = ops.dropout(ops.linear(y, self.c_proj.weight, self.c_proj.bias), self.dropout, True)
+            return y if residual is None else residual + y
+        return ops.linear(y, self.c_proj.weight, self.c_proj.bias, residual=residual)
+
+
+class MLP(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.c_fc = nn.Linear(config.n_embd, 4 * config.n_embd, bias=config.bias)
+        self.c_proj = nn.Linear(4 * config.n_embd, config.n_embd, bias=config.bias)
+        self.dropout = config.dropout
+
+    def forward(self, x, residual=None):
+        h = ops.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias))
+        if self.training and self.dropout > 0:
+            y = ops.dropout(ops.linear(h, self.c_proj.weight, self.c_proj.bias), self.dropout, True)
+            return y if residual is None else residual + y
+        return ops.linear(h, self.c_proj.weight, self.c_proj.bias, residual=residual)
+
+
+class Block(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.ln_1 = LayerNorm(config.n_embd, bias=config.bias)
+        self.attn = CausalSelfAttention(config)
+        self.ln_2 = LayerNorm(config.n_embd, bias=config.bias)
+        self.mlp = MLP(config)
+
+    def forward(self, x):
+        x = self.attn(self.ln_1(x), residual=x)
+        x = self.mlp(self.ln_2(x), residual=x)
+        return x
+
+
+class GPT(nn.Module):
+    def __init__(self, config: GPTConfig):
+        super().__init__()
+        assert config.vocab_size is not None
+        assert config.block_size is not None
+        self.config = config
+        self.grad_ckpt = False
+        self.compute_dtype = torch.float32
+
+        self.transformer = nn.ModuleDict(dict(
+            wte=nn.Embedding(config.vocab_size, config.n_embd),
+            wpe=nn.Embedding(config.block_size, config.n_embd),
+            drop=nn.Dropout(config.dropout),
+            h=nn.ModuleList([Block(config) for _ in range(config.n_layer)]),
+            ln_f=LayerNorm(config.n_embd, bias=config.bias),
+        ))
+        self.lm_head = nn.Linear(config.n_embd, config.vocab_size, bias=False)
+        # weight tying (https://paperswithcode.com/method/weight-tying)
+        self.transformer.wte.weight = self.lm_head.weight
+
+        # init all weights
+        self.apply(self._init_weights)
+        # apply special scaled init to the residual projections, per GPT-2 paper
+        for pn, p in self.named_parameters():
+            if pn.endswith("c_proj.weight"):
+                torch.nn.init.normal_(p, mean=0.0, std=0.02 / math.sqrt(2 * config.n_layer))
+
+    # ------------------------------------------------------------------ utils
+    def get_num_params(self, non_embedding=True):
+        """Parameter count; position embeddings are subtracted by default (token
+        embeddings stay, since they are tied to the lm_head)."""
+        n_params = sum(p.numel() for p in self.parameters())
+        if non_embedding:
+            n_params -= self.transformer.wpe.weight.numel()
+        return n_params
+
+    def _init_weights(self, module):
+        if isinstance(module, nn.Linear):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02)
+            if module.bias is not None:
+                torch.nn.init.zeros_(module.bias)
+        elif isinstance(module, nn.Embedding):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02)
+
+    def set_compute_dtype(self, dtype: torch.dtype):
+        """Activation dtype of the forward pass (bf16 on MI355X, fp32 on CPU)."""
+        self.compute_dtype = dtype
+        return self
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, idx, targets=None):
+        b, t = idx.size()
+        assert t <= self.config.block_size, \
+            f"Cannot forward sequence of length {t}, block size is only {self.config.block_size}"
+        tr = self.transformer
+        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, self.config.dropout, self.training,
+                          dtype=self.compute_dtype)
+        for block in tr.h:
+            if self.grad_ckpt and self.training and torch.is_grad_enabled():
+                x = checkpoint(block, x, use_reentrant=False)
+            else:
+                x = block(x)
+        x = tr.ln_f(x)
+
+        if targets is not None:
+            loss = ops.lm_head_loss(x, self.lm_head.weight, targets)
+            logits = None  # the [B,T,V] logits are consumed in place by the fused CE kernel
+        else:
+            # inference-time mini-optimization: only forward the lm_head on the very last position
+            logits = ops.lm_head_logits(x[:, [-1], :], self.lm_head.weight)
+            loss = None
+        return logits, loss
+
+    def forward_logits(self, idx):
+        """Full [B, T, V] fp32 logits (evaluation / tests)."""
+        tr = self.transformer
+        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.compute_dtype)
+        for block in tr.h:
+            x = block(x)
+        x = tr.ln_f(x)
+        return ops.lm_head_logits(x, self.lm_head.weight)
+
+    # ------------------------------------------------------------ surgery/api
+    def crop_block_size(self, block_size):
+        """Model surgery to decrease the block size if necessary (e.g. load gpt2 at 1024, use 256)."""
+        assert block_size <= self.config.block_size
+        self.config.block_size = block_size
+        self.transformer.wpe.weight = nn.Parameter(self.transformer.wpe.weight[:block_size].detach().clone())
+        for block in self.transformer.h:
+            if hasattr(block.attn, "bias"):
+                block.attn.bias = block.attn.bias[:, :, :block_size, :block_size]
+
+    @classmethod
+    def from_pretrained(cls, model_type, override_args=None):
+        """Load OpenAI GPT-2 weights from a local HuggingFace snapshot (no network here)."""
+        from ..utils.hf import load_hf_gpt2_state_dict
+        assert model_type in {"gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl"}
+        override_args = override_args or {}
+        assert all(k == "dropout" for k in override_args)
+        config_args = {
+            "gpt2": dict(n_layer=12, n_head=12, n_embd=768),  # 124M params
+            "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),  # 350M params
+            "gpt2-large": dict(n_layer=36, n_head=20, n_embd=1280),  # 774M params
+            "gpt2-xl": dict(n_layer=48, n_head=25, n_embd=1600),  # 1558M params
+        }[model_type]
+        print(f"loading weights from pretrained gpt: {model_type}")
+        config_args["vocab_size"] = 50257
+        config_args["block_size"] = 1024
+        config_args["bias"] = True
+        if "dropout" in override_args:
+            print(f"overriding dropout rate to {override_args['dropout']}")
+            config_args["dropout"] = override_args["dropout"]
+        model = GPT(GPTConfig(**config_args))
+        sd = model.state_dict()
+        sd_hf = load_hf_gpt2_state_dict(model_type)
+        transposed = ["attn.c_attn.weight", "attn.c_proj.weight", "mlp.c_fc.weight", "mlp.c_proj.weight"]
+        keys_hf = [k for k in sd_hf if not k.endswith(".attn.masked_bias") and not k.endswith(".attn.bias")]
+        keys = [k for k in sd if not k.endswith(".attn.bias")]
+        assert len(keys_hf) == len(keys), f"mismatched keys: {len(keys_hf)} != {len(keys)}"
+        with torch.no_grad():
+            for k in keys_hf:
+                if any(k.endswith(w) for w in transposed):
+                    # HF uses Conv1D modules: [in, out] weights
+                    assert sd_hf[k].shape[::-1] == sd[k].shape
+                    sd[k].copy_(sd_hf[k].t())
+                else:
+                    assert sd_hf[k].shape == sd[k].shape
+                    sd[k].copy_(sd_hf[k])
+        return model
+
+    def optimizer_groups(self, weight_decay):
+        """nanoGPT grouping: every >=2D tensor decays, biases/LayerNorms do not."""
+        param_dict = {pn: p for pn, p in self.named_parameters() if p.requires_grad}
+        decay_params = [p for n, p in param_dict.items() if p.dim() >= 2]
+        nodecay_params = [p for n, p in param_dict.items() if p.dim() < 2]
+        return [
+            {"params": decay_params, "weight_decay": weight_decay},
+            {"params": nodecay_params, "weight_decay": 0.0},
+        ]
+
+    def configure_optimizers(self, weight_decay, learning_rate, betas, device_type, store=None):
+        """Two AdamW groups; on MI355X the optimizer is our fused flat HIP AdamW.
+
+        With ``store`` (a ``FlatParamStore``) the fused flat optimizer is
+        returned; without it a torch AdamW (``fused=True`` on GPU when available)
+        is built, exactly like nanoGPT.
+        """
+        optim_groups = self.optimizer_groups(weight_decay)
+        num_decay_params = sum(p.numel() for p in optim_groups[0]["params"])
+        num_nodecay_params = sum(p.numel() for p in optim_groups[1]["params"])
+        print(f"num decayed parameter tensors: {len(optim_groups[0]['params'])}, "
+              f"with {num_decay_params:,} parameters")
+        print(f"num non-decayed parameter tensors: {len(optim_groups[1]['params'])}, "
+              f"with {num_nodecay_params:,} parameters")
+        if store is not None:
+            from ..optim.fused_adamw import FusedAdamW
+            optimizer = FusedAdamW(store, optim_groups, lr=learning_rate, betas=betas)
+            print(f"using fused AdamW: True (flat HIP kernel, {store.numel:,} elements)")
+            return optimizer
+        fused_available = "fused" in inspect.signature(torch.optim.AdamW).parameters
+        use_fused = fused_available and device_type == "cuda"
+        extra_args = dict(fused=True) if use_fused else dict()
+        optimizer = torch.optim.AdamW(optim_groups, lr=learning_rate, betas=betas, **extra_args)
+        print(f"using fused AdamW: {use_fused}")
+        return optimizer
+
+    def flops_per_token(self, seq_len=None):
+        """nanoGPT's PaLM-appendix estimate: 6N + 12·L·H·Q·T (fwd+bwd)."""
+        N = self.get_num_params()
+        cfg = self.config
+        L, H, Q, T = cfg.n_layer, cfg.n_head, cfg.n_embd // cfg.n_head, seq_len or cfg.block_size
+        return 6 * N + 12 * L * H * Q * T
+
+    def estimate_mfu(self, fwdbwd_per_iter, dt, peak_flops=MI355X_BF16_PEAK_FLOPS):
+        """Model flops utilization in units of MI355X bf16 dense peak (not A100's 312 TF)."""
+        T = self.config.block_size
+        flops_per_fwdbwd = self.flops_per_token() * T
+        flops_per_iter = flops_per_fwdbwd * fwdbwd_per_iter
+        flops_achieved = flops_per_iter * (1.0 / dt)  # per second
+        return flops_achieved / peak_flops
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens, temperature=1.0, top_k=None):
+        """Autoregressive sampling: crop context, last-token logits / temperature,
+        optional top-k, softmax, multinomial, append."""
+        for _ in range(max_new_tokens):
+            # if the sequence context is growing too long we must crop it at block_size
+            idx_cond = idx if idx.size(1) <= self.config.block_size else idx[:, -self.config.block_size:]
+            logits, _ = self(idx_cond)
+            logits = logits[:, -1, :] / temperature
+            if top_k is not None:
+                v, _ = torch.topk(logits, min(top_k, logits.size(-1)))
+                logits[logits < v[:, [-1]]] = -float("Inf")
+            probs = torch.softmax(logits, dim=-1)
+            idx_next = torch.multinomial(probs, num_samples=1)
+            idx = torch.cat((idx, idx_next), dim=1)
+        return idx

@@ -1,0 +1,13 @@
+"""Fused GPT ops: HIP kernels on gfx950, fp32 torch reference on CPU."""
+
+from .functional import (  # noqa: F401
+    attention,
+    compute_weight,
+    dropout,
+    embedding,
+    gelu,
+    layer_norm,
+    linear,
+    lm_head_logits,
+    lm_head_loss,
+)

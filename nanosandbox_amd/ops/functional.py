@@ -1,0 +1,516 @@
+"""Autograd functions for every op of the GPT hot path.
+
+Each op has exactly one GPU implementation — our gfx950 HIP kernels from
+``libnsa_kernels.so`` (GEMMs go to hipBLASLt through ``torch.mm``/``addmm``)
+— and a CPU implementation in plain fp32 torch that doubles as the numerics
+reference for the kernel tests.  The choice is by tensor device, not a
+backend switch.
+
+Op inventory (nanoGPT ``model.py`` call sites):
+
+=========  ==========================================  =========================
+op         computes                                     nanoGPT site
+=========  ==========================================  =========================
+K11/K12    ``drop(wte[idx] + wpe[t])``                 ``GPT.forward``
+K3         LayerNorm, eps 1e-5, optional bias           ``LayerNorm.forward``
+K5-K9      ``residual + x @ W^T + b``                   ``nn.Linear`` (+ residual add)
+K4         exact-erf GELU                               ``MLP.forward``
+K1/K2      causal flash attention (+dropout)            ``CausalSelfAttention``
+K8+K10     tied lm_head + fused cross-entropy           ``GPT.forward`` loss
+=========  ==========================================  =========================
+
+Gradient accumulation is fused: if a parameter carries ``main_grad`` (a view
+into the flat fp32 gradient buffer owned by ``optim.flat.FlatParamStore``),
+weight gradients are accumulated straight into it — for Linear weights inside
+the GEMM itself (``addmm`` with an fp32 output, beta=1) — and the parameter's
+``_nsa_grad_hook`` is called so the bucketed reducer can launch an all-reduce
+as soon as a bucket is complete.  Without ``main_grad`` the gradient is
+returned to autograd normally (plain ``.grad`` semantics, used by torch DDP
+and the gradcheck tests).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+# ----------------------------------------------------------------------------
+# helpers
+# ----------------------------------------------------------------------------
+
+def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """The tensor used for compute: the bf16 shadow kept by the optimizer if present."""
+    c = getattr(p, "compute", None)
+    if c is not None and c.dtype == dtype:
+        return c
+    p = p.detach()
+    return p if p.dtype == dtype else p.to(dtype)
+
+
+def notify_grad_ready(p: torch.Tensor) -> None:
+    hook = getattr(p, "_nsa_grad_hook", None)
+    if hook is not None:
+        hook(p)
+
+
+def _accumulate(p: torch.Tensor, g: torch.Tensor):
+    """Add ``g`` (fp32) into ``p.main_grad`` if fused accumulation is on; else return it."""
+    mg = getattr(p, "main_grad", None)
+    if mg is None:
+        return g.to(p.dtype).view_as(p)
+    mg.add_(g.view_as(mg))
+    notify_grad_ready(p)
+    return None
+
+
+_ADDMM_INPLACE_OK = None
+
+
+def _addmm_f32_inplace_supported() -> bool:
+    """Probe once whether hipBLASLt accepts ``addmm(C, A_bf16, B_bf16, out_dtype=f32, out=C)``."""
+    global _ADDMM_INPLACE_OK
+    if _ADDMM_INPLACE_OK is None:
+        try:
+            a = torch.randn(40, 24, device="cuda", dtype=BF16)
+            b = torch.randn(24, 56, device="cuda", dtype=BF16)
+            c = torch.randn(40, 56, device="cuda", dtype=F32)
+            ref = c + a.float() @ b.float()
+            torch.addmm(c, a, b, out_dtype=F32, out=c)
+            _ADDMM_INPLACE_OK = bool(torch.allclose(c, ref, atol=1e-1, rtol=1e-2))
+        except Exception:  # pragma: no cover - depends on the ROCm build
+            _ADDMM_INPLACE_OK = False
+    return _ADDMM_INPLACE_OK
+
+
+def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
+    """dW = dy2^T @ x2 accumulated in fp32 (into ``p.main_grad`` when present)."""
+    mg = getattr(p, "main_grad", None)
+    if dy2.is_cuda and dy2.dtype == BF16:
+        if mg is not None:
+            if _addmm_f32_inplace_supported():
+                torch.addmm(mg, dy2.t(), x2, out_dtype=F32, out=mg)
+            else:
+                mg.add_(torch.mm(dy2.t(), x2, out_dtype=F32))
+            notify_grad_ready(p)
+            return None
+        return torch.mm(dy2.t(), x2, out_dtype=F32).to(p.dtype)
+    g = dy2.t().float() @ x2.float()
+    return _accumulate(p, g)
+
+
+def new_seed() -> int:
+    # drawn from torch's CPU generator so activation checkpointing (which
+    # restores RNG state on recompute) replays the same dropout masks
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+# ----------------------------------------------------------------------------
+# dropout (hash-based on GPU: the mask is regenerated in backward, never stored)
+# ----------------------------------------------------------------------------
+
+def _cpu_keep_mask(shape, p, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g) >= p
+
+
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        seed = new_seed()
+        ctx.p, ctx.seed = p, seed
+        if x.is_cuda:
+            y = torch.empty_like(x)
+            _lib.call("nsa_dropout", _lib.ptr(x.contiguous()), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
+            return y
+        mask = _cpu_keep_mask(x.shape, p, seed)
+        return x * mask / (1.0 - p)
+
+    @staticmethod
+    def backward(ctx, dy):
+        if dy.is_cuda:
+            dx = torch.empty_like(dy)
+            _lib.call("nsa_dropout", _lib.ptr(dy.contiguous()), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
+                      _lib.stream())
+            return dx, None
+        mask = _cpu_keep_mask(dy.shape, ctx.p, ctx.seed)
+        return dy * mask / (1.0 - ctx.p), None
+
+
+def dropout(x, p: float, training: bool):
+    if not training or p == 0.0:
+        return x
+    return DropoutFn.apply(x, p)
+
+
+# ----------------------------------------------------------------------------
+# embedding: x = drop(wte[idx] + wpe[arange(T)])
+# ----------------------------------------------------------------------------
+
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe, p, dtype):
+        B, T = idx.shape
+        V, C = wte.shape
+        seed = new_seed() if p > 0 else 0
+        ctx.p, ctx.seed, ctx.shape = p, seed, (B, T, V, C)
+        ctx.save_for_backward(idx, wte, wpe)
+        if idx.is_cuda:
+            assert C % 8 == 0, "embedding kernel needs n_embd % 8 == 0"
+            idx = idx.contiguous()
+            out = torch.empty(B, T, C, device=idx.device, dtype=dtype)
+            _lib.call("nsa_embedding_fwd", _lib.ptr(idx), _lib.ptr(compute_weight(wte, dtype)),
+                      _lib.ptr(compute_weight(wpe, dtype)), _lib.ptr(out), B * T, T, C, p, seed, _lib.stream())
+            return out
+        x = wte.detach()[idx] + wpe.detach()[:T].unsqueeze(0)
+        if p > 0:
+            x = x * _cpu_keep_mask(x.shape, p, seed) / (1.0 - p)
+        return x.to(dtype)
+
+    @staticmethod
+    def backward(ctx, dx):
+        idx, wte, wpe = ctx.saved_tensors
+        B, T, V, C = ctx.shape
+        if dx.is_cuda:
+            dx = dx.contiguous()
+            gwte = getattr(wte, "main_grad", None)
+            gwpe = getattr(wpe, "main_grad", None)
+            ret_wte = gwte is None
+            ret_wpe = gwpe is None
+            if ret_wte:
+                gwte = torch.zeros(V, C, device=dx.device, dtype=F32)
+            if ret_wpe:
+                gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
+            _lib.call("nsa_embedding_bwd", _lib.ptr(idx), _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe),
+                      B, T, C, ctx.p, ctx.seed, _lib.stream())
+            out_wte = gwte.to(wte.dtype) if ret_wte else None
+            out_wpe = gwpe.to(wpe.dtype) if ret_wpe else None
+            if not ret_wte:
+                notify_grad_ready(wte)
+            if not ret_wpe:
+                notify_grad_ready(wpe)
+            return None, out_wte, out_wpe, None, None
+        d = dx.float()
+        if ctx.p > 0:
+            d = d * _cpu_keep_mask(d.shape, ctx.p, ctx.seed) / (1.0 - ctx.p)
+        gwte = torch.zeros(V, C, dtype=F32)
+        gwte.index_add_(0, idx.reshape(-1), d.reshape(-1, C))
+        gwpe = torch.zeros(wpe.shape[0], C, dtype=F32)
+        gwpe[:T] = d.sum(0)
+        return None, _accumulate(wte, gwte), _accumulate(wpe, gwpe), None, None
+
+
+def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32):
+    return EmbeddingFn.apply(idx, wte, wpe, p if training else 0.0, dtype)
+
+
+# ----------------------------------------------------------------------------
+# LayerNorm (eps 1e-5, optional bias)
+# ----------------------------------------------------------------------------
+
+LN_EPS = 1e-5
+_LN_BWD_BLOCKS = 512
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        N = x2.shape[0]
+        ctx.has_bias = b is not None
+        if x.is_cuda:
+            assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
+            x2 = x2.contiguous()
+            y = torch.empty_like(x2)
+            mean = torch.empty(N, device=x.device, dtype=F32)
+            rstd = torch.empty(N, device=x.device, dtype=F32)
+            wc = compute_weight(w, x.dtype)
+            bc = compute_weight(b, x.dtype) if b is not None else None
+            _lib.call("nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y),
+                      _lib.ptr(mean), _lib.ptr(rstd), N, C, LN_EPS, _lib.stream())
+        else:
+            xf = x2.float()
+            mean = xf.mean(-1)
+            var = xf.var(-1, unbiased=False)
+            rstd = torch.rsqrt(var + LN_EPS)
+            y = (xf - mean[:, None]) * rstd[:, None] * w.detach().float()
+            if b is not None:
+                y = y + b.detach().float()
+            y = y.to(x.dtype)
+        ctx.save_for_backward(x2, w, b if b is not None else mean, mean, rstd)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
+        b = b_or_mean if ctx.has_bias else None
+        C = x2.shape[-1]
+        N = x2.shape[0]
+        dy2 = dy.reshape(-1, C)
+        if dy.is_cuda:
+            dy2 = dy2.contiguous()
+            dx = torch.empty_like(x2)
+            nblk = min(_LN_BWD_BLOCKS, max(1, (N + 3) // 4))
+            dw_part = torch.empty(nblk, C, device=dy.device, dtype=F32)
+            db_part = torch.empty(nblk, C, device=dy.device, dtype=F32) if b is not None else None
+            _lib.call("nsa_layernorm_bwd", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(compute_weight(w, x2.dtype)),
+                      _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(dx), _lib.ptr(dw_part), _lib.ptr(db_part),
+                      N, C, nblk, _lib.stream())
+            gw = _colsum_into(w, dw_part)
+            gb = _colsum_into(b, db_part) if b is not None else None
+            return dx.view(dy.shape), gw, gb
+        xf = x2.float()
+        d = dy2.float()
+        xhat = (xf - mean[:, None]) * rstd[:, None]
+        wf = w.detach().float()
+        dxhat = d * wf
+        dx = rstd[:, None] * (dxhat - dxhat.mean(-1, keepdim=True) - xhat * (dxhat * xhat).mean(-1, keepdim=True))
+        gw = _accumulate(w, (d * xhat).sum(0))
+        gb = _accumulate(b, d.sum(0)) if b is not None else None
+        return dx.to(dy.dtype).view(dy.shape), gw, gb
+
+
+def _colsum_into(p, partial):
+    """Reduce per-block partial column sums into p.main_grad (fused) or a fresh fp32 grad."""
+    mg = getattr(p, "main_grad", None)
+    rows, C = partial.shape
+    if mg is not None:
+        _lib.call("nsa_colsum_accum", _lib.ptr(partial), _lib.ptr(mg), rows, C, _lib.stream())
+        notify_grad_ready(p)
+        return None
+    out = torch.zeros(C, device=partial.device, dtype=F32)
+    _lib.call("nsa_colsum_accum", _lib.ptr(partial), _lib.ptr(out), rows, C, _lib.stream())
+    return out.to(p.dtype)
+
+
+def layer_norm(x, w, b):
+    return LayerNormFn.apply(x, w, b)
+
+
+# ----------------------------------------------------------------------------
+# Linear: out = residual + x @ W^T + b     (GEMM on hipBLASLt, fp32 dW fused)
+# ----------------------------------------------------------------------------
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual):
+        K = x.shape[-1]
+        Nout = w.shape[0]
+        x2 = x.reshape(-1, K)
+        wc = compute_weight(w, x.dtype)
+        bc = compute_weight(b, x.dtype) if b is not None else None
+        if residual is not None:
+            r2 = residual.reshape(-1, Nout)
+            base = r2 if bc is None else r2 + bc
+            out = torch.addmm(base, x2, wc.t())
+        elif bc is not None:
+            out = torch.addmm(bc, x2, wc.t())
+        else:
+            out = x2 @ wc.t()
+        ctx.has_bias = b is not None
+        ctx.has_residual = residual is not None
+        ctx.save_for_backward(x2, w, b if b is not None else w)
+        return out.view(*x.shape[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, w, b = ctx.saved_tensors
+        Nout = w.shape[0]
+        d2 = dout.reshape(-1, Nout)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (d2 @ compute_weight(w, d2.dtype)).view(*dout.shape[:-1], x2.shape[-1])
+        gw = weight_grad(w, d2, x2)
+        gb = None
+        if ctx.has_bias:
+            gb = _accumulate(b, d2.sum(0, dtype=F32))
+        dres = dout if ctx.has_residual else None
+        return dx, gw, gb, dres
+
+
+def linear(x, w, b=None, residual=None):
+    return LinearFn.apply(x, w, b, residual)
+
+
+# ----------------------------------------------------------------------------
+# GELU (exact erf, nn.GELU() default)
+# ----------------------------------------------------------------------------
+
+_INV_SQRT2 = 1.0 / math.sqrt(2.0)
+_INV_SQRT2PI = 1.0 / math.sqrt(2.0 * math.pi)
+
+
+class GeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        if x.is_cuda:
+            x = x.contiguous()
+            y = torch.empty_like(x)
+            _lib.call("nsa_gelu_fwd", _lib.ptr(x), _lib.ptr(y), x.numel(), _lib.stream())
+            return y
+        return F.gelu(x.float()).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        if dy.is_cuda:
+            dy = dy.contiguous()
+            dx = torch.empty_like(x)
+            _lib.call("nsa_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dx), x.numel(), _lib.stream())
+            return dx
+        xf = x.float()
+        cdf = 0.5 * (1.0 + torch.erf(xf * _INV_SQRT2))
+        pdf = torch.exp(-0.5 * xf * xf) * _INV_SQRT2PI
+        return (dy.float() * (cdf + xf * pdf)).to(dy.dtype)
+
+
+def gelu(x):
+    return GeluFn.apply(x)
+
+
+# ----------------------------------------------------------------------------
+# causal self-attention on the packed qkv activation [B, T, 3C]
+# ----------------------------------------------------------------------------
+
+def _attn_reference(q, k, v, p, seed):
+    """fp32 causal attention with a reproducible dropout mask. q,k,v: [B,H,T,D]."""
+    T, D = q.shape[-2], q.shape[-1]
+    att = (q @ k.transpose(-2, -1)) * (1.0 / math.sqrt(D))
+    mask = torch.ones(T, T, dtype=torch.bool, device=q.device).tril()
+    att = att.masked_fill(~mask, float("-inf"))
+    att = torch.softmax(att, dim=-1)
+    if p > 0:
+        att = att * _cpu_keep_mask(att.shape, p, seed).to(att.device) / (1.0 - p)
+    return att @ v
+
+
+class AttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_head, p):
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        H = n_head
+        D = C // H
+        seed = new_seed() if p > 0 else 0
+        ctx.meta = (B, T, H, D, p, seed)
+        scale = 1.0 / math.sqrt(D)
+        if qkv.is_cuda:
+            assert D in (32, 64, 128), "flash kernel supports head_dim 32/64/128"
+            qkv = qkv.contiguous()
+            y = torch.empty(B, T, C, device=qkv.device, dtype=qkv.dtype)
+            lse = torch.empty(B, H, T, device=qkv.device, dtype=F32)
+            _lib.call("nsa_flash_fwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, D, scale, p, seed,
+                      _lib.stream())
+            ctx.save_for_backward(qkv, y, lse)
+            return y
+        q, k, v = qkv.float().view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+        y = _attn_reference(q, k, v, p, seed).transpose(1, 2).reshape(B, T, C)
+        ctx.save_for_backward(qkv)
+        return y.to(qkv.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, T, H, D, p, seed = ctx.meta
+        C = H * D
+        if dy.is_cuda:
+            qkv, y, lse = ctx.saved_tensors
+            dy = dy.contiguous()
+            dqkv = torch.empty_like(qkv)
+            delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
+            dq_acc = torch.zeros(B, T, C, device=dy.device, dtype=F32)
+            _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
+                      _lib.ptr(dq_acc), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
+            return dqkv, None, None
+        (qkv,) = ctx.saved_tensors
+        with torch.enable_grad():
+            x = qkv.detach().float().requires_grad_(True)
+            q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+            y = _attn_reference(q, k, v, p, seed).transpose(1, 2).reshape(B, T, C)
+            (g,) = torch.autograd.grad(y, x, dy.float())
+        return g.to(qkv.dtype), None, None
+
+
+def attention(qkv, n_head: int, p: float, training: bool):
+    return AttentionFn.apply(qkv, n_head, p if training else 0.0)
+
+
+# ----------------------------------------------------------------------------
+# tied lm_head + cross-entropy (ignore_index=-1, mean over valid targets)
+# ----------------------------------------------------------------------------
+
+class LMHeadLossFn(torch.autograd.Function):
+    """loss = cross_entropy(x @ wte^T, targets, ignore_index=-1).
+
+    GPU: the [N, V] bf16 logits buffer is overwritten in place by the fused
+    CE kernel with (softmax - onehot); backward applies grad/n_valid to the
+    small [N, C] side of each GEMM instead of re-scaling the [N, V] tensor.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, targets, need_grad):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        t = targets.reshape(-1)
+        N = x2.shape[0]
+        wc = compute_weight(w, x.dtype)
+        if x.is_cuda:
+            V = wc.shape[0]
+            logits = x2 @ wc.t()
+            row_loss = torch.empty(N, device=x.device, dtype=F32)
+            _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t.contiguous()), _lib.ptr(row_loss), N, V,
+                      1 if need_grad else 0, _lib.stream())
+            n_valid = (t != -1).sum().to(F32)
+            loss = row_loss.sum() / n_valid
+            ctx.save_for_backward(x2, w, logits, n_valid)
+            ctx.xshape = x.shape
+            return loss
+        logits = x2.float() @ wc.float().t()
+        logp = torch.log_softmax(logits, dim=-1)
+        valid = t != -1
+        n_valid = valid.sum().to(F32)
+        tt = t.clamp(min=0)
+        row_loss = -logp.gather(1, tt[:, None]).squeeze(1) * valid
+        loss = row_loss.sum() / n_valid
+        dlogits = logp.exp()
+        dlogits[torch.arange(N), tt] -= 1.0
+        dlogits = dlogits * valid[:, None]
+        ctx.save_for_backward(x2, w, dlogits, n_valid)
+        ctx.xshape = x.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        x2, w, dlogits, n_valid = ctx.saved_tensors
+        g = (gl.float() / n_valid)
+        wc = compute_weight(w, x2.dtype)
+        if x2.is_cuda:
+            dx = (dlogits @ wc)
+            dx.mul_(g.to(dx.dtype))
+            xs = x2 * g.to(x2.dtype)
+            gw = weight_grad(w, dlogits, xs)
+            return dx.view(ctx.xshape), gw, None, None
+        dx = (dlogits @ wc.float()) * g
+        gw = weight_grad(w, dlogits, x2.float() * g)
+        return dx.to(x2.dtype).view(ctx.xshape), gw, None, None
+
+
+def lm_head_loss(x, w, targets):
+    # grad mode is off inside Function.forward, so decide here whether the
+    # fused kernel must also write d(loss)/d(logits) into the logits buffer
+    need_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
+    return LMHeadLossFn.apply(x, w, targets, need_grad)
+
+
+def lm_head_logits(x, w):
+    """Inference-time logits for the given positions: x @ wte^T (fp32 result)."""
+    wc = compute_weight(w, x.dtype)
+    return (x @ wc.t()).float()

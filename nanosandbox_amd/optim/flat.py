@@ -1,0 +1,131 @@
+"""Flat parameter / gradient / compute-shadow storage.
+
+MI355X-first layout (288 GB HBM per GPU makes the memory cost irrelevant; the
+win is in the number and size of passes):
+
+* ``master`` — one contiguous fp32 buffer holding every parameter; the
+  ``nn.Parameter`` objects become views into it.
+* ``grad``   — one contiguous fp32 buffer; each parameter's ``main_grad`` is a
+  view.  Linear/LayerNorm/Embedding backward kernels accumulate into it
+  directly, and the DDP reducer all-reduces contiguous slices of it (buckets)
+  with zero copies.
+* ``compute`` — one contiguous bf16 buffer, the forward/backward weights
+  (``param.compute``), rewritten by the fused AdamW kernel in the same pass
+  that updates ``master`` — so no per-micro-step autocast weight casts.
+* ``wd_mask`` — one byte per 64-element chunk: 1 where weight decay applies
+  (nanoGPT rule: tensors with ``dim >= 2``).  Each parameter is padded to a
+  multiple of 64 elements so a chunk never straddles two parameters.
+
+Parameters are laid out in *reverse registration order*, which is the order
+their gradients become final during backward (ln_f, last block ... first
+block, wpe, wte — the tied wte/lm_head gradient is complete only after the
+embedding backward).  Buckets are therefore contiguous and fire in order.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+CHUNK = 64  # elements per weight-decay flag; also the per-parameter padding granule
+
+
+@dataclass
+class ParamSlot:
+    name: str
+    param: torch.nn.Parameter
+    offset: int
+    numel: int
+    padded: int
+    decay: bool
+
+
+class FlatParamStore:
+    def __init__(self, model: torch.nn.Module, device, compute_dtype=None, fused_grad=True):
+        self.device = torch.device(device)
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]  # dedups tied weights
+        self.slots: list[ParamSlot] = []
+        off = 0
+        for name, p in reversed(named):
+            n = p.numel()
+            padded = (n + CHUNK - 1) // CHUNK * CHUNK
+            self.slots.append(ParamSlot(name, p, off, n, padded, p.dim() >= 2))
+            off += padded
+        self.numel = off
+        self.master = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
+        flags = torch.zeros(off // CHUNK, dtype=torch.uint8)
+        with torch.no_grad():
+            for s in self.slots:
+                view = self.master[s.offset:s.offset + s.numel]
+                view.copy_(s.param.detach().reshape(-1).to(self.device, torch.float32))
+                s.param.data = view.view(s.param.shape)
+                if s.decay:
+                    flags[s.offset // CHUNK:(s.offset + s.padded) // CHUNK] = 1
+        self.wd_mask = flags.to(self.device)
+        self.fused_grad = fused_grad
+        for s in self.slots:
+            g = self.grad[s.offset:s.offset + s.numel].view(s.param.shape)
+            if fused_grad:
+                s.param.main_grad = g
+            else:
+                s.param.grad = g
+        self.compute_dtype = compute_dtype
+        self.compute = None
+        if compute_dtype is not None and compute_dtype != torch.float32:
+            self.compute = torch.empty(off, dtype=compute_dtype, device=self.device)
+            for s in self.slots:
+                s.param.compute = self.compute[s.offset:s.offset + s.numel].view(s.param.shape)
+            self.refresh_compute()
+
+    # ----------------------------------------------------------------- views
+    def slot_of(self, p) -> ParamSlot:
+        for s in self.slots:
+            if s.param is p:
+                return s
+        raise KeyError("parameter not in store")
+
+    def param_view(self, buf: torch.Tensor, s: ParamSlot) -> torch.Tensor:
+        return buf[s.offset:s.offset + s.numel].view(s.param.shape)
+
+    # ------------------------------------------------------------ operations
+    @torch.no_grad()
+    def refresh_compute(self):
+        """Re-derive the bf16 compute shadow from the fp32 master (after load/broadcast)."""
+        if self.compute is None:
+            return
+        if self.device.type == "cuda":
+            from ..ops import _lib
+            _lib.call("nsa_cast_f32_bf16", _lib.ptr(self.master), _lib.ptr(self.compute), self.numel,
+                      _lib.stream())
+        else:
+            self.compute.copy_(self.master)
+
+    @torch.no_grad()
+    def zero_grad(self):
+        self.grad.zero_()
+        if not self.fused_grad:
+            # torch DDP / plain autograd path: keep .grad pointing at the flat buffer
+            for s in self.slots:
+                if s.param.grad is None or s.param.grad.data_ptr() != self.param_view(self.grad, s).data_ptr():
+                    s.param.grad = self.param_view(self.grad, s)
+
+    def buckets(self, cap_bytes: int):
+        """Contiguous [start, end) element ranges of ``grad``, cut at parameter
+        boundaries once a bucket reaches ``cap_bytes`` (fp32)."""
+        out = []
+        start = 0
+        size = 0
+        members = []
+        for s in self.slots:
+            members.append(s)
+            size += s.padded * 4
+            if size >= cap_bytes:
+                out.append((start, s.offset + s.padded, members))
+                start = s.offset + s.padded
+                size = 0
+                members = []
+        if members:
+            out.append((start, self.numel, members))
+        return out

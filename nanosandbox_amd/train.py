@@ -1,0 +1,279 @@
+"""Trainer: nanoGPT's ``train.py`` contract on the MI355X-native stack.
+
+Usage (identical CLI to nanoGPT; reference
+``notebooks/colab_nanoGPT_companion.ipynb:70-79,107-116``)::
+
+    python train.py config/train_shakespeare_char.py --device=cpu --compile=False
+    torchrun --standalone --nproc_per_node=8 train.py config/train_gpt2.py --dataset=synthetic
+
+What is the same: config keys and defaults, distributed init, grad accumulation
+(divided by world size), cosine LR, eval/checkpoint cadence and rules, resume,
+stdout log lines, checkpoint layout.
+
+What is MI355X-native: parameters/grads/optimizer state in flat HBM buffers,
+bf16 compute weights maintained by the fused AdamW kernel, HIP kernels for
+every non-GEMM op, our bucketed RCCL reducer instead of torch DDP (``ddp_impl``
+keeps torch DDP selectable), evaluation through the unwrapped module (avoids
+the reference's DDP-forward-on-rank-0 hazard), JSONL +
+tfevents metrics, atomic checkpoints, opt-in auto-resume and fault injection
+for elastic restarts.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import torch
+
+from .config import TRAIN_DEFAULTS, config_keys, parse_argv
+from .data import load_meta, make_batch_source, resolve_data_dir
+from .models import GPT, GPTConfig
+from .optim import FlatParamStore
+from .parallel import FlatBucketReducer, destroy, init_distributed
+from .utils import MetricsLogger, get_lr, load_checkpoint, load_model_state, save_checkpoint
+
+
+def _compute_dtype(device_type: str, dtype: str) -> torch.dtype:
+    if device_type != "cuda":
+        return torch.float32  # nanoGPT: nullcontext on CPU -> fp32
+    if dtype in ("bfloat16", "float16"):
+        # MI355X runs bf16 and fp16 MFMA at the same rate; bf16 needs no GradScaler
+        return torch.bfloat16
+    raise NotImplementedError("GPU path computes in bf16 (MFMA); use --dtype=bfloat16")
+
+
+class Trainer:
+    def __init__(self, cfg: dict):
+        self.cfg = cfg
+        c = cfg
+        self.info = init_distributed(c["backend"], c["device"])
+        info = self.info
+        self.device = info.device
+        self.device_type = "cuda" if "cuda" in self.device else "cpu"
+        self.master = info.master_process
+        gas = c["gradient_accumulation_steps"]
+        if info.ddp:
+            assert gas % info.world_size == 0
+            gas //= info.world_size
+        self.gas = gas
+        self.tokens_per_iter = gas * info.world_size * c["batch_size"] * c["block_size"]
+        if self.master:
+            print(f"tokens per iteration will be: {self.tokens_per_iter:,}")
+            os.makedirs(c["out_dir"], exist_ok=True)
+        torch.manual_seed(c["seed"] + info.seed_offset)
+        self.compute_dtype = _compute_dtype(self.device_type, c["dtype"])
+
+        # ---------------------------------------------------------------- data
+        self.data_dir = resolve_data_dir(c["dataset"], c["data_dir"])
+        meta = load_meta(self.data_dir) if c["dataset"] != "synthetic" else None
+        meta_vocab_size = meta["vocab_size"] if meta else None
+        if meta_vocab_size is not None:
+            print(f"found vocab_size = {meta_vocab_size} (inside {self.data_dir})")
+
+        # --------------------------------------------------------------- model
+        init_from = c["init_from"]
+        ckpt_path = os.path.join(c["out_dir"], "ckpt.pt")
+        if c["auto_resume"] and os.path.exists(ckpt_path):
+            print(f"auto_resume: found {ckpt_path}")
+            init_from = "resume"
+        model_args = dict(n_layer=c["n_layer"], n_head=c["n_head"], n_embd=c["n_embd"], block_size=c["block_size"],
+                          bias=c["bias"], vocab_size=None, dropout=c["dropout"])
+        self.iter_num = 0
+        self.best_val_loss = 1e9
+        checkpoint = None
+        if init_from == "scratch":
+            print("Initializing a new model from scratch")
+            if meta_vocab_size is None:
+                print("defaulting to vocab_size of GPT-2 to 50304 (50257 rounded up for efficiency)")
+            model_args["vocab_size"] = meta_vocab_size if meta_vocab_size is not None else 50304
+            model = GPT(GPTConfig(**model_args))
+        elif init_from == "resume":
+            print(f"Resuming training from {c['out_dir']}")
+            checkpoint = load_checkpoint(ckpt_path, map_location="cpu")
+            for k in ["n_layer", "n_head", "n_embd", "block_size", "bias", "vocab_size"]:
+                model_args[k] = checkpoint["model_args"][k]
+            model = GPT(GPTConfig(**model_args))
+            load_model_state(model, checkpoint["model"])
+            self.iter_num = checkpoint["iter_num"]
+            self.best_val_loss = float(checkpoint["best_val_loss"])
+        elif init_from.startswith("gpt2"):
+            print(f"Initializing from OpenAI GPT-2 weights: {init_from}")
+            model = GPT.from_pretrained(init_from, dict(dropout=c["dropout"]))
+            for k in ["n_layer", "n_head", "n_embd", "block_size", "bias", "vocab_size"]:
+                model_args[k] = getattr(model.config, k)
+        else:
+            raise ValueError(f"unknown init_from {init_from!r}")
+        if c["block_size"] < model.config.block_size:
+            model.crop_block_size(c["block_size"])
+            model_args["block_size"] = c["block_size"]
+        self.model_args = model_args
+        model.to(self.device)
+        model.set_compute_dtype(self.compute_dtype)
+        model.grad_ckpt = c["grad_ckpt"]
+        print(f"number of parameters: {model.get_num_params() / 1e6:.2f}M")
+
+        # ------------------------------------------- flat store + fused AdamW
+        self.ddp_impl = c["ddp_impl"] if info.ddp else "none"
+        fused_grad = self.ddp_impl != "torch"
+        self.store = FlatParamStore(model, self.device,
+                                    compute_dtype=self.compute_dtype if self.device_type == "cuda" else None,
+                                    fused_grad=fused_grad)
+        self.optimizer = model.configure_optimizers(c["weight_decay"], c["learning_rate"], (c["beta1"], c["beta2"]),
+                                                    self.device_type, store=self.store)
+        if init_from == "resume" and checkpoint is not None:
+            self.optimizer.load_state_dict(checkpoint["optimizer"])
+        checkpoint = None  # free up memory
+        if c["compile"]:
+            print("compile=True: no Triton/Inductor on this stack; hot ops already run as fused HIP kernels")
+
+        # ----------------------------------------------------------------- DDP
+        self.raw_model = model
+        self.model = model
+        self.reducer = None
+        if info.ddp:
+            if self.ddp_impl == "flat":
+                rdt = torch.bfloat16 if c["grad_reduce_dtype"] == "bfloat16" else torch.float32
+                self.reducer = FlatBucketReducer(self.store, bucket_cap_mb=c["ddp_bucket_mb"], reduce_dtype=rdt)
+                self.reducer.broadcast_parameters()
+                self.optimizer.grad_scale = self.reducer.grad_scale
+                if self.master:
+                    print(f"DDP: flat bucketed reducer, {len(self.reducer.buckets)} buckets "
+                          f"(cap {c['ddp_bucket_mb']} MiB, {c['grad_reduce_dtype']})")
+            elif self.ddp_impl == "torch":
+                from torch.nn.parallel import DistributedDataParallel as DDP
+                self.model = DDP(model, device_ids=[info.local_rank] if self.device_type == "cuda" else None,
+                                 bucket_cap_mb=c["ddp_bucket_mb"])
+                self.store.refresh_compute()
+            else:
+                raise ValueError(f"unknown ddp_impl {self.ddp_impl!r}")
+
+        self.batches = make_batch_source(c["dataset"], c["data_dir"], c["block_size"], c["batch_size"], self.device,
+                                         seed=c["seed"] + info.seed_offset, vocab_size=model_args["vocab_size"])
+        run_name = c["wandb_run_name"] or "run"
+        self.metrics = MetricsLogger(c["out_dir"], jsonl=c["metrics_jsonl"], tensorboard_dir=c["tensorboard_dir"],
+                                     run_name=run_name, enabled=self.master)
+        if c["wandb_log"] and self.master:
+            print("wandb_log=True: wandb is not installed in this image; logging to metrics.jsonl/tfevents instead")
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def estimate_loss(self):
+        out = {}
+        m = self.raw_model  # never forward the DDP wrapper on one rank (SURVEY.md §2.8 hazard)
+        m.eval()
+        for split in ["train", "val"]:
+            losses = torch.zeros(self.cfg["eval_iters"], device=self.device)
+            for k in range(self.cfg["eval_iters"]):
+                X, Y = self.batches.get_batch(split)
+                _, loss = m(X, Y)
+                losses[k] = loss.float()
+            out[split] = losses.mean().item()
+        m.train()
+        return out
+
+    def _save(self):
+        print(f"saving checkpoint to {self.cfg['out_dir']}")
+        save_checkpoint(os.path.join(self.cfg["out_dir"], "ckpt.pt"), self.raw_model, self.optimizer,
+                        self.model_args, self.iter_num, self.best_val_loss,
+                        {k: self.cfg[k] for k in config_keys(self.cfg)})
+
+    # ------------------------------------------------------------------ step
+    def train_step(self, X, Y):
+        """One optimizer iteration (grad_accum micro-steps + clip + fused AdamW).
+
+        Returns (last micro-step loss tensor, grad-norm tensor or None, next X, next Y)."""
+        c = self.cfg
+        for micro_step in range(self.gas):
+            sync = micro_step == self.gas - 1
+            if self.reducer is not None:
+                self.reducer.prepare(sync)
+            elif self.ddp_impl == "torch":
+                self.model.require_backward_grad_sync = sync
+            _, loss = self.model(X, Y)
+            loss = loss / self.gas  # scale the loss to account for gradient accumulation
+            # immediately async prefetch next batch while model is doing the forward pass on the GPU
+            X, Y = self.batches.get_batch("train")
+            loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        norm = None
+        if c["grad_clip"] != 0.0:
+            norm = self.optimizer.clip_grad_norm_(c["grad_clip"])
+        self.optimizer.step()
+        self.optimizer.zero_grad(set_to_none=True)
+        return loss, norm, X, Y
+
+    def fit(self):
+        c = self.cfg
+        X, Y = self.batches.get_batch("train")
+        t0 = time.time()
+        local_iter_num = 0
+        running_mfu = -1.0
+        prof = self._profiler() if c["profile"] and self.master else None
+        while True:
+            lr = get_lr(self.iter_num, c["learning_rate"], c["warmup_iters"], c["lr_decay_iters"], c["min_lr"]) \
+                if c["decay_lr"] else c["learning_rate"]
+            for param_group in self.optimizer.param_groups:
+                param_group["lr"] = lr
+
+            if self.iter_num % c["eval_interval"] == 0 and self.master:
+                losses = self.estimate_loss()
+                print(f"step {self.iter_num}: train loss {losses['train']:.4f}, val loss {losses['val']:.4f}")
+                self.metrics.log("eval", self.iter_num, train_loss=losses["train"], val_loss=losses["val"], lr=lr)
+                if losses["val"] < self.best_val_loss or c["always_save_checkpoint"]:
+                    self.best_val_loss = losses["val"]
+                    if self.iter_num > 0:
+                        self._save()
+            if self.iter_num == 0 and c["eval_only"]:
+                break
+            if c["fault_inject_iter"] == self.iter_num and c["fault_inject_rank"] == self.info.rank:
+                raise RuntimeError(f"injected fault at iter {self.iter_num} on rank {self.info.rank}")
+
+            loss, norm, X, Y = self.train_step(X, Y)
+            if prof is not None:
+                prof.step()
+
+            t1 = time.time()
+            dt = t1 - t0
+            t0 = t1
+            if self.iter_num % c["log_interval"] == 0 and self.master:
+                lossf = loss.item() * self.gas
+                if local_iter_num >= 5:  # let the training loop settle a bit
+                    mfu = self.raw_model.estimate_mfu(c["batch_size"] * self.gas, dt)  # per-GPU, as nanoGPT
+                    running_mfu = mfu if running_mfu == -1.0 else 0.9 * running_mfu + 0.1 * mfu
+                print(f"iter {self.iter_num}: loss {lossf:.4f}, time {dt * 1000:.2f}ms, mfu {running_mfu * 100:.2f}%")
+                extra = {"grad_norm": float(norm.item())} if norm is not None else {}
+                self.metrics.log("train", self.iter_num, loss=lossf, lr=lr, dt_ms=dt * 1000,
+                                 tokens_per_s=self.tokens_per_iter / dt, mfu=running_mfu, **extra)
+            self.iter_num += 1
+            local_iter_num += 1
+            if self.iter_num > c["max_iters"]:
+                break
+        if prof is not None:
+            prof.stop()
+        self.metrics.close()
+
+    def _profiler(self):
+        from torch.profiler import ProfilerActivity, profile, schedule, tensorboard_trace_handler
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.device_type == "cuda" else [])
+        p = profile(activities=acts, schedule=schedule(wait=5, warmup=5, active=5, repeat=1),
+                    on_trace_ready=tensorboard_trace_handler(os.path.join(self.cfg["out_dir"], "trace")),
+                    record_shapes=True, profile_memory=True)
+        p.start()
+        return p
+
+
+def main(argv=None):
+    cfg = parse_argv(TRAIN_DEFAULTS, sys.argv[1:] if argv is None else argv)
+    trainer = Trainer(cfg)
+    try:
+        trainer.fit()
+    finally:
+        destroy()
+    return trainer
+
+
+if __name__ == "__main__":
+    main()

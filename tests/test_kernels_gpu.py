@@ -1,0 +1,242 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference.
+
+Each test feeds the kernel bf16 inputs and compares with the fp32 torch op on
+the same (bf16-rounded) inputs; tolerances are bf16-output tolerances.
+SURVEY.md §4.2 item 4: shapes from §2.7 plus edge shapes (T not a multiple of
+the tile, D = 32 for the smoke config).
+"""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+class _P(torch.nn.Parameter):
+    pass
+
+
+def param(t, fused=False):
+    p = torch.nn.Parameter(t.float().clone())
+    if fused:
+        p.main_grad = torch.zeros_like(p, dtype=torch.float32)
+    p.compute = p.detach().to(BF)
+    return p
+
+
+# ---------------------------------------------------------------- layernorm
+@pytest.mark.parametrize("N,C,bias", [(300, 768, True), (129, 384, False), (64, 64, True), (33, 1600, True)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_layernorm(kernels, N, C, bias, fused):
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, device=DEV) * 2 + 0.5).to(BF).requires_grad_(True)
+    w = param(torch.randn(C, device=DEV) * 0.5 + 1, fused)
+    b = param(torch.randn(C, device=DEV) * 0.1, fused) if bias else None
+    y = ops.layer_norm(x, w, b)
+    dy = torch.randn(N, C, device=DEV).to(BF)
+    y.backward(dy)
+
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.compute.float().requires_grad_(True)
+    br = b.compute.float().requires_grad_(True) if bias else None
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    gw = w.main_grad if fused else w.grad
+    assert rel_err(gw, wr.grad) < 1e-3
+    if bias:
+        gb = b.main_grad if fused else b.grad
+        assert rel_err(gb, br.grad) < 1e-3
+
+
+# --------------------------------------------------------------------- gelu
+@pytest.mark.parametrize("n", [12288 * 8, 1000, 7])
+def test_gelu(kernels, n):
+    from nanosandbox_amd import ops
+
+    x = (torch.randn(n, device=DEV) * 3).to(BF).requires_grad_(True)
+    y = ops.gelu(x)
+    dy = torch.randn(n, device=DEV).to(BF)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.gelu(xr)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 1e-2
+
+
+# --------------------------------------------------------------- embedding
+@pytest.mark.parametrize("B,T,V,C", [(4, 128, 1000, 768), (3, 77, 65, 384)])
+def test_embedding(kernels, B, T, V, C):
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    idx[0, :5] = 3  # repeated tokens exercise the atomic accumulation
+    wte = param(torch.randn(V, C, device=DEV) * 0.02, fused=True)
+    wpe = param(torch.randn(T + 5, C, device=DEV) * 0.02, fused=True)
+    x = ops.embedding(idx, wte, wpe, 0.0, True, dtype=BF)
+    dx = torch.randn(B, T, C, device=DEV).to(BF)
+    x.backward(dx)
+    ref = wte.compute.float()[idx] + wpe.compute.float()[:T][None]
+    assert rel_err(x, ref) < 1e-2
+    gwte = torch.zeros(V, C, device=DEV).index_add_(0, idx.reshape(-1), dx.float().reshape(-1, C))
+    gwpe = torch.zeros(T + 5, C, device=DEV)
+    gwpe[:T] = dx.float().sum(0)
+    assert rel_err(wte.main_grad, gwte) < 1e-5
+    assert rel_err(wpe.main_grad, gwpe) < 1e-5
+
+
+# ------------------------------------------------------------ cross-entropy
+@pytest.mark.parametrize("N,V,C", [(256, 50304, 128), (200, 65, 64)])
+def test_lm_head_loss(kernels, N, V, C):
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, device=DEV)).to(BF).requires_grad_(True)
+    w = param(torch.randn(V, C, device=DEV) * 0.05, fused=True)
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[::7] = -1  # ignore_index
+    loss = ops.lm_head_loss(x, w, t)
+    (loss * 0.5).backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.compute.float().requires_grad_(True)
+    lr = F.cross_entropy(xr @ wr.t(), t, ignore_index=-1)
+    (lr * 0.5).backward()
+    assert abs(loss.item() - lr.item()) < 2e-2 * max(1.0, abs(lr.item()))
+    assert rel_err(x.grad, xr.grad) < 3e-2
+    assert rel_err(w.main_grad, wr.grad) < 3e-2
+
+
+# ----------------------------------------------------------------- dropout
+def test_dropout_mask_consistency(kernels):
+    from nanosandbox_amd import ops
+
+    x = torch.randn(1 << 16, device=DEV).to(BF).requires_grad_(True)
+    y = ops.dropout(x, 0.2, True)
+    y.backward(torch.ones_like(y))
+    zero = y == 0
+    frac = zero.float().mean().item()
+    assert 0.18 < frac < 0.22
+    assert torch.equal(x.grad == 0, zero)
+    kept = ~zero
+    assert torch.allclose(y[kept].float(), x[kept].float() / 0.8, rtol=1e-2)
+
+
+# --------------------------------------------------------- flash attention
+def attn_ref(qkv, H):
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    q, k, v = qkv.float().view(B, T, 3, H, C // H).permute(2, 0, 3, 1, 4)
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    return y.transpose(1, 2).reshape(B, T, C)
+
+
+@pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
+                                     (1, 77, 1, 32), (1, 192, 2, 128)])
+def test_flash_attention(kernels, B, T, H, D):
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    C = H * D
+    qkv = torch.randn(B, T, 3 * C, device=DEV).to(BF).requires_grad_(True)
+    y = ops.attention(qkv, H, 0.0, True)
+    dy = torch.randn(B, T, C, device=DEV).to(BF)
+    y.backward(dy)
+    xr = qkv.detach().float().requires_grad_(True)
+    yr = attn_ref(xr, H)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 2e-2, rel_err(y, yr)
+    g = qkv.grad.float().view(B, T, 3, C)
+    gr = xr.grad.view(B, T, 3, C)
+    for i, name in enumerate("qkv"):
+        e = rel_err(g[:, :, i], gr[:, :, i])
+        assert e < 3e-2, f"d{name} rel err {e}"
+
+
+def test_flash_attention_dropout_statistics(kernels):
+    """With dropout the kernel output is an unbiased estimate of the no-dropout output."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    B, T, H, D = 1, 128, 2, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
+    y0 = ops.attention(qkv, H, 0.0, True).float()
+    acc = torch.zeros_like(y0)
+    n = 64
+    for _ in range(n):
+        acc += ops.attention(qkv, H, 0.2, True).float()
+    assert rel_err(acc / n, y0) < 0.1
+
+
+# ------------------------------------------------------------------- AdamW
+def test_fused_adamw_matches_torch(kernels):
+    from nanosandbox_amd.models import GPT, GPTConfig
+    from nanosandbox_amd.optim import FlatParamStore
+
+    torch.manual_seed(0)
+    cfg = GPTConfig(block_size=64, vocab_size=128, n_layer=2, n_head=2, n_embd=64, bias=True)
+    m1 = GPT(cfg).to(DEV)
+    m2 = GPT(cfg).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    store = FlatParamStore(m1, DEV, compute_dtype=BF)
+    opt1 = m1.configure_optimizers(0.1, 1e-2, (0.9, 0.95), "cuda", store=store)
+    opt2 = m2.configure_optimizers(0.1, 1e-2, (0.9, 0.95), "cuda")
+    names = [n for n, _ in m1.named_parameters()]
+    p1 = dict(m1.named_parameters())
+    p2 = dict(m2.named_parameters())
+    for it in range(3):
+        for n in names:
+            g = torch.randn_like(p2[n]) * (it + 1)
+            p1[n].main_grad.copy_(g)
+            p2[n].grad = g.clone()
+        n1 = opt1.clip_grad_norm_(1.0)
+        n2 = torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        assert abs(n1.item() - n2.item()) < 1e-3 * n2.item()
+        opt1.step()
+        opt2.step()
+        opt1.zero_grad()
+    for n in names:
+        assert rel_err(p1[n], p2[n]) < 1e-5, n
+        assert rel_err(p1[n].compute, p2[n]) < 1e-2, n
+    sd = opt1.state_dict()
+    assert len(sd["state"]) == len(names)
+
+
+# ---------------------------------------------------------- whole model
+def test_gpt_gpu_matches_cpu_reference(kernels):
+    """bf16 HIP path vs the fp32 CPU path of the same model and weights."""
+    from nanosandbox_amd.models import GPT, GPTConfig
+    from nanosandbox_amd.optim import FlatParamStore
+
+    torch.manual_seed(0)
+    cfg = GPTConfig(block_size=128, vocab_size=1000, n_layer=2, n_head=4, n_embd=256, bias=True)
+    mc = GPT(cfg)
+    mg = GPT(cfg)
+    mg.load_state_dict(mc.state_dict())
+    mg.to(DEV).set_compute_dtype(BF)
+    sc = FlatParamStore(mc, "cpu")
+    sg = FlatParamStore(mg, DEV, compute_dtype=BF)
+    idx = torch.randint(0, 1000, (4, 128))
+    tgt = torch.randint(0, 1000, (4, 128))
+    _, lc = mc(idx, tgt)
+    lc.backward()
+    _, lg = mg(idx.to(DEV), tgt.to(DEV))
+    lg.backward()
+    assert abs(lc.item() - lg.item()) < 2e-2
+    assert rel_err(sg.grad.cpu(), sc.grad) < 5e-2
