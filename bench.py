@@ -1,9 +1,13 @@
 """Headline benchmark: whole-node training tokens/sec, GPT-2 124M bf16 DDP.
 
-BASELINE.json metric/config: GPT-2 124M, nanoGPT semantics — micro-batch 12 x
-block 1024, 40 micro-steps per optimizer step divided over the ranks
-(491,520 tokens per step regardless of N, i.e. strong scaling of a fixed
-global batch), synthetic tokens, random init.  One timed "step" is a full
+BASELINE.json metric/config: GPT-2 124M, nanoGPT ``train_gpt2`` semantics —
+480 sequences x 1024 tokens = 491,520 tokens per optimizer step regardless of
+N (strong scaling of a fixed global batch), synthetic tokens, random init.
+nanoGPT reaches that batch as micro-batch 12 x 40 accumulation steps because
+an A100 has 40 GB; on a 288 GB MI355X the same global batch runs as fewer,
+larger micro-steps (auto: the largest divisor of 480/N that is <= 120, i.e.
+120 x 4 on one GPU, 60 x 1 per rank on eight).  ``--micro-batch 12``
+reproduces nanoGPT's exact schedule.  One timed "step" is a full
 optimizer iteration: grad_accum x (fwd + bwd) with the bucketed RCCL
 all-reduce overlapped on the last micro-step, global-norm clip, fused AdamW.
 
@@ -35,7 +39,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--micro-batch", type=int, default=12)
+    ap.add_argument("--micro-batch", type=int, default=0,
+                    help="sequences per micro-step; 0 = auto: the largest divisor of the per-rank "
+                         "batch (480/N sequences) that is <= 120 (uses MI355X's 288 GB instead of "
+                         "nanoGPT's A100-sized 12; the 491,520-token global batch is unchanged)")
     ap.add_argument("--block-size", type=int, default=1024)
     ap.add_argument("--model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl"])
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
@@ -54,10 +61,14 @@ def main():
 
     dims = {"gpt2": (12, 12, 768), "gpt2-medium": (24, 16, 1024), "gpt2-large": (36, 20, 1280),
             "gpt2-xl": (48, 25, 1600)}[args.model]
+    per_rank_seqs = GLOBAL_MICRO_STEPS * 12 // world  # nanoGPT: 12 x 40 = 480 sequences per step
+    assert GLOBAL_MICRO_STEPS * 12 % world == 0, "global batch must divide over the ranks"
+    if args.micro_batch <= 0:
+        args.micro_batch = max(d for d in range(1, 121) if per_rank_seqs % d == 0)
+    assert per_rank_seqs % args.micro_batch == 0, "micro-batch must divide the per-rank batch"
     tokens_per_micro = args.micro_batch * args.block_size
-    # keep nanoGPT's 491,520 tokens/step even when the micro-batch is changed
-    total_micro = GLOBAL_MICRO_STEPS * 12 // args.micro_batch
-    assert total_micro % world == 0, "global micro-steps must divide over the ranks"
+    # keep nanoGPT's 491,520 tokens/step whatever the micro-batch
+    total_micro = per_rank_seqs // args.micro_batch * world
     cfg = dict(TRAIN_DEFAULTS)
     cfg.update(dataset="synthetic", batch_size=args.micro_batch, block_size=args.block_size,
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],

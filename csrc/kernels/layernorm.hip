@@ -18,7 +18,8 @@
 namespace {
 
 template <int NK>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                    bf16_t* __restrict__ sum_out, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                     int N, int C, float eps) {
@@ -33,6 +34,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
     const int c = (k * 64 + lane) * 8;
     if (c < C) {
       load8(xr + c, v[k]);
+      if (res) {  // fused residual add: s = x + res, written out (bf16) and normalised
+        float rv[8];
+        load8(res + (int64_t)row * C + c, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + rv[j]));
+        store8(sum_out + (int64_t)row * C + c, v[k]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[k][j];
     } else {
@@ -80,7 +88,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 template <int NK>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
-                                                    const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+                                                    const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+                                                    bf16_t* __restrict__ dx,
                                                     float* __restrict__ dw_part, float* __restrict__ db_part, int N,
                                                     int C) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
@@ -135,6 +144,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
+        if (dres) {  // gradient arriving through the residual path of the fused add
+          float rv[8];
+          load8(dres + (int64_t)row * C + c, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rv[j];
+        }
         store8(dx + (int64_t)row * C + c, o);
       }
     }
@@ -159,59 +174,53 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 }
 
 template <int NK>
-hipError_t launch_fwd(const void* x, const void* w, const void* b, void* y, void* mean, void* rstd, int N, int C,
-                      float eps, hipStream_t s) {
-  ln_fwd_kernel<NK><<<(N + 3) / 4, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
-                                                (float*)mean, (float*)rstd, N, C, eps);
+hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
+                      void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
+  ln_fwd_kernel<NK><<<(N + 3) / 4, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)sum_out,
+                                                (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (float*)mean,
+                                                (float*)rstd, N, C, eps);
   return hipGetLastError();
 }
 
 template <int NK>
-hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd, void* dx,
-                      void* dw_part, void* db_part, int N, int C, int nblk, hipStream_t s) {
+hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd,
+                      const void* dres, void* dx, void* dw_part, void* db_part, int N, int C, int nblk,
+                      hipStream_t s) {
   ln_bwd_kernel<NK><<<nblk, 256, 4 * C * sizeof(float), s>>>(
-      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd, (bf16_t*)dx,
+      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+      (const bf16_t*)dres, (bf16_t*)dx,
       (float*)dw_part, (float*)db_part, N, C);
   return hipGetLastError();
 }
 
 }  // namespace
 
-NSA_API hipError_t nsa_layernorm_fwd(const void* x, const void* w, const void* b, void* y, void* mean, void* rstd,
-                                     int N, int C, float eps, hipStream_t s) {
-  if (C % 8 != 0) return hipErrorInvalidValue;
-  const int nk = (C + 511) / 512;
-  switch (nk) {
-    case 1: return launch_fwd<1>(x, w, b, y, mean, rstd, N, C, eps, s);
-    case 2: return launch_fwd<2>(x, w, b, y, mean, rstd, N, C, eps, s);
-    case 3: return launch_fwd<3>(x, w, b, y, mean, rstd, N, C, eps, s);
-    case 4: return launch_fwd<4>(x, w, b, y, mean, rstd, N, C, eps, s);
-    case 5:
-    case 6: return launch_fwd<6>(x, w, b, y, mean, rstd, N, C, eps, s);
-    case 7:
-    case 8: return launch_fwd<8>(x, w, b, y, mean, rstd, N, C, eps, s);
-    default:
-      if (nk <= 16) return launch_fwd<16>(x, w, b, y, mean, rstd, N, C, eps, s);
-      return hipErrorInvalidValue;
+#define NSA_NK_SWITCH(NK_EXPR, CALL)                      \
+  switch (NK_EXPR) {                                        \
+    case 1: { constexpr int K_ = 1; return CALL; }          \
+    case 2: { constexpr int K_ = 2; return CALL; }          \
+    case 3: { constexpr int K_ = 3; return CALL; }          \
+    case 4: { constexpr int K_ = 4; return CALL; }          \
+    case 5:                                                 \
+    case 6: { constexpr int K_ = 6; return CALL; }          \
+    case 7:                                                 \
+    case 8: { constexpr int K_ = 8; return CALL; }          \
+    default:                                                \
+      if ((NK_EXPR) <= 16) { constexpr int K_ = 16; return CALL; } \
+      return hipErrorInvalidValue;                          \
   }
+
+// y = LN(x [+ res]) ; with res != NULL also writes sum_out = x + res (bf16)
+NSA_API hipError_t nsa_layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                                     void* y, void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512, launch_fwd<K_>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s));
 }
 
+// dx = LN'(dy) [+ dres]; per-block dw/db partial rows for nsa_colsum_accum
 NSA_API hipError_t nsa_layernorm_bwd(const void* dy, const void* x, const void* w, const void* mean,
-                                     const void* rstd, void* dx, void* dw_part, void* db_part, int N, int C, int nblk,
-                                     hipStream_t s) {
+                                     const void* rstd, const void* dres, void* dx, void* dw_part, void* db_part,
+                                     int N, int C, int nblk, hipStream_t s) {
   if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
-  const int nk = (C + 511) / 512;
-  switch (nk) {
-    case 1: return launch_bwd<1>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    case 2: return launch_bwd<2>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    case 3: return launch_bwd<3>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    case 4: return launch_bwd<4>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    case 5:
-    case 6: return launch_bwd<6>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    case 7:
-    case 8: return launch_bwd<8>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-    default:
-      if (nk <= 16) return launch_bwd<16>(dy, x, w, mean, rstd, dx, dw_part, db_part, N, C, nblk, s);
-      return hipErrorInvalidValue;
-  }
+  NSA_NK_SWITCH((C + 511) / 512, launch_bwd<K_>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, N, C, nblk, s));
 }

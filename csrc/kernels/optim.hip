@@ -100,19 +100,26 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict
 }
 
 // out[c] += sum_r partial[r][c]   (LayerNorm dW/db second-stage reduction)
+// grid = (ceil(C/64), splits): each block sums its slice of rows for 64 columns
+// (4 waves x strided rows, lane = column, coalesced 256-B rows), folds the 4
+// waves in LDS and adds into the fp32 gradient with one atomic per column —
+// `splits`-way contention per address only.
 __global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict__ partial, float* __restrict__ out,
-                                                       int rows, int C) {
+                                                       int rows, int C, int rows_per_split) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
   float acc = 0.0f;
   if (c < C) {
-    for (int r = w; r < rows; r += 4) acc += partial[(int64_t)r * C + c];
+#pragma unroll 4
+    for (int r = r0 + w; r < r1; r += 4) acc += partial[(int64_t)r * C + c];
   }
   __shared__ float red[4][64];
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && c < C) out[c] += red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  if (w == 0 && c < C) atomicAdd(out + c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 }  // namespace
@@ -144,6 +151,11 @@ NSA_API hipError_t nsa_clip_coef(const void* partial, int nparts, float scale, f
 }
 
 NSA_API hipError_t nsa_colsum_accum(const void* partial, void* out, int rows, int C, hipStream_t s) {
-  colsum_kernel<<<(C + 63) / 64, kBlock, 0, s>>>((const float*)partial, (float*)out, rows, C);
+  int splits = rows / 32;
+  if (splits < 1) splits = 1;
+  if (splits > 32) splits = 32;
+  const int rps = (rows + splits - 1) / splits;
+  dim3 grid((C + 63) / 64, splits);
+  colsum_kernel<<<grid, kBlock, 0, s>>>((const float*)partial, (float*)out, rows, C, rps);
   NSA_LAUNCH_CHECK();
 }

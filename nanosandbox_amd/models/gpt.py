@@ -67,14 +67,11 @@ class CausalSelfAttention(nn.Module):
         self.dropout = config.dropout
         self.flash = True  # always: our flash kernel (gfx950) / fp32 reference on CPU
 
-    def forward(self, x, residual=None):
-        """Returns ``residual + c_proj(attn(x))`` (residual folded into the GEMM when no dropout)."""
+    def forward(self, x):
+        """resid_dropout(c_proj(attn(c_attn(x)))) — the residual add is fused downstream."""
         qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)
         y = ops.attention(qkv, self.n_head, self.dropout, self.training)
-        if self.training and self.dropout > 0:
-            y = ops.dropout(ops.linear(y, self.c_proj.weight, self.c_proj.bias), self.dropout, True)
-            return y if residual is None else residual + y
-        return ops.linear(y, self.c_proj.weight, self.c_proj.bias, residual=residual)
+        return ops.dropout(ops.linear(y, self.c_proj.weight, self.c_proj.bias), self.dropout, self.training)
 
 
 class MLP(nn.Module):
@@ -84,15 +81,20 @@ class MLP(nn.Module):
         self.c_proj = nn.Linear(4 * config.n_embd, config.n_embd, bias=config.bias)
         self.dropout = config.dropout
 
-    def forward(self, x, residual=None):
+    def forward(self, x):
         h = ops.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias))
-        if self.training and self.dropout > 0:
-            y = ops.dropout(ops.linear(h, self.c_proj.weight, self.c_proj.bias), self.dropout, True)
-            return y if residual is None else residual + y
-        return ops.linear(h, self.c_proj.weight, self.c_proj.bias, residual=residual)
+        return ops.dropout(ops.linear(h, self.c_proj.weight, self.c_proj.bias), self.dropout, self.training)
 
 
 class Block(nn.Module):
+    """Pre-norm block ``x = x + attn(ln_1(x)); x = x + mlp(ln_2(x))``.
+
+    The hot path (``fused_forward``) takes ``h = ln_1(x)`` already computed and
+    returns the MLP branch un-added: every residual add is fused with the
+    LayerNorm that follows it (``ops.add_layer_norm``), so the residual stream
+    is read/written once per add and the backward needs no gradient-sum kernel.
+    """
+
     def __init__(self, config):
         super().__init__()
         self.ln_1 = LayerNorm(config.n_embd, bias=config.bias)
@@ -100,10 +102,18 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(config.n_embd, bias=config.bias)
         self.mlp = MLP(config)
 
+    def fused_forward(self, x, h):
+        x, h2 = ops.add_layer_norm(x, self.attn(h), self.ln_2.weight, self.ln_2.bias)
+        return x, self.mlp(h2)
+
     def forward(self, x):
-        x = self.attn(self.ln_1(x), residual=x)
-        x = self.mlp(self.ln_2(x), residual=x)
-        return x
+        x, y = self.fused_forward(x, self.ln_1(x))
+        return x + y
+
+
+def _block_step(block, next_ln, x, h):
+    x, y = block.fused_forward(x, h)
+    return ops.add_layer_norm(x, y, next_ln.weight, next_ln.bias)
 
 
 class GPT(nn.Module):
@@ -163,12 +173,7 @@ class GPT(nn.Module):
         tr = self.transformer
         x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, self.config.dropout, self.training,
                           dtype=self.compute_dtype)
-        for block in tr.h:
-            if self.grad_ckpt and self.training and torch.is_grad_enabled():
-                x = checkpoint(block, x, use_reentrant=False)
-            else:
-                x = block(x)
-        x = tr.ln_f(x)
+        x = self._trunk(x)
 
         if targets is not None:
             loss = ops.lm_head_loss(x, self.lm_head.weight, targets)
@@ -179,14 +184,25 @@ class GPT(nn.Module):
             loss = None
         return logits, loss
 
+    def _trunk(self, x):
+        """Blocks + ln_f with every residual add fused into the following LayerNorm."""
+        tr = self.transformer
+        blocks = tr.h
+        h = blocks[0].ln_1(x)
+        ckpt = self.grad_ckpt and self.training and torch.is_grad_enabled()
+        for i, block in enumerate(blocks):
+            nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else tr.ln_f
+            if ckpt:
+                x, h = checkpoint(_block_step, block, nxt, x, h, use_reentrant=False)
+            else:
+                x, h = _block_step(block, nxt, x, h)
+        return h
+
     def forward_logits(self, idx):
         """Full [B, T, V] fp32 logits (evaluation / tests)."""
         tr = self.transformer
         x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.compute_dtype)
-        for block in tr.h:
-            x = block(x)
-        x = tr.ln_f(x)
-        return ops.lm_head_logits(x, self.lm_head.weight)
+        return ops.lm_head_logits(self._trunk(x), self.lm_head.weight)
 
     # ------------------------------------------------------------ surgery/api
     def crop_block_size(self, block_size):

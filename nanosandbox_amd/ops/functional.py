@@ -216,66 +216,94 @@ def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32):
 # ----------------------------------------------------------------------------
 
 LN_EPS = 1e-5
-_LN_BWD_BLOCKS = 512
+_LN_BWD_BLOCKS = 2048  # ~2 rows per wave at N = 12288: enough waves to hide HBM latency
 
 
 class LayerNormFn(torch.autograd.Function):
+    """h = LN(x [+ y]).  With ``y`` the residual add is fused: returns (s = x + y, h).
+
+    Backward of the fused form: ds_total = LN'(dh) + ds (gradient that reached s
+    through the residual stream), computed in one kernel pass, and returned as
+    the gradient of both x and y — no separate autograd add kernel."""
+
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, y, w, b):
+        ctx.set_materialize_grads(False)
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         N = x2.shape[0]
         ctx.has_bias = b is not None
+        ctx.fused = y is not None
         if x.is_cuda:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
             x2 = x2.contiguous()
-            y = torch.empty_like(x2)
+            y2 = y.reshape(-1, C).contiguous() if y is not None else None
+            s2 = torch.empty_like(x2) if y is not None else None
+            h = torch.empty_like(x2)
             mean = torch.empty(N, device=x.device, dtype=F32)
             rstd = torch.empty(N, device=x.device, dtype=F32)
             wc = compute_weight(w, x.dtype)
             bc = compute_weight(b, x.dtype) if b is not None else None
-            _lib.call("nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y),
-                      _lib.ptr(mean), _lib.ptr(rstd), N, C, LN_EPS, _lib.stream())
+            _lib.call("nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(y2), _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc),
+                      _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C, LN_EPS, _lib.stream())
+            inp = s2 if y is not None else x2
         else:
             xf = x2.float()
+            if y is not None:
+                xf = xf + y.reshape(-1, C).float()
+            inp = xf.to(x.dtype)
             mean = xf.mean(-1)
             var = xf.var(-1, unbiased=False)
             rstd = torch.rsqrt(var + LN_EPS)
-            y = (xf - mean[:, None]) * rstd[:, None] * w.detach().float()
+            h = (xf - mean[:, None]) * rstd[:, None] * w.detach().float()
             if b is not None:
-                y = y + b.detach().float()
-            y = y.to(x.dtype)
-        ctx.save_for_backward(x2, w, b if b is not None else mean, mean, rstd)
-        return y.view(x.shape)
+                h = h + b.detach().float()
+            h = h.to(x.dtype)
+        ctx.save_for_backward(inp, w, b if b is not None else mean, mean, rstd)
+        if y is not None:
+            return inp.view(x.shape), h.view(x.shape)
+        return h.view(x.shape)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *grads):
+        if ctx.fused:
+            ds, dh = grads
+        else:
+            ds, dh = None, grads[0]
         x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
         b = b_or_mean if ctx.has_bias else None
         C = x2.shape[-1]
         N = x2.shape[0]
-        dy2 = dy.reshape(-1, C)
-        if dy.is_cuda:
+        shape = (dh if dh is not None else ds).shape
+        if dh is None:  # only the residual output was used
+            return ds, (ds if ctx.fused else None), None, None
+        dy2 = dh.reshape(-1, C)
+        if dh.is_cuda:
             dy2 = dy2.contiguous()
+            ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
             dx = torch.empty_like(x2)
-            nblk = min(_LN_BWD_BLOCKS, max(1, (N + 3) // 4))
-            dw_part = torch.empty(nblk, C, device=dy.device, dtype=F32)
-            db_part = torch.empty(nblk, C, device=dy.device, dtype=F32) if b is not None else None
+            nblk = min(_LN_BWD_BLOCKS, max(1, (N + 7) // 8))
+            dw_part = torch.empty(nblk, C, device=dh.device, dtype=F32)
+            db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
             _lib.call("nsa_layernorm_bwd", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(compute_weight(w, x2.dtype)),
-                      _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(dx), _lib.ptr(dw_part), _lib.ptr(db_part),
-                      N, C, nblk, _lib.stream())
+                      _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dw_part),
+                      _lib.ptr(db_part), N, C, nblk, _lib.stream())
             gw = _colsum_into(w, dw_part)
             gb = _colsum_into(b, db_part) if b is not None else None
-            return dx.view(dy.shape), gw, gb
+            dx = dx.view(shape)
+            return dx, (dx if ctx.fused else None), gw, gb
         xf = x2.float()
         d = dy2.float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
         wf = w.detach().float()
         dxhat = d * wf
         dx = rstd[:, None] * (dxhat - dxhat.mean(-1, keepdim=True) - xhat * (dxhat * xhat).mean(-1, keepdim=True))
+        if ds is not None:
+            dx = dx + ds.reshape(-1, C).float()
         gw = _accumulate(w, (d * xhat).sum(0))
         gb = _accumulate(b, d.sum(0)) if b is not None else None
-        return dx.to(dy.dtype).view(dy.shape), gw, gb
+        dx = dx.to(dh.dtype).view(shape)
+        return dx, (dx if ctx.fused else None), gw, gb
 
 
 def _colsum_into(p, partial):
@@ -292,7 +320,12 @@ def _colsum_into(p, partial):
 
 
 def layer_norm(x, w, b):
-    return LayerNormFn.apply(x, w, b)
+    return LayerNormFn.apply(x, None, w, b)
+
+
+def add_layer_norm(x, y, w, b):
+    """Fused residual add + LayerNorm: returns (x + y, LN(x + y))."""
+    return LayerNormFn.apply(x, y, w, b)
 
 
 # ----------------------------------------------------------------------------

@@ -87,7 +87,13 @@ def init_distributed(backend: str, device: str) -> DistInfo:
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     world = int(os.environ["WORLD_SIZE"])
-    if device.startswith("cuda"):
+    if device.startswith("cuda") and os.environ.get("NSA_REHEARSAL_ONE_GPU") == "1":
+        # multi-rank rehearsal on a 1-GPU box: every rank shares cuda:0 and the
+        # collectives go through gloo (RCCL refuses two ranks on one device)
+        device = "cuda:0"
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend="gloo")
+    elif device.startswith("cuda"):
         device = f"cuda:{local_rank}"
         torch.cuda.set_device(device)
         dist.init_process_group(backend=backend, device_id=torch.device(device))

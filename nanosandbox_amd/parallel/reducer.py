@@ -58,7 +58,7 @@ class FlatBucketReducer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
         self.reduce_dtype = reduce_dtype
-        cap = max(1, int(bucket_cap_mb)) * 1024 * 1024
+        cap = max(1, int(bucket_cap_mb * 1024 * 1024))
         self.buckets = [_Bucket(i, s, e, [m.param for m in members])
                         for i, (s, e, members) in enumerate(store.buckets(cap))]
         self._bucket_of = {}

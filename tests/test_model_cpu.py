@@ -1,0 +1,176 @@
+"""GPT model contract on CPU: parameter counts, state-dict keys, init, forward/backward
+parity with an independent plain-PyTorch nanoGPT-style reference, generate, surgery."""
+
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from nanosandbox_amd.models import GPT, GPTConfig
+from nanosandbox_amd.optim import FlatParamStore
+
+
+# ----------------------------------------------------------- reference model
+class RefBlock(nn.Module):
+    """Straight PyTorch version of nanoGPT's Block (SDPA math path), used as an oracle."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        C = cfg.n_embd
+        self.ln_1 = nn.LayerNorm(C, bias=cfg.bias)
+        self.c_attn = nn.Linear(C, 3 * C, bias=cfg.bias)
+        self.c_proj = nn.Linear(C, C, bias=cfg.bias)
+        self.ln_2 = nn.LayerNorm(C, bias=cfg.bias)
+        self.c_fc = nn.Linear(C, 4 * C, bias=cfg.bias)
+        self.mlp_proj = nn.Linear(4 * C, C, bias=cfg.bias)
+        self.n_head = cfg.n_head
+
+    def forward(self, x):
+        B, T, C = x.shape
+        q, k, v = self.c_attn(self.ln_1(x)).split(C, dim=2)
+        q, k, v = (t.view(B, T, self.n_head, C // self.n_head).transpose(1, 2) for t in (q, k, v))
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        x = x + self.c_proj(y.transpose(1, 2).contiguous().view(B, T, C))
+        return x + self.mlp_proj(F.gelu(self.c_fc(self.ln_2(x))))
+
+
+class RefGPT(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.block_size, cfg.n_embd)
+        self.h = nn.ModuleList([RefBlock(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = nn.LayerNorm(cfg.n_embd, bias=cfg.bias)
+
+    def forward(self, idx, targets):
+        x = self.wte(idx) + self.wpe(torch.arange(idx.shape[1]))
+        for b in self.h:
+            x = b(x)
+        logits = self.ln_f(x) @ self.wte.weight.t()
+        return F.cross_entropy(logits.view(-1, logits.size(-1)), targets.view(-1), ignore_index=-1)
+
+
+def load_ref(ref, sd, cfg):
+    m = {"wte.weight": "transformer.wte.weight", "wpe.weight": "transformer.wpe.weight",
+         "ln_f.weight": "transformer.ln_f.weight"}
+    if cfg.bias:
+        m["ln_f.bias"] = "transformer.ln_f.bias"
+    for i in range(cfg.n_layer):
+        for a, b in [("ln_1", "ln_1"), ("c_attn", "attn.c_attn"), ("c_proj", "attn.c_proj"), ("ln_2", "ln_2"),
+                     ("c_fc", "mlp.c_fc"), ("mlp_proj", "mlp.c_proj")]:
+            m[f"h.{i}.{a}.weight"] = f"transformer.h.{i}.{b}.weight"
+            if cfg.bias:
+                m[f"h.{i}.{a}.bias"] = f"transformer.h.{i}.{b}.bias"
+    ref.load_state_dict({k: sd[v] for k, v in m.items()})
+    return m
+
+
+# --------------------------------------------------------------------- tests
+def test_gpt2_124m_param_count():
+    with torch.device("meta"):
+        m = GPT(GPTConfig(n_layer=12, n_head=12, n_embd=768, block_size=1024, vocab_size=50304, bias=False))
+    total = sum(p.numel() for p in m.parameters())
+    assert total == 124_373_760  # 124.37M with tied wte/lm_head
+    assert m.get_num_params() == 123_587_328  # 123.59M non-embedding (wpe subtracted)
+
+
+def test_state_dict_keys_nanogpt_layout():
+    cfg = GPTConfig(n_layer=2, n_head=2, n_embd=32, block_size=16, vocab_size=50, bias=True)
+    sd = GPT(cfg).state_dict()
+    expect = {"transformer.wte.weight", "transformer.wpe.weight", "transformer.ln_f.weight",
+              "transformer.ln_f.bias", "lm_head.weight"}
+    for i in range(2):
+        for n in ["ln_1", "attn.c_attn", "attn.c_proj", "ln_2", "mlp.c_fc", "mlp.c_proj"]:
+            expect |= {f"transformer.h.{i}.{n}.weight", f"transformer.h.{i}.{n}.bias"}
+    assert set(sd) == expect
+    m = GPT(cfg)
+    assert m.transformer.wte.weight is m.lm_head.weight  # weight tying
+
+
+def test_init_statistics():
+    torch.manual_seed(0)
+    cfg = GPTConfig(n_layer=4, n_head=4, n_embd=256, block_size=64, vocab_size=2000, bias=True)
+    m = GPT(cfg)
+    assert m.transformer.h[0].attn.c_attn.weight.std().item() == pytest.approx(0.02, rel=0.05)
+    assert m.transformer.h[0].mlp.c_proj.weight.std().item() == pytest.approx(0.02 / math.sqrt(8), rel=0.05)
+    assert m.transformer.h[0].attn.c_attn.bias.abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("bias", [True, False])
+@pytest.mark.parametrize("flat", [False, True])
+def test_forward_backward_parity_with_reference(bias, flat):
+    torch.manual_seed(0)
+    cfg = GPTConfig(n_layer=2, n_head=4, n_embd=64, block_size=32, vocab_size=97, bias=bias)
+    m = GPT(cfg)
+    ref = RefGPT(cfg)
+    names = load_ref(ref, m.state_dict(), cfg)
+    store = FlatParamStore(m, "cpu") if flat else None
+    idx = torch.randint(0, 97, (3, 32))
+    tgt = torch.randint(0, 97, (3, 32))
+    tgt[0, :4] = -1
+    _, loss = m(idx, tgt)
+    loss.backward()
+    lref = ref(idx, tgt)
+    lref.backward()
+    assert loss.item() == pytest.approx(lref.item(), rel=1e-5)
+    ours = dict(m.named_parameters())
+    for rk, ok in names.items():
+        p = ours[ok] if ok in ours else m.lm_head.weight
+        g = p.main_grad if flat else p.grad
+        gr = dict(ref.named_parameters())[rk].grad
+        assert torch.allclose(g, gr, atol=1e-5, rtol=1e-4), rk
+
+
+def test_eval_logits_last_position_and_generate():
+    torch.manual_seed(0)
+    cfg = GPTConfig(n_layer=1, n_head=2, n_embd=32, block_size=16, vocab_size=40)
+    m = GPT(cfg).eval()
+    idx = torch.randint(0, 40, (2, 10))
+    logits, loss = m(idx)
+    assert loss is None and logits.shape == (2, 1, 40)
+    full = m.forward_logits(idx)
+    assert torch.allclose(full[:, -1], logits[:, 0], atol=1e-5)
+    out = m.generate(idx, 12, temperature=0.8, top_k=5)
+    assert out.shape == (2, 22) and torch.equal(out[:, :10], idx)
+
+
+def test_crop_block_size():
+    cfg = GPTConfig(n_layer=1, n_head=2, n_embd=32, block_size=64, vocab_size=40)
+    m = GPT(cfg)
+    w = m.transformer.wpe.weight[:16].clone()
+    m.crop_block_size(16)
+    assert m.config.block_size == 16 and torch.equal(m.transformer.wpe.weight, w)
+    with pytest.raises(AssertionError):
+        m(torch.zeros(1, 17, dtype=torch.long))
+
+
+def test_grad_ckpt_matches():
+    torch.manual_seed(0)
+    cfg = GPTConfig(n_layer=2, n_head=2, n_embd=32, block_size=16, vocab_size=40, dropout=0.1)
+    m = GPT(cfg)
+    idx = torch.randint(0, 40, (2, 16))
+    torch.manual_seed(5)
+    _, l1 = m(idx, idx)
+    l1.backward()
+    g1 = [p.grad.clone() for p in m.parameters()]
+    m.zero_grad()
+    m.grad_ckpt = True
+    torch.manual_seed(5)
+    _, l2 = m(idx, idx)
+    l2.backward()
+    assert l1.item() == pytest.approx(l2.item(), rel=1e-6)
+    for a, b in zip(g1, [p.grad for p in m.parameters()]):
+        assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_mfu_uses_mi355x_peak():
+    cfg = GPTConfig(n_layer=12, n_head=12, n_embd=768, block_size=1024, vocab_size=50304, bias=False)
+    with torch.device("meta"):
+        m = GPT(cfg)
+    fpt = m.flops_per_token()
+    # 6N + 12 L H Q T for 124M at T=1024 ~ 0.855 GFLOP/token
+    assert fpt == pytest.approx(0.855e9, rel=0.01)
+    mfu = m.estimate_mfu(12 * 40, 1.0)
+    assert mfu == pytest.approx(fpt * 1024 * 480 / 2.5e15)
