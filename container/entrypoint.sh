@@ -1,0 +1,85 @@
+#!/usr/bin/env bash
+# Pod entrypoint: derive the node rank and launch torchrun.
+#
+# Reference behaviour (README.md:21,102): in the multi-Pod StatefulSet the pod
+# ordinal becomes NODE_RANK (train-multipod-3 -> 3) and every pod rendezvouses
+# with pod 0 through the headless Service.  Single-Pod jobs use --standalone.
+#
+# Environment (all optional):
+#   NNODES          number of pods (1 = single-Pod topology)          [1]
+#   NPROC_PER_NODE  processes (= GPUs) per pod                         [1]
+#   NODE_RANK       explicit rank; default: ordinal suffix of POD_NAME/HOSTNAME
+#   MASTER_ADDR     rendezvous host, e.g. train-multipod-0.train-mp-headless
+#   MASTER_PORT     rendezvous port                                    [29500]
+#   RDZV_BACKEND    static (MASTER_ADDR/PORT + node_rank) | c10d         [static]
+#   RDZV_ID         c10d job id                                        [disttrain]
+#   MAX_RESTARTS    torchrun --max-restarts (elastic recovery)         [0]
+#   NSA_RCCL_PRESET xgmi (single node, P2P) | socket (pods without shared IPC)
+#   NSA_DRY_RUN=1   print the torchrun command instead of running it
+# Arguments: the training command after torchrun, e.g. train.py config/x.py --k=v
+set -euo pipefail
+
+NNODES="${NNODES:-1}"
+NPROC_PER_NODE="${NPROC_PER_NODE:-1}"
+MASTER_PORT="${MASTER_PORT:-29500}"
+RDZV_BACKEND="${RDZV_BACKEND:-static}"
+RDZV_ID="${RDZV_ID:-disttrain}"
+MAX_RESTARTS="${MAX_RESTARTS:-0}"
+
+ordinal_of() {
+  local host="$1"
+  if [[ "$host" =~ -([0-9]+)$ ]]; then
+    echo "${BASH_REMATCH[1]}"
+  else
+    echo ""
+  fi
+}
+
+if [[ -z "${NODE_RANK:-}" ]]; then
+  host="${POD_NAME:-${HOSTNAME:-$(hostname)}}"
+  NODE_RANK="$(ordinal_of "$host")"
+  if [[ -z "$NODE_RANK" ]]; then
+    if [[ "$NNODES" != "1" ]]; then
+      echo "entrypoint: cannot derive NODE_RANK from hostname '$host' (expected <name>-<ordinal>)" >&2
+      exit 2
+    fi
+    NODE_RANK=0
+  fi
+fi
+export NODE_RANK
+
+# RCCL transport preset: xGMI P2P inside one pod; socket fallback across pods
+# that do not share IPC (the reference's NCCL_IB_DISABLE/NCCL_SOCKET_IFNAME).
+if [[ "${NSA_RCCL_PRESET:-}" == "socket" ]]; then
+  export NCCL_IB_DISABLE="${NCCL_IB_DISABLE:-1}"
+  export NCCL_SOCKET_IFNAME="${NCCL_SOCKET_IFNAME:-eth0}"
+fi
+export HSA_ENABLE_IPC_MODE_LEGACY="${HSA_ENABLE_IPC_MODE_LEGACY:-0}"
+export TORCH_NCCL_HIGH_PRIORITY="${TORCH_NCCL_HIGH_PRIORITY:-1}"
+
+args=()
+if [[ "$NNODES" == "1" ]]; then
+  args+=(--standalone --nnodes=1 --nproc-per-node="$NPROC_PER_NODE")
+else
+  : "${MASTER_ADDR:?MASTER_ADDR must be set for NNODES > 1}"
+  if [[ "$RDZV_BACKEND" == "c10d" ]]; then
+    args+=(--nnodes="$NNODES" --nproc-per-node="$NPROC_PER_NODE" --rdzv-backend=c10d
+           --rdzv-endpoint="${MASTER_ADDR}:${MASTER_PORT}" --rdzv-id="$RDZV_ID" --node-rank="$NODE_RANK")
+  else
+    args+=(--nnodes="$NNODES" --nproc-per-node="$NPROC_PER_NODE" --node-rank="$NODE_RANK"
+           --master-addr="$MASTER_ADDR" --master-port="$MASTER_PORT")
+  fi
+fi
+if [[ "$MAX_RESTARTS" != "0" ]]; then
+  args+=(--max-restarts="$MAX_RESTARTS")
+fi
+
+PY="${PYTHON:-python3}"
+cmd=("$PY" -m torch.distributed.run "${args[@]}" "$@")
+echo "entrypoint: NODE_RANK=$NODE_RANK NNODES=$NNODES NPROC_PER_NODE=$NPROC_PER_NODE rdzv=$RDZV_BACKEND" >&2
+if [[ "${NSA_DRY_RUN:-0}" == "1" ]]; then
+  printf '%q ' "${cmd[@]}"
+  echo
+  exit 0
+fi
+exec "${cmd[@]}"

@@ -107,19 +107,35 @@ def write_token_dataset(out_dir: str, n_tokens: int, vocab: int = 50257, seed: i
     print(f"train has {n_tokens - n_val:,} tokens, val has {n_val:,} tokens")
 
 
+def _download(url: str, timeout: float = 30.0):
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:  # honours HTTP(S)_PROXY
+            return r.read().decode("utf-8")
+    except Exception as e:  # no network: keep the pipeline usable
+        print(f"download of {url} failed ({e}); using the synthetic corpus instead")
+        return None
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("kind", choices=["char", "tokens"])
     ap.add_argument("--out", required=True)
     ap.add_argument("--input", default="")
+    ap.add_argument("--url", default="", help="download the text (through HTTP(S)_PROXY); falls back to "
+                                              "the synthetic corpus when unreachable (air-gapped clusters)")
     ap.add_argument("--n_tokens", type=int, default=10_000_000)
     ap.add_argument("--seed", type=int, default=1337)
     a = ap.parse_args(argv)
     if a.kind == "char":
+        text = None
         if a.input:
             with open(a.input) as f:
                 text = f.read()
-        else:
+        elif a.url:
+            text = _download(a.url)
+        if text is None:
             text = synthetic_corpus(seed=a.seed)
         write_char_dataset(a.out, text)
     else:

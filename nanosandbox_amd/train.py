@@ -143,8 +143,8 @@ class Trainer:
                           f"(cap {c['ddp_bucket_mb']} MiB, {c['grad_reduce_dtype']})")
             elif self.ddp_impl == "torch":
                 from torch.nn.parallel import DistributedDataParallel as DDP
-                self.model = DDP(model, device_ids=[info.local_rank] if self.device_type == "cuda" else None,
-                                 bucket_cap_mb=c["ddp_bucket_mb"])
+                dev_ids = [torch.device(self.device).index] if self.device_type == "cuda" else None
+                self.model = DDP(model, device_ids=dev_ids, bucket_cap_mb=c["ddp_bucket_mb"])
                 self.store.refresh_compute()
             else:
                 raise ValueError(f"unknown ddp_impl {self.ddp_impl!r}")

@@ -10,9 +10,12 @@ pytestmark = pytest.mark.gpu
 
 def _cfg(tmp_path, **kw):
     from nanosandbox_amd.config import TRAIN_DEFAULTS
+    from nanosandbox_amd.data.prepare import synthetic_corpus, write_char_dataset
 
+    if not (tmp_path / "data" / "chars" / "train.bin").exists():
+        write_char_dataset(str(tmp_path / "data" / "chars"), synthetic_corpus(300_000))
     c = dict(TRAIN_DEFAULTS)
-    c.update(dataset="synthetic", out_dir=str(tmp_path), n_layer=2, n_head=4, n_embd=256, block_size=256,
+    c.update(dataset="chars", data_dir=str(tmp_path / "data"), out_dir=str(tmp_path), n_layer=2, n_head=4, n_embd=256, block_size=256,
              batch_size=8, gradient_accumulation_steps=2, max_iters=30, eval_interval=15, eval_iters=2,
              log_interval=5, learning_rate=3e-3, warmup_iters=2, lr_decay_iters=30, min_lr=3e-4,
              compile=False, device="cuda", always_save_checkpoint=True, tensorboard_dir=str(tmp_path / "runs"))
@@ -34,13 +37,16 @@ def test_train_and_resume(kernels, tmp_path):
     import json
     recs = [json.loads(l) for l in open(os.path.join(tmp_path, "metrics.jsonl"))]
     train = [r for r in recs if r["kind"] == "train"]
-    assert train[-1]["loss"] < train[0]["loss"]  # random tokens: loss falls towards ln(vocab)
+    assert train[-1]["loss"] < 0.8 * train[0]["loss"]  # learnable char data
     ev = [f for f in os.listdir(tmp_path / "runs" / "gpt2")]
     assert ev and read_events(str(tmp_path / "runs" / "gpt2" / ev[0]))
 
     tr2 = Trainer(_cfg(tmp_path, init_from="resume", max_iters=32))
     assert tr2.iter_num == 30
-    for a, b in zip(tr.raw_model.parameters(), tr2.raw_model.parameters()):
-        assert torch.equal(a.detach(), b.detach())
-    assert torch.equal(tr.optimizer.exp_avg, tr2.optimizer.exp_avg)
+    # the checkpoint is written at the eval of iter 30, before that iteration's step
+    for k, v in tr2.raw_model.state_dict().items():
+        assert torch.equal(v.cpu(), sd["model"][k]), k
+    st = tr2.optimizer.state_dict()["state"]
+    for i, s in sd["optimizer"]["state"].items():
+        assert torch.equal(st[i]["exp_avg"].cpu(), s["exp_avg"])
     tr2.fit()
