@@ -95,3 +95,29 @@ static inline uint32_t nsa_drop_thresh(float p) {
   if (t <= 0.0) return 0u;
   return (uint32_t)t;
 }
+
+// GELU (exact-erf form of nn.GELU) with a fast erf: Abramowitz & Stegun 7.1.26
+// (|error| < 1.5e-7, far below one bf16 ulp), sharing one exp between erf and
+// the normal pdf:  with z = x/sqrt(2), exp(-z^2) = exp(-x^2/2) = sqrt(2 pi) pdf(x).
+__device__ __forceinline__ void nsa_gelu_cdf_pdf(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = __expf(-z * z);
+  const float erf_abs = 1.0f - poly * e;
+  const float erf_z = x < 0.0f ? -erf_abs : erf_abs;
+  cdf = 0.5f * (1.0f + erf_z);
+  pdf = e * 0.39894228040143268f;
+}
+
+__device__ __forceinline__ float nsa_gelu(float x) {
+  float c, p;
+  nsa_gelu_cdf_pdf(x, c, p);
+  return x * c;
+}
+
+__device__ __forceinline__ float nsa_gelu_grad(float x) {
+  float c, p;
+  nsa_gelu_cdf_pdf(x, c, p);
+  return c + x * p;
+}

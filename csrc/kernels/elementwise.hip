@@ -17,13 +17,8 @@ inline int grid_for(int64_t n_vec) {
   return (int)g;
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
-  return cdf + x * pdf;
-}
+__device__ __forceinline__ float gelu_f(float x) { return nsa_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return nsa_gelu_grad(x); }
 
 __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          int64_t n) {

@@ -1,0 +1,316 @@
+// bf16 MFMA GEMM for gfx950 with the layouts and epilogues of GPT training
+// (every nn.Linear forward, input-grad and weight-grad).
+//
+//   C[M,N] (+)= A[M,K] · B[K,N]     fp32 accumulate, v_mfma_f32_16x16x32_bf16
+//
+// Operand storage (row-major torch tensors; `lda`/`ldb` are row strides):
+//   A_K = true : A stored [M][K]   (forward X, input-grad dY)       -> ds_read_b128 fragments
+//   A_K = false: A stored [K][M]   (weight-grad dY^T: dY is [M][N]) -> ds_read_b64_tr_b16 fragments
+//   B_K = true : B stored [N][K]   (forward W: nn.Linear weight)    -> ds_read_b128
+//   B_K = false: B stored [K][N]   (input-grad W, weight-grad X)    -> ds_read_b64_tr_b16
+// so   forward      Y  = X · W^T     is <A_K=1, B_K=1>
+//      input grad   dX = dY · W      is <A_K=1, B_K=0>
+//      weight grad  dW = dY^T · X    is <A_K=0, B_K=0>, split over K (=tokens) with an
+//                   fp32 atomic-add epilogue straight into the flat fp32 gradient buffer.
+//
+// Structure (cdna_hip_programming.md §5): 256x256 block tile, BK = 64, 8 waves as
+// 2 (M) x 4 (N), each wave 128x64 = 8x4 16x16 accumulators (128 AGPR/VGPR).
+// Tiles are staged global -> registers -> LDS (T14 split: loads for tile k+1 are
+// issued before the MFMAs of tile k and written to the other LDS buffer after
+// them; one barrier per K step).  LDS images are XOR-swizzled per 16-byte chunk
+// (scripts/lds_swizzle_check.py: conflict-free for the b128 and tr16 patterns).
+// The epilogue goes through LDS so that every global store / atomic wave
+// instruction covers whole contiguous rows (256 B of fp32 for the atomics — the
+// full-rate shape of MI355X_MICROARCH.md "Global float atomics").
+// Block ids are remapped so that the blocks sharing an XCD (b % 8) walk
+// neighbouring tiles (T1, bijective form).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int WAVES_M = 2, WAVES_N = 4;
+constexpr int WTM = BM / WAVES_M;  // 128
+constexpr int WTN = BN / WAVES_N;  // 64
+constexpr int FM = WTM / 16;       // 8
+constexpr int FN = WTN / 16;       // 4
+constexpr int TILE_A_BYTES = BM * BK * 2;
+constexpr int TILE_B_BYTES = BN * BK * 2;
+constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;  // 64 KiB
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;                // 128 KiB
+constexpr int EP_LD = 68;                                 // epilogue row pitch (fp32), +4 breaks bank aliasing
+constexpr int EP_BYTES = (NTHREADS / 64) * 64 * EP_LD * 4;  // 136 KiB
+constexpr int SMEM_BYTES = LDS_BYTES > EP_BYTES ? LDS_BYTES : EP_BYTES;
+
+enum Epi : int { EPI_STORE_BF16 = 0, EPI_ATOMIC_F32 = 1, EPI_GELU = 2, EPI_DGELU = 3 };
+
+// ---- swizzled LDS addressing -------------------------------------------------
+// K-contiguous image [rows][64]: 128-B rows, chunk' = chunk ^ ((row >> 1) & 7)
+__device__ __forceinline__ int kimg(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// row-contiguous image [64][W]: 2W-byte rows, chunk' = chunk ^ 2*g(row), g = (r&3) | ((r>>3)&1)<<2
+template <int W>
+__device__ __forceinline__ int rimg(int row, int chunk) {
+  const int g = (row & 3) | (((row >> 3) & 1) << 2);
+  return row * (W * 2) + ((chunk ^ (2 * g)) << 4);
+}
+
+__device__ __forceinline__ bf16x8 as_frag(uint4 u) { return __builtin_bit_cast(bf16x8, u); }
+
+__device__ __forceinline__ s16x4 lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+// operand fragment of 16 rows (or columns) x 32 k for the 16x16x32 MFMA
+// lane l: element j = X[r0 + (l & 15)][k = 32*kk + 8*(l >> 4) + j]
+template <bool KCONTIG, int W>
+__device__ __forceinline__ bf16x8 load_frag(const char* tile, int r0, int kk, int lane) {
+  if constexpr (KCONTIG) {
+    return as_frag(*reinterpret_cast<const uint4*>(tile + kimg(r0 + (lane & 15), 4 * kk + (lane >> 4))));
+  } else {
+    const int ig = lane & 15;
+    const int q = ig >> 2, p = ig & 3;
+    const int krow = 32 * kk + 8 * (lane >> 4) + q;
+    const int col = r0 + 4 * p;
+    const int off = (col & 7) * 2;
+    const s16x4 a = lds_tr(tile + rimg<W>(krow, col >> 3) + off);
+    const s16x4 b = lds_tr(tile + rimg<W>(krow + 4, col >> 3) + off);
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return nsa_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return nsa_gelu_grad(x); }
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;          // bf16 [M][ldc] or fp32 [M][ldc] (atomic epilogue)
+  bf16_t* C2;       // EPI_GELU: gelu(acc) output (C holds the pre-activation)
+  const bf16_t* U;  // EPI_DGELU: pre-activation whose gelu' scales acc
+  int M, N, K;
+  int lda, ldb, ldc;
+  int k_per_split;
+  int tiles_m, tiles_n;
+};
+
+template <bool A_K, bool B_K, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+
+  // XCD-aware, bijective block -> tile remap (blocks b, b+8, ... share an XCD)
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k_begin = blockIdx.z * g.k_per_split;
+  const int nk = g.k_per_split / BK;
+
+  // ---- global -> register staging: 4 x 16 B of A and 4 x 16 B of B per thread
+  // (plain code, no lambdas: a by-reference capture of ra/rb sends them to scratch)
+  uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+#define NSA_LOAD_A(c, dst, k0)                                                                   \
+  {                                                                                              \
+    const int e = tid + NTHREADS * (c);                                                          \
+    if constexpr (A_K) {                                                                         \
+      const int m = min(m0 + (e >> 3), g.M - 1);                                                 \
+      dst = *reinterpret_cast<const uint4*>(g.A + (int64_t)m * g.lda + (k0) + (e & 7) * 8);      \
+    } else {                                                                                     \
+      const int m = min(m0 + (e & 31) * 8, g.M - 8);                                             \
+      dst = *reinterpret_cast<const uint4*>(g.A + (int64_t)((k0) + (e >> 5)) * g.lda + m);       \
+    }                                                                                            \
+  }
+#define NSA_LOAD_B(c, dst, k0)                                                                   \
+  {                                                                                              \
+    const int e = tid + NTHREADS * (c);                                                          \
+    if constexpr (B_K) {                                                                         \
+      const int n = min(n0 + (e >> 3), g.N - 1);                                                 \
+      dst = *reinterpret_cast<const uint4*>(g.B + (int64_t)n * g.ldb + (k0) + (e & 7) * 8);      \
+    } else {                                                                                     \
+      const int n = min(n0 + (e & 31) * 8, g.N - 8);                                             \
+      dst = *reinterpret_cast<const uint4*>(g.B + (int64_t)((k0) + (e >> 5)) * g.ldb + n);       \
+    }                                                                                            \
+  }
+#define NSA_STORE_A(c, src, ta)                                                                  \
+  {                                                                                              \
+    const int e = tid + NTHREADS * (c);                                                          \
+    if constexpr (A_K) *reinterpret_cast<uint4*>((ta) + kimg(e >> 3, e & 7)) = src;              \
+    else *reinterpret_cast<uint4*>((ta) + rimg<BM>(e >> 5, e & 31)) = src;                       \
+  }
+#define NSA_STORE_B(c, src, tb)                                                                  \
+  {                                                                                              \
+    const int e = tid + NTHREADS * (c);                                                          \
+    if constexpr (B_K) *reinterpret_cast<uint4*>((tb) + kimg(e >> 3, e & 7)) = src;              \
+    else *reinterpret_cast<uint4*>((tb) + rimg<BN>(e >> 5, e & 31)) = src;                       \
+  }
+#define NSA_STAGE_LOAD(k0)                                                                       \
+  {                                                                                              \
+    NSA_LOAD_A(0, ra0, k0) NSA_LOAD_A(1, ra1, k0) NSA_LOAD_A(2, ra2, k0) NSA_LOAD_A(3, ra3, k0)  \
+    NSA_LOAD_B(0, rb0, k0) NSA_LOAD_B(1, rb1, k0) NSA_LOAD_B(2, rb2, k0) NSA_LOAD_B(3, rb3, k0)  \
+  }
+#define NSA_STAGE_WRITE(buf)                                                                     \
+  {                                                                                              \
+    char* ta_ = smem + (buf) * STAGE_BYTES;                                                      \
+    char* tb_ = ta_ + TILE_A_BYTES;                                                              \
+    NSA_STORE_A(0, ra0, ta_) NSA_STORE_A(1, ra1, ta_) NSA_STORE_A(2, ra2, ta_) NSA_STORE_A(3, ra3, ta_) \
+    NSA_STORE_B(0, rb0, tb_) NSA_STORE_B(1, rb1, tb_) NSA_STORE_B(2, rb2, tb_) NSA_STORE_B(3, rb3, tb_) \
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  NSA_STAGE_LOAD(k_begin)
+  NSA_STAGE_WRITE(0)
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) NSA_STAGE_LOAD(k_begin + (kt + 1) * BK)
+    const char* ta = smem + cur * STAGE_BYTES;
+    const char* tb = ta + TILE_A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = load_frag<A_K, BM>(ta, wm * WTM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = load_frag<B_K, BN>(tb, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) NSA_STAGE_WRITE(cur ^ 1)
+    __syncthreads();
+  }
+
+  // ---- epilogue through LDS: per wave a private [64 rows][64 + 4 pad] fp32 region,
+  // the 128-row wave tile in two halves of 64 rows.
+  float* ep = reinterpret_cast<float*>(smem) + wave * 64 * EP_LD;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int ii = 0; ii < FM / 2; ++ii) {
+      const int i = half * (FM / 2) + ii;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[(16 * ii + 4 * (lane >> 4) + e) * EP_LD + 16 * j + (lane & 15)] = acc[i][j][e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int row_base = m0 + wm * WTM + half * 64;
+    const int col_base = n0 + wn * WTN;
+    if constexpr (EPI == EPI_ATOMIC_F32) {
+      // one wave instruction = one 64-float (256 B) contiguous row segment
+      float* C = reinterpret_cast<float*>(g.C);
+      const int col = col_base + lane;
+      if (col < g.N) {
+        for (int rr = 0; rr < 64; ++rr) {
+          const int row = row_base + rr;
+          if (row < g.M) atomicAdd(C + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+        }
+      }
+    } else {
+      // 16 lanes x 4 columns per row, 4 rows per wave instruction, 8-byte bf16 stores
+      bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+      const int c4 = (lane & 15) * 4;
+      const int col = col_base + c4;
+      for (int rr = lane >> 4; rr < 64; rr += 4) {
+        const int row = row_base + rr;
+        if (row < g.M && col < g.N) {
+          const float4 v = *reinterpret_cast<const float4*>(ep + rr * EP_LD + c4);
+          float o[4] = {v.x, v.y, v.z, v.w};
+          const int64_t off = (int64_t)row * g.ldc + col;
+          if constexpr (EPI == EPI_DGELU) {
+            const uint2 u = *reinterpret_cast<const uint2*>(g.U + off);
+            o[0] *= gelu_grad(__uint_as_float(u.x << 16));
+            o[1] *= gelu_grad(__uint_as_float(u.x & 0xffff0000u));
+            o[2] *= gelu_grad(__uint_as_float(u.y << 16));
+            o[3] *= gelu_grad(__uint_as_float(u.y & 0xffff0000u));
+          }
+          uint2 w;
+          w.x = pack2(o[0], o[1]);
+          w.y = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(C + off) = w;
+          if constexpr (EPI == EPI_GELU) {
+            // gelu of the bf16-rounded pre-activation, exactly what a separate kernel would see
+            uint2 gv;
+            gv.x = pack2(gelu_f(__uint_as_float(w.x << 16)), gelu_f(__uint_as_float(w.x & 0xffff0000u)));
+            gv.y = pack2(gelu_f(__uint_as_float(w.y << 16)), gelu_f(__uint_as_float(w.y & 0xffff0000u)));
+            *reinterpret_cast<uint2*>(g.C2 + off) = gv;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <bool A_K, bool B_K, int EPI>
+hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  a.k_per_split = a.K / splits;
+  dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
+  (void)variant;  // reserved for alternative tilings
+  gemm_kernel<A_K, B_K, EPI><<<grid, NTHREADS, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// layout: 0 = NT (A [M][K], B [N][K]: forward), 1 = NN (A [M][K], B [K][N]: input grad),
+//         2 = TN (A stored [K][M], B [K][N]: weight grad)
+// epi: 0 store bf16, 1 fp32 atomic add into C, 2 store pre-activation + gelu into C2,
+//      3 store acc * gelu'(U)
+// bits 8..15 of `epi` select a tiling variant (reserved; 0 = 256x256, 8 waves)
+NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                            void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
+  const int variant = (epi >> 8) & 0xff;
+  epi &= 0xff;
+  if (K % (BK * splits) != 0 || M < 8 || N < 8 || M % 8 || N % 8) return hipErrorInvalidValue;
+  if (layout == 2 && M % 8) return hipErrorInvalidValue;
+  if (epi != EPI_ATOMIC_F32 && splits != 1) return hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = C;
+  a.C2 = (bf16_t*)C2;
+  a.U = (const bf16_t*)U;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+#define NSA_GEMM_CASE(L, AK, BKc)                                                       \
+  if (layout == L) {                                                                   \
+    switch (epi) {                                                                     \
+      case EPI_STORE_BF16: return launch<AK, BKc, EPI_STORE_BF16>(a, splits, variant, s);       \
+      case EPI_ATOMIC_F32: return launch<AK, BKc, EPI_ATOMIC_F32>(a, splits, variant, s);       \
+      case EPI_GELU: return launch<AK, BKc, EPI_GELU>(a, splits, variant, s);                   \
+      case EPI_DGELU: return launch<AK, BKc, EPI_DGELU>(a, splits, variant, s);                 \
+      default: return hipErrorInvalidValue;                                            \
+    }                                                                                  \
+  }
+  NSA_GEMM_CASE(0, true, true)
+  NSA_GEMM_CASE(1, true, false)
+  NSA_GEMM_CASE(2, false, false)
+#undef NSA_GEMM_CASE
+  return hipErrorInvalidValue;
+}

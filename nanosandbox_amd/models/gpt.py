@@ -82,8 +82,8 @@ class MLP(nn.Module):
         self.dropout = config.dropout
 
     def forward(self, x):
-        h = ops.gelu(ops.linear(x, self.c_fc.weight, self.c_fc.bias))
-        return ops.dropout(ops.linear(h, self.c_proj.weight, self.c_proj.bias), self.dropout, self.training)
+        y = ops.mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
+        return ops.dropout(y, self.dropout, self.training)
 
 
 class Block(nn.Module):

@@ -11,4 +11,5 @@ from .functional import (  # noqa: F401
     linear,
     lm_head_logits,
     lm_head_loss,
+    mlp,
 )

@@ -37,6 +37,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm as _gemm
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -90,17 +91,33 @@ def _addmm_f32_inplace_supported() -> bool:
     return _ADDMM_INPLACE_OK
 
 
-def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
-    """dW = dy2^T @ x2 accumulated in fp32 (into ``p.main_grad`` when present)."""
+def _nsa_wgrad_ok(dy2, x2) -> bool:
+    return (dy2.is_cuda and dy2.dtype == BF16 and x2.dtype == BF16 and dy2.is_contiguous() and x2.is_contiguous()
+            and dy2.shape[0] % 64 == 0 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0)
+
+
+def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, use_nsa: bool = True):
+    """dW = dy2^T @ x2 accumulated in fp32 (into ``p.main_grad`` when present).
+
+    On MI355X the transformer weight gradients use our split-K MFMA GEMM whose
+    epilogue atomically adds fp32 partials straight into the flat gradient
+    buffer (no bf16 dW, no separate accumulate pass); hipBLASLt's fp32-output
+    addmm is kept for the lm_head (50304-row output, where it is faster)."""
     mg = getattr(p, "main_grad", None)
     if dy2.is_cuda and dy2.dtype == BF16:
         if mg is not None:
-            if _addmm_f32_inplace_supported():
+            if use_nsa and _nsa_wgrad_ok(dy2, x2):
+                _gemm.wgrad_acc(dy2, x2, mg)
+            elif _addmm_f32_inplace_supported():
                 torch.addmm(mg, dy2.t(), x2, out_dtype=F32, out=mg)
             else:
                 mg.add_(torch.mm(dy2.t(), x2, out_dtype=F32))
             notify_grad_ready(p)
             return None
+        if use_nsa and _nsa_wgrad_ok(dy2, x2):
+            g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
+            _gemm.wgrad_acc(dy2, x2, g)
+            return g.to(p.dtype)
         return torch.mm(dy2.t(), x2, out_dtype=F32).to(p.dtype)
     g = dy2.t().float() @ x2.float()
     return _accumulate(p, g)
@@ -374,6 +391,67 @@ def linear(x, w, b=None, residual=None):
 
 
 # ----------------------------------------------------------------------------
+# MLP: c_proj(gelu(c_fc(x))) with GELU fused into GEMM epilogues (MI355X path)
+# ----------------------------------------------------------------------------
+
+# GEMM-epilogue GELU fusion is correct (tests/test_kernels_gpu.py::test_fused_mlp) but
+# measured slower than hipBLASLt + the standalone GELU kernels at GPT-2 shapes
+# (profiles/: the erf tail runs with the MFMA pipes idle at 1 workgroup/CU), so it
+# is opt-in until the GEMM main loop overtakes hipBLASLt.
+FUSE_GELU_EPILOGUE = False
+
+
+class MLPFn(torch.autograd.Function):
+    """c_proj(gelu(c_fc(x))) as ONE autograd node (bias-free GPT-2 configs).
+
+    Forward: u = x W_fc^T, g = gelu(u), y = g W_proj^T.  Backward: dg = dy W_proj,
+    du = dg * gelu'(u), dx = du W_fc, and both weight gradients accumulated in fp32
+    by our split-K GEMM.  With FUSE_GELU_EPILOGUE the activation (forward) and its
+    derivative (backward) run inside the GEMM epilogues instead."""
+
+    @staticmethod
+    def forward(ctx, x, w_fc, w_proj):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        wf = compute_weight(w_fc, x.dtype)
+        if FUSE_GELU_EPILOGUE:
+            u, g = _gemm.fwd_gelu(x2, wf)
+        else:
+            u = x2 @ wf.t()
+            g = torch.empty_like(u)
+            _lib.call("nsa_gelu_fwd", _lib.ptr(u), _lib.ptr(g), u.numel(), _lib.stream())
+        y = g @ compute_weight(w_proj, x.dtype).t()
+        ctx.save_for_backward(x2, u, g, w_fc, w_proj)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w_proj.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, u, g, w_fc, w_proj = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        wp = compute_weight(w_proj, dy.dtype)
+        if FUSE_GELU_EPILOGUE:
+            du = _gemm.dgrad(dy2, wp, u=u)
+        else:
+            dg = dy2 @ wp
+            du = torch.empty_like(dg)
+            _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
+        gw_proj = weight_grad(w_proj, dy2, g)
+        dx = du @ compute_weight(w_fc, dy.dtype)
+        gw_fc = weight_grad(w_fc, du, x2)
+        return dx.view(ctx.xshape), gw_fc, gw_proj
+
+
+def mlp(x, w_fc, b_fc, w_proj, b_proj):
+    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X when bias-free."""
+    M = x.numel() // x.shape[-1]
+    if (x.is_cuda and x.dtype == BF16 and b_fc is None and b_proj is None and M % 64 == 0
+            and x.shape[-1] % 64 == 0 and w_fc.shape[0] % 64 == 0):
+        return MLPFn.apply(x, w_fc, w_proj)
+    return linear(gelu(linear(x, w_fc, b_fc)), w_proj, b_proj)
+
+
+# ----------------------------------------------------------------------------
 # GELU (exact erf, nn.GELU() default)
 # ----------------------------------------------------------------------------
 
@@ -529,7 +607,7 @@ class LMHeadLossFn(torch.autograd.Function):
             dx = (dlogits @ wc)
             dx.mul_(g.to(dx.dtype))
             xs = x2 * g.to(x2.dtype)
-            gw = weight_grad(w, dlogits, xs)
+            gw = weight_grad(w, dlogits, xs, use_nsa=False)
             return dx.view(ctx.xshape), gw, None, None
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)

@@ -1,0 +1,98 @@
+"""Python front-end of our gfx950 MFMA GEMM (``csrc/kernels/gemm.hip``).
+
+Three layouts cover every nn.Linear GEMM of training (no transposed copies):
+
+* ``fwd(x, w)``            Y  = X · W^T            (x [M,K], w [N,K])
+* ``dgrad(dy, w)``         dX = dY · W             (dy [M,N], w [N,K])
+* ``wgrad_acc(dy, x, g)``  g += dY^T · X  (fp32)   split over the token dim,
+                                                    atomically accumulated into the
+                                                    flat fp32 gradient (no bf16 dW)
+plus fused epilogues: ``fwd_gelu`` (pre-activation + GELU in one pass) and
+``dgrad_dgelu`` (dX * gelu'(u), the MLP backward through the activation).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+BF16 = torch.bfloat16
+LAYOUT_NT, LAYOUT_NN, LAYOUT_TN = 0, 1, 2
+EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
+BK = 64
+TILE = 256
+
+
+def _check(t, name):
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name} must be 16-byte aligned")
+
+
+def supported(M, N, K) -> bool:
+    return M % 8 == 0 and N % 8 == 0 and K % BK == 0 and M >= 8 and N >= 8
+
+
+def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, C2=None, U=None):
+    _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, _lib.ptr(C2),
+              _lib.ptr(U), M, N, K, splits, _lib.stream())
+
+
+def fwd(x2, w, epi=EPI_STORE):
+    M, K = x2.shape
+    N = w.shape[0]
+    _check(x2, "x")
+    _check(w, "w")
+    out = torch.empty(M, N, device=x2.device, dtype=BF16)
+    if epi == EPI_GELU:
+        act = torch.empty_like(out)
+        _call(LAYOUT_NT, EPI_GELU, x2, K, w, K, out, N, M, N, K, C2=act)
+        return out, act
+    _call(LAYOUT_NT, EPI_STORE, x2, K, w, K, out, N, M, N, K)
+    return out
+
+
+def fwd_gelu(x2, w):
+    """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
+    return fwd(x2, w, epi=EPI_GELU)
+
+
+def dgrad(dy2, w, u=None):
+    """dX = dY @ W; with ``u`` also multiplies by gelu'(u) (fused activation backward)."""
+    M, N = dy2.shape
+    K = w.shape[1]
+    _check(dy2, "dy")
+    _check(w, "w")
+    out = torch.empty(M, K, device=dy2.device, dtype=BF16)
+    if u is not None:
+        _check(u, "u")
+        _call(LAYOUT_NN, EPI_DGELU, dy2, N, w, K, out, K, M, K, N, U=u)
+    else:
+        _call(LAYOUT_NN, EPI_STORE, dy2, N, w, K, out, K, M, K, N)
+    return out
+
+
+def wgrad_splits(n_out, n_in, tokens, cus=256):
+    tiles = -(-n_out // TILE) * -(-n_in // TILE)
+    best = 1
+    for s in range(1, 65):
+        if tokens % (BK * s):
+            continue
+        if tiles * s <= 2 * cus:
+            best = s
+    return best
+
+
+def wgrad_acc(dy2, x2, g32, splits=None):
+    """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel."""
+    T, N_out = dy2.shape
+    K_in = x2.shape[1]
+    _check(dy2, "dy")
+    _check(x2, "x")
+    _check(g32, "grad")
+    if splits is None:
+        splits = wgrad_splits(N_out, K_in, T)
+    _call(LAYOUT_TN, EPI_ATOMIC, dy2, N_out, x2, K_in, g32, K_in, N_out, K_in, T, splits=splits)
+    return g32

@@ -11,7 +11,13 @@ output + add.  Prints TFLOP/s so the op layer can pick the fastest form.
 import argparse
 import json
 
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nanosandbox_amd.ops import gemm as nsa_gemm  # noqa: E402
 
 
 def bench(fn, iters=20, warmup=5):
@@ -58,6 +64,9 @@ def main():
             "dW_bf16": lambda: dy.t() @ x,
             "dW_bf16_then_add": lambda: mg.add_(dy.t() @ x),
             "dW_f32_then_add": lambda: mg.add_(torch.mm(dy.t(), x, out_dtype=torch.float32)),
+            "ours_fwd": lambda: nsa_gemm.fwd(x, w),
+            "ours_dx": lambda: nsa_gemm.dgrad(dy, w),
+            "ours_dW_acc": lambda: nsa_gemm.wgrad_acc(dy, x, mg),
         }
         only = set(a.only.split(",")) if a.only else set(cands)
         t = {}

@@ -219,13 +219,15 @@ def test_fused_adamw_matches_torch(kernels):
 
 
 # ---------------------------------------------------------- whole model
-def test_gpt_gpu_matches_cpu_reference(kernels):
-    """bf16 HIP path vs the fp32 CPU path of the same model and weights."""
+@pytest.mark.parametrize("bias", [True, False])
+def test_gpt_gpu_matches_cpu_reference(kernels, bias):
+    """bf16 HIP path vs the fp32 CPU path of the same model and weights
+    (bias=False exercises the fused GELU-epilogue MLP and split-K weight grads)."""
     from nanosandbox_amd.models import GPT, GPTConfig
     from nanosandbox_amd.optim import FlatParamStore
 
     torch.manual_seed(0)
-    cfg = GPTConfig(block_size=128, vocab_size=1000, n_layer=2, n_head=4, n_embd=256, bias=True)
+    cfg = GPTConfig(block_size=128, vocab_size=1000, n_layer=2, n_head=4, n_embd=256, bias=bias)
     mc = GPT(cfg)
     mg = GPT(cfg)
     mg.load_state_dict(mc.state_dict())
@@ -240,3 +242,29 @@ def test_gpt_gpu_matches_cpu_reference(kernels):
     lg.backward()
     assert abs(lc.item() - lg.item()) < 2e-2
     assert rel_err(sg.grad.cpu(), sc.grad) < 5e-2
+
+
+@pytest.mark.parametrize("fuse", [False, True])
+def test_fused_mlp(kernels, fuse, monkeypatch):
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional
+
+    monkeypatch.setattr(functional, "FUSE_GELU_EPILOGUE", fuse)
+
+    torch.manual_seed(0)
+    M, C = 512, 256
+    x = torch.randn(M, C, device=DEV).to(BF).requires_grad_(True)
+    wf = param(torch.randn(4 * C, C, device=DEV) * 0.05, fused=True)
+    wp = param(torch.randn(C, 4 * C, device=DEV) * 0.05, fused=True)
+    y = ops.mlp(x, wf, None, wp, None)
+    dy = torch.randn(M, C, device=DEV).to(BF)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wfr = wf.compute.float().requires_grad_(True)
+    wpr = wp.compute.float().requires_grad_(True)
+    yr = F.gelu(xr @ wfr.t()) @ wpr.t()
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(x.grad, xr.grad) < 3e-2
+    assert rel_err(wf.main_grad, wfr.grad) < 3e-2
+    assert rel_err(wp.main_grad, wpr.grad) < 3e-2
