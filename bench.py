@@ -84,6 +84,9 @@ def main():
         X, Y = tr.batches.get_batch("train")
         for _ in range(args.warmup):
             loss, _, X, Y = tr.train_step(X, Y)
+        from nanosandbox_amd.ops import gemm_tune
+        for k, v in sorted(gemm_tune.table().items()):
+            print(f"gemm backend {k}: {v}")
         torch.cuda.synchronize()
         if dist.is_initialized():
             dist.barrier()

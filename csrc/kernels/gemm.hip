@@ -260,6 +260,247 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Variant 1 ("ring"): same 256x256 tile / 8 waves / 2x4 wave grid, but K is
+// staged in 32-deep slices by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into a
+// 4-slot LDS ring with TWO slices in flight: slice k+2 is issued while slice k
+// is multiplied, and each wave waits only for slice k with a counted
+// `s_waitcnt vmcnt(8)` folded into the raw `s_barrier` (never vmcnt(0) in the
+// loop — cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4).
+// The DMA is issued from inline asm: with the builtin, hipcc sees a pending LDS
+// write and drains vmcnt(0) before every ds_read.  Because the DMA destination is
+// lane-linear, the XOR swizzle is applied to the per-lane GLOBAL source address
+// (rule 21): image row r, physical chunk p holds logical chunk p ^ h(r).
+// WAR: slice k+3 reuses the slot of slice k-2 (5 slots), whose last reads
+// finished before every wave passed the barrier of iteration k-1.
+// The MFMA operands are swapped (C^T = B^T A^T) so each lane's accumulator holds
+// 4 consecutive output COLUMNS of one row: bf16 results are stored straight from
+// registers as 8-byte pieces (no LDS round trip); only the fp32 atomic epilogue
+// re-shapes through LDS into whole 256-B rows.
+// ---------------------------------------------------------------------------
+constexpr int RBK = 32;
+constexpr int RSLOT_A = BM * RBK * 2;          // 16 KiB
+constexpr int RSLOT_BYTES = 2 * RSLOT_A;       // A + B
+template <int SLOTS>
+struct RingGeo {
+  static constexpr int BYTES = SLOTS * RSLOT_BYTES;
+  static constexpr int SMEM = BYTES > EP_BYTES ? BYTES : EP_BYTES;
+  static_assert(SMEM <= 163840, "LDS budget");
+};
+
+// K-contiguous [256][32] image: 64-B rows, chunk' = chunk ^ (((row >> 3) & 1) << 1)
+__device__ __forceinline__ int kimg32(int row, int chunk) {
+  return row * 64 + ((chunk ^ (((row >> 3) & 1) << 1)) << 4);
+}
+
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ bf16x8 ring_frag(const char* tile, int r0, int lane) {
+  if constexpr (KCONTIG) {
+    return as_frag(*reinterpret_cast<const uint4*>(tile + kimg32(r0 + (lane & 15), lane >> 4)));
+  } else {
+    return load_frag<false, 256>(tile, r0, 0, lane);
+  }
+}
+
+template <bool A_K, bool B_K, int EPI, int RSLOTS, bool DIRECT>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_ring_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[RingGeo<RSLOTS>::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k_begin = blockIdx.z * g.k_per_split;
+  const int nk = g.k_per_split / RBK;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // per thread and slice: 2 DMA pieces of A and 2 of B (16 KiB each / 512 lanes / 16 B)
+  auto issue = [&](int s) {
+    const int k0 = k_begin + s * RBK;
+    const uint32_t slot = lds0 + (uint32_t)((s % RSLOTS) * RSLOT_BYTES);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = j * NTHREADS + tid;  // 16-byte piece index == LDS byte offset / 16
+      const uint32_t wbase = (uint32_t)((j * NTHREADS + wave * 64) * 16);
+      const bf16_t* srcA;
+      const bf16_t* srcB;
+      if constexpr (A_K) {
+        const int row = e >> 2, pc = e & 3;
+        const int c = pc ^ (((row >> 3) & 1) << 1);
+        srcA = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
+      } else {
+        const int row = e >> 5, pc = e & 31;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = pc ^ (2 * gg);
+        srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
+      }
+      if constexpr (B_K) {
+        const int row = e >> 2, pc = e & 3;
+        const int c = pc ^ (((row >> 3) & 1) << 1);
+        srcB = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + c * 8;
+      } else {
+        const int row = e >> 5, pc = e & 31;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = pc ^ (2 * gg);
+        srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
+      }
+      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + RSLOT_A + wbase));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int AHEAD = RSLOTS - 2;  // slices in flight beyond the one being multiplied
+  // prologue: slices 0 .. AHEAD-1; the loop issues slice k + AHEAD at iteration k
+#pragma unroll
+  for (int a = 0; a < AHEAD; ++a)
+    if (nk > a) issue(a);
+  for (int k = 0; k < nk; ++k) {
+    // wait for slice k; the younger slices (up to AHEAD, 4 DMA pieces each) may stay in flight
+    const int younger = min(AHEAD, nk - 1 - k);
+    if (k + AHEAD < nk) issue(k + AHEAD);
+    if constexpr (AHEAD == 3) {
+      if (younger == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+      else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const char* ta = smem + (k % RSLOTS) * RSLOT_BYTES;
+    const char* tb = ta + RSLOT_A;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = ring_frag<B_K>(tb, wn * WTN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = ring_frag<A_K>(ta, wm * WTM + 16 * i, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)  // swapped operands: acc[i][j][e] = C[16i + (l&15)][16j + 4(l>>4) + e]
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int lrow = lane & 15, lcol = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_ATOMIC_F32 || !DIRECT) {
+    // re-shape through LDS so each atomic wave-instruction covers one 256-B row
+    __syncthreads();
+    float* ep = reinterpret_cast<float*>(smem) + wave * 64 * EP_LD;
+    float* C = reinterpret_cast<float*>(g.C);
+    (void)C;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < FM / 2; ++ii) {
+        const int i = half * (FM / 2) + ii;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *reinterpret_cast<float4*>(ep + (16 * ii + lrow) * EP_LD + 16 * j + lcol) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int row_base = m0 + wm * WTM + half * 64;
+      if constexpr (EPI == EPI_ATOMIC_F32) {
+        const int col = n0 + wn * WTN + lane;
+        if (col < g.N) {
+          for (int rr = 0; rr < 64; ++rr) {
+            const int row = row_base + rr;
+            if (row < g.M) atomicAdd(C + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+          }
+        }
+      } else {
+        // 16 lanes x 4 columns = one 64-column row, 4 rows per wave instruction
+        bf16_t* Cb = reinterpret_cast<bf16_t*>(g.C);
+        const int c4 = (lane & 15) * 4;
+        const int col = n0 + wn * WTN + c4;
+        for (int rr = lane >> 4; rr < 64; rr += 4) {
+          const int row = row_base + rr;
+          if (row < g.M && col < g.N) {
+            const float4 v = *reinterpret_cast<const float4*>(ep + rr * EP_LD + c4);
+            float o[4] = {v.x, v.y, v.z, v.w};
+            const int64_t off = (int64_t)row * g.ldc + col;
+            if constexpr (EPI == EPI_DGELU) {
+              const uint2 u = *reinterpret_cast<const uint2*>(g.U + off);
+              o[0] *= gelu_grad(__uint_as_float(u.x << 16));
+              o[1] *= gelu_grad(__uint_as_float(u.x & 0xffff0000u));
+              o[2] *= gelu_grad(__uint_as_float(u.y << 16));
+              o[3] *= gelu_grad(__uint_as_float(u.y & 0xffff0000u));
+            }
+            uint2 w;
+            w.x = pack2(o[0], o[1]);
+            w.y = pack2(o[2], o[3]);
+            *reinterpret_cast<uint2*>(Cb + off) = w;
+            if constexpr (EPI == EPI_GELU) {
+              uint2 gv;
+              gv.x = pack2(gelu_f(__uint_as_float(w.x << 16)), gelu_f(__uint_as_float(w.x & 0xffff0000u)));
+              gv.y = pack2(gelu_f(__uint_as_float(w.y << 16)), gelu_f(__uint_as_float(w.y & 0xffff0000u)));
+              *reinterpret_cast<uint2*>(g.C2 + off) = gv;
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else {
+    bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = m0 + wm * WTM + 16 * i + lrow;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wn * WTN + 16 * j + lcol;
+        if (col >= g.N) continue;
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        const int64_t off = (int64_t)row * g.ldc + col;
+        if constexpr (EPI == EPI_DGELU) {
+          const uint2 u = *reinterpret_cast<const uint2*>(g.U + off);
+          o[0] *= gelu_grad(__uint_as_float(u.x << 16));
+          o[1] *= gelu_grad(__uint_as_float(u.x & 0xffff0000u));
+          o[2] *= gelu_grad(__uint_as_float(u.y << 16));
+          o[3] *= gelu_grad(__uint_as_float(u.y & 0xffff0000u));
+        }
+        uint2 w;
+        w.x = pack2(o[0], o[1]);
+        w.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(C + off) = w;
+        if constexpr (EPI == EPI_GELU) {
+          uint2 gv;
+          gv.x = pack2(gelu_f(__uint_as_float(w.x << 16)), gelu_f(__uint_as_float(w.x & 0xffff0000u)));
+          gv.y = pack2(gelu_f(__uint_as_float(w.y << 16)), gelu_f(__uint_as_float(w.y & 0xffff0000u)));
+          *reinterpret_cast<uint2*>(g.C2 + off) = gv;
+        }
+      }
+    }
+  }
+}
+
 template <bool A_K, bool B_K, int EPI>
 hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   GemmArgs a = a0;
@@ -267,8 +508,16 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.k_per_split = a.K / splits;
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  (void)variant;  // reserved for alternative tilings
-  gemm_kernel<A_K, B_K, EPI><<<grid, NTHREADS, 0, s>>>(a);
+  if (variant == 1)
+    gemm_ring_kernel<A_K, B_K, EPI, 4, false><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 2)
+    gemm_ring_kernel<A_K, B_K, EPI, 5, false><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 3)
+    gemm_ring_kernel<A_K, B_K, EPI, 4, true><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 4)
+    gemm_ring_kernel<A_K, B_K, EPI, 5, true><<<grid, NTHREADS, 0, s>>>(a);
+  else
+    gemm_kernel<A_K, B_K, EPI><<<grid, NTHREADS, 0, s>>>(a);
   return hipGetLastError();
 }
 
@@ -278,7 +527,11 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
 //         2 = TN (A stored [K][M], B [K][N]: weight grad)
 // epi: 0 store bf16, 1 fp32 atomic add into C, 2 store pre-activation + gelu into C2,
 //      3 store acc * gelu'(U)
-// bits 8..15 of `epi` select a tiling variant (reserved; 0 = 256x256, 8 waves)
+// bits 8..15 of `epi` select the pipeline: 0 = register-staged BK=64 double buffer,
+// 1..4 = LDS-DMA ring (BK=32 slices): 1 = 4 slots (2 in flight) + LDS epilogue,
+// 2 = 5 slots + LDS epilogue, 3 = 4 slots + direct stores, 4 = 5 slots + direct stores
+// (fragment double-buffering across slices was tried: 256 registers + 468 B/lane of
+// scratch at 2 waves/SIMD, so it is not kept)
 NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
                             void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
   const int variant = (epi >> 8) & 0xff;

@@ -38,6 +38,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import gemm as _gemm
+from . import gemm_tune as _tune
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -91,34 +92,24 @@ def _addmm_f32_inplace_supported() -> bool:
     return _ADDMM_INPLACE_OK
 
 
-def _nsa_wgrad_ok(dy2, x2) -> bool:
-    return (dy2.is_cuda and dy2.dtype == BF16 and x2.dtype == BF16 and dy2.is_contiguous() and x2.is_contiguous()
-            and dy2.shape[0] % 64 == 0 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0)
-
-
-def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, use_nsa: bool = True):
+def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     """dW = dy2^T @ x2 accumulated in fp32 (into ``p.main_grad`` when present).
 
-    On MI355X the transformer weight gradients use our split-K MFMA GEMM whose
-    epilogue atomically adds fp32 partials straight into the flat gradient
-    buffer (no bf16 dW, no separate accumulate pass); hipBLASLt's fp32-output
-    addmm is kept for the lm_head (50304-row output, where it is faster)."""
+    On MI355X the accumulate runs in the GEMM itself — our split-K MFMA kernel
+    atomically adds fp32 partials into the flat gradient, or hipBLASLt's
+    fp32-output addmm (beta=1), whichever the per-shape tuner measured faster.
+    No bf16 dW and no separate accumulate pass either way."""
     mg = getattr(p, "main_grad", None)
     if dy2.is_cuda and dy2.dtype == BF16:
+        dy2 = dy2.contiguous()
+        x2 = x2.contiguous()
         if mg is not None:
-            if use_nsa and _nsa_wgrad_ok(dy2, x2):
-                _gemm.wgrad_acc(dy2, x2, mg)
-            elif _addmm_f32_inplace_supported():
-                torch.addmm(mg, dy2.t(), x2, out_dtype=F32, out=mg)
-            else:
-                mg.add_(torch.mm(dy2.t(), x2, out_dtype=F32))
+            _tune.wgrad_acc(dy2, x2, mg)
             notify_grad_ready(p)
             return None
-        if use_nsa and _nsa_wgrad_ok(dy2, x2):
-            g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
-            _gemm.wgrad_acc(dy2, x2, g)
-            return g.to(p.dtype)
-        return torch.mm(dy2.t(), x2, out_dtype=F32).to(p.dtype)
+        g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
+        _tune.wgrad_acc(dy2, x2, g)
+        return g.to(p.dtype)
     g = dy2.t().float() @ x2.float()
     return _accumulate(p, g)
 
@@ -363,6 +354,8 @@ class LinearFn(torch.autograd.Function):
             out = torch.addmm(base, x2, wc.t())
         elif bc is not None:
             out = torch.addmm(bc, x2, wc.t())
+        elif x2.is_cuda and x2.dtype == BF16:
+            out = _tune.fwd(x2.contiguous(), wc)
         else:
             out = x2 @ wc.t()
         ctx.has_bias = b is not None
@@ -377,7 +370,9 @@ class LinearFn(torch.autograd.Function):
         d2 = dout.reshape(-1, Nout)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (d2 @ compute_weight(w, d2.dtype)).view(*dout.shape[:-1], x2.shape[-1])
+            wc = compute_weight(w, d2.dtype)
+            dx = _tune.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
+            dx = dx.view(*dout.shape[:-1], x2.shape[-1])
         gw = weight_grad(w, d2, x2)
         gb = None
         if ctx.has_bias:
@@ -417,10 +412,10 @@ class MLPFn(torch.autograd.Function):
         if FUSE_GELU_EPILOGUE:
             u, g = _gemm.fwd_gelu(x2, wf)
         else:
-            u = x2 @ wf.t()
+            u = _tune.fwd(x2, wf)
             g = torch.empty_like(u)
             _lib.call("nsa_gelu_fwd", _lib.ptr(u), _lib.ptr(g), u.numel(), _lib.stream())
-        y = g @ compute_weight(w_proj, x.dtype).t()
+        y = _tune.fwd(g, compute_weight(w_proj, x.dtype))
         ctx.save_for_backward(x2, u, g, w_fc, w_proj)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w_proj.shape[0])
@@ -433,11 +428,11 @@ class MLPFn(torch.autograd.Function):
         if FUSE_GELU_EPILOGUE:
             du = _gemm.dgrad(dy2, wp, u=u)
         else:
-            dg = dy2 @ wp
+            dg = _tune.dgrad(dy2, wp)
             du = torch.empty_like(dg)
             _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
         gw_proj = weight_grad(w_proj, dy2, g)
-        dx = du @ compute_weight(w_fc, dy.dtype)
+        dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
         gw_fc = weight_grad(w_fc, du, x2)
         return dx.view(ctx.xshape), gw_fc, gw_proj
 
@@ -575,7 +570,7 @@ class LMHeadLossFn(torch.autograd.Function):
         wc = compute_weight(w, x.dtype)
         if x.is_cuda:
             V = wc.shape[0]
-            logits = x2 @ wc.t()
+            logits = _tune.fwd(x2.contiguous(), wc)
             row_loss = torch.empty(N, device=x.device, dtype=F32)
             _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t.contiguous()), _lib.ptr(row_loss), N, V,
                       1 if need_grad else 0, _lib.stream())
@@ -604,10 +599,10 @@ class LMHeadLossFn(torch.autograd.Function):
         g = (gl.float() / n_valid)
         wc = compute_weight(w, x2.dtype)
         if x2.is_cuda:
-            dx = (dlogits @ wc)
+            dx = _tune.dgrad(dlogits, wc)
             dx.mul_(g.to(dx.dtype))
             xs = x2 * g.to(x2.dtype)
-            gw = weight_grad(w, dlogits, xs, use_nsa=False)
+            gw = weight_grad(w, dlogits, xs)
             return dx.view(ctx.xshape), gw, None, None
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)

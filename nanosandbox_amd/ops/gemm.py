@@ -13,6 +13,8 @@ plus fused epilogues: ``fwd_gelu`` (pre-activation + GELU in one pass) and
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -22,6 +24,8 @@ LAYOUT_NT, LAYOUT_NN, LAYOUT_TN = 0, 1, 2
 EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
 BK = 64
 TILE = 256
+# pipeline variant: 0 = register-staged BK=64 double buffer, 1 = LDS-DMA ring (2 slices in flight)
+VARIANT = int(os.environ.get("NSA_GEMM_VARIANT", "1"))
 
 
 def _check(t, name):
@@ -35,12 +39,13 @@ def supported(M, N, K) -> bool:
     return M % 8 == 0 and N % 8 == 0 and K % BK == 0 and M >= 8 and N >= 8
 
 
-def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, C2=None, U=None):
+def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, C2=None, U=None, variant=None):
+    epi = epi | ((VARIANT if variant is None else variant) << 8)
     _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, _lib.ptr(C2),
               _lib.ptr(U), M, N, K, splits, _lib.stream())
 
 
-def fwd(x2, w, epi=EPI_STORE):
+def fwd(x2, w, epi=EPI_STORE, variant=None):
     M, K = x2.shape
     N = w.shape[0]
     _check(x2, "x")
@@ -48,18 +53,18 @@ def fwd(x2, w, epi=EPI_STORE):
     out = torch.empty(M, N, device=x2.device, dtype=BF16)
     if epi == EPI_GELU:
         act = torch.empty_like(out)
-        _call(LAYOUT_NT, EPI_GELU, x2, K, w, K, out, N, M, N, K, C2=act)
+        _call(LAYOUT_NT, EPI_GELU, x2, K, w, K, out, N, M, N, K, C2=act, variant=variant)
         return out, act
-    _call(LAYOUT_NT, EPI_STORE, x2, K, w, K, out, N, M, N, K)
+    _call(LAYOUT_NT, EPI_STORE, x2, K, w, K, out, N, M, N, K, variant=variant)
     return out
 
 
-def fwd_gelu(x2, w):
+def fwd_gelu(x2, w, variant=None):
     """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
-    return fwd(x2, w, epi=EPI_GELU)
+    return fwd(x2, w, epi=EPI_GELU, variant=variant)
 
 
-def dgrad(dy2, w, u=None):
+def dgrad(dy2, w, u=None, variant=None):
     """dX = dY @ W; with ``u`` also multiplies by gelu'(u) (fused activation backward)."""
     M, N = dy2.shape
     K = w.shape[1]
@@ -68,9 +73,9 @@ def dgrad(dy2, w, u=None):
     out = torch.empty(M, K, device=dy2.device, dtype=BF16)
     if u is not None:
         _check(u, "u")
-        _call(LAYOUT_NN, EPI_DGELU, dy2, N, w, K, out, K, M, K, N, U=u)
+        _call(LAYOUT_NN, EPI_DGELU, dy2, N, w, K, out, K, M, K, N, U=u, variant=variant)
     else:
-        _call(LAYOUT_NN, EPI_STORE, dy2, N, w, K, out, K, M, K, N)
+        _call(LAYOUT_NN, EPI_STORE, dy2, N, w, K, out, K, M, K, N, variant=variant)
     return out
 
 
@@ -85,7 +90,7 @@ def wgrad_splits(n_out, n_in, tokens, cus=256):
     return best
 
 
-def wgrad_acc(dy2, x2, g32, splits=None):
+def wgrad_acc(dy2, x2, g32, splits=None, variant=None):
     """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel."""
     T, N_out = dy2.shape
     K_in = x2.shape[1]
@@ -94,5 +99,6 @@ def wgrad_acc(dy2, x2, g32, splits=None):
     _check(g32, "grad")
     if splits is None:
         splits = wgrad_splits(N_out, K_in, T)
-    _call(LAYOUT_TN, EPI_ATOMIC, dy2, N_out, x2, K_in, g32, K_in, N_out, K_in, T, splits=splits)
+    _call(LAYOUT_TN, EPI_ATOMIC, dy2, N_out, x2, K_in, g32, K_in, N_out, K_in, T, splits=splits,
+          variant=variant)
     return g32

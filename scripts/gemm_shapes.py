@@ -64,9 +64,13 @@ def main():
             "dW_bf16": lambda: dy.t() @ x,
             "dW_bf16_then_add": lambda: mg.add_(dy.t() @ x),
             "dW_f32_then_add": lambda: mg.add_(torch.mm(dy.t(), x, out_dtype=torch.float32)),
-            "ours_fwd": lambda: nsa_gemm.fwd(x, w),
-            "ours_dx": lambda: nsa_gemm.dgrad(dy, w),
-            "ours_dW_acc": lambda: nsa_gemm.wgrad_acc(dy, x, mg),
+            "ours_fwd": lambda: nsa_gemm.fwd(x, w, variant=0),
+            "ours_dx": lambda: nsa_gemm.dgrad(dy, w, variant=0),
+            "ours_dW_acc": lambda: nsa_gemm.wgrad_acc(dy, x, mg, variant=0),
+            **{f"v{v}_{n}": f for v in (1, 2, 3, 4) for n, f in (
+                ("fwd", lambda v=v: nsa_gemm.fwd(x, w, variant=v)),
+                ("dx", lambda v=v: nsa_gemm.dgrad(dy, w, variant=v)),
+                ("dW", lambda v=v: nsa_gemm.wgrad_acc(dy, x, mg, variant=v)))},
         }
         only = set(a.only.split(",")) if a.only else set(cands)
         t = {}

@@ -100,3 +100,31 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def search_bk32():
+    """K-contiguous [rows][32] tiles (64-B rows, 4 chunks): 16x16x32 operand read, kk = 0 only."""
+    def pattern(swz):
+        worst = 1
+        for r0 in range(0, 64, 16):
+            addrs = [swz(r0 + (l & 15), (l >> 4)) for l in range(64)]
+            worst = max(worst, degree(addrs, B128_GROUPS, 16))
+        return worst
+    import itertools as it
+    ident = lambda r, c: r * 64 + (c << 4)
+    print("BK=32 K-contig unswizzled degree:", pattern(ident))
+    for table in it.product(range(4), repeat=4):  # h depends on (row >> 2) & 3
+        sw = lambda r, c, t=table: r * 64 + ((c ^ t[(r >> 2) & 3]) << 4)
+        if pattern(sw) == 1:
+            print("  conflict-free h((row>>2)&3) =", table, "write:", write_b128(sw, 4, 256))
+            return table
+    for table in it.product(range(4), repeat=8):  # h depends on (row >> 1) & 7
+        sw = lambda r, c, t=table: r * 64 + ((c ^ t[(r >> 1) & 7]) << 4)
+        if pattern(sw) == 1:
+            print("  conflict-free h((row>>1)&7) =", table, "write:", write_b128(sw, 4, 256))
+            return table
+    print("  none found")
+
+
+if __name__ == "__main__":
+    search_bk32()

@@ -15,29 +15,31 @@ def rel(a, b):
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
                                    (256, 256, 3072)])
-def test_fwd(kernels, M, N, K):
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_fwd(kernels, M, N, K, variant):
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    y = gemm.fwd(x, w)
+    y = gemm.fwd(x, w, variant=variant)
     assert rel(y, x.float() @ w.float().t()) < 1e-2
-    u, g = gemm.fwd_gelu(x, w)
+    u, g = gemm.fwd_gelu(x, w, variant=variant)
     assert torch.equal(u, y)
     assert rel(g, F.gelu(u.float())) < 1e-2
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 3072, 768), (264, 512, 200), (2048, 50304, 768)])
-def test_dgrad(kernels, M, N, K):
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_dgrad(kernels, M, N, K, variant):
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
     dy = torch.randn(M, N, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    dx = gemm.dgrad(dy, w)
+    dx = gemm.dgrad(dy, w, variant=variant)
     ref = dy.float() @ w.float()
     assert rel(dx, ref) < 1e-2
     u = torch.randn(M, K, device=DEV).to(BF)
-    dxg = gemm.dgrad(dy, w, u=u)
+    dxg = gemm.dgrad(dy, w, u=u, variant=variant)
     uf = u.float()
     gp = 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
     assert rel(dxg, ref * gp) < 1.5e-2
@@ -45,7 +47,8 @@ def test_dgrad(kernels, M, N, K):
 
 @pytest.mark.parametrize("T,N,K,splits", [(1024, 768, 768, None), (4096, 2304, 768, None), (512, 520, 200, 2),
                                           (2048, 768, 3072, 4), (1024, 50304, 768, 1)])
-def test_wgrad_acc(kernels, T, N, K, splits):
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_wgrad_acc(kernels, T, N, K, splits, variant):
     from nanosandbox_amd.ops import gemm
     if K % 8:
         K = K - K % 8
@@ -54,15 +57,19 @@ def test_wgrad_acc(kernels, T, N, K, splits):
     x = torch.randn(T, K, device=DEV).to(BF)
     g = torch.randn(N, K, device=DEV)
     ref = g + dy.float().t() @ x.float()
-    gemm.wgrad_acc(dy, x, g, splits=splits)
+    gemm.wgrad_acc(dy, x, g, splits=splits, variant=variant)
     assert rel(g, ref) < 5e-3
 
 
-def test_asymmetric_identity(kernels):
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_asymmetric_identity(kernels, variant):
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from nanosandbox_amd.ops import gemm
     n = 256
     eye = torch.eye(n, device=DEV).to(BF)
     b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(251).to(BF)
-    assert torch.equal(gemm.fwd(eye, b).float(), b.float().t())  # I @ b^T
-    assert torch.equal(gemm.dgrad(eye, b).float(), b.float())     # I @ b
+    assert torch.equal(gemm.fwd(eye, b, variant=variant).float(), b.float().t())  # I @ b^T
+    assert torch.equal(gemm.dgrad(eye, b, variant=variant).float(), b.float())     # I @ b
+    g = torch.zeros(n, n, device=DEV)
+    gemm.wgrad_acc(eye, b, g, variant=variant)                                     # I^T @ b
+    assert torch.equal(g, b.float())
