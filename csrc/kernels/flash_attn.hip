@@ -108,11 +108,130 @@ __device__ __forceinline__ bf16x8 tr_frag_w(const char* tile, int r0, int r1, in
 // =============================================================================
 // forward
 // =============================================================================
-template <int D>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                          float* __restrict__ lse_out, int B, int T, int H,
-                                                          float scale_log2, uint32_t drop_thresh, float drop_scale,
-                                                          uint64_t seed) {
+// Deferred rescale (cdna_hip_programming.md T13): a lane keeps its running max
+// until a tile's max exceeds it by more than kDeferLog2 (log2 units), so the
+// O-wide rescale runs only on the (rare, after the first tiles) tiles where some
+// lane's max grows that much.  P is then bounded by 2^kDeferLog2 = 256, which the
+// fp32 accumulators absorb; l and the saved LSE stay exact (both relative to m).
+constexpr float kDeferLog2 = 8.0f;
+
+// sum / max with the other half-wave (lane ^ 32) through one v_permlane32_swap:
+// the swap returns {own value for lanes < 32 | partner's for lanes >= 32,
+// partner's for lanes < 32 | own for lanes >= 32}, so combining both halves of
+// the pair gives the pair's reduction on every lane.
+__device__ __forceinline__ float half_swap_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float half_swap_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Dropout parameters of one launch (char config); unused by the DROP=false build.
+struct DropArgs {
+  uint32_t thresh;
+  float scale;
+  uint64_t seed;
+  int bh, T;
+};
+
+// One 64-key tile for one wave (32 queries): S^T = K·Q^T, online softmax, O^T += V^T·P^T.
+// MASK: the tile straddles this wave's causal diagonal (exactly one tile per wave).
+template <int D, bool MASK, bool DROP>
+__device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+                                         f32x16 (&o)[D / 32], float& m_i, float& l_i, int kv0, int qpos, int h,
+                                         int r, int lane, float scale_log2, const DropArgs& dr) {
+  constexpr int NKS = D / 16;
+  constexpr int NDT = D / 32;
+  f32x16 st[2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
+      st[sb] = mfma(kf, qf[ks], st[sb]);
+    }
+  }
+  float mt = -INFINITY;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (MASK) {
+        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
+      }
+      mt = fmaxf(mt, st[sb][i]);
+    }
+  }
+  mt = half_swap_max(mt);
+  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
+  if (__builtin_amdgcn_ballot_w64(grow)) {  // wave-uniform: rescale only when some lane's max moved
+    const float m_new = grow ? mt : m_i;
+    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
+    l_i *= alpha;
+    m_i = m_new;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
+  }
+  const float mc = m_i * scale_log2;
+  float rs = 0.0f;
+  bf16x8 pf[2][2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(st[sb][i] * scale_log2 - mc);
+      rs += p;
+      if constexpr (DROP) {
+        const int kpos = kv0 + 32 * sb + acc_row(i, h);
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
+        p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
+      }
+      pf[sb][i >> 3][i & 7] = (__bf16)p;
+    }
+  }
+  l_i += half_swap_sum(rs);
+  // O^T += V^T · P^T
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
+        o[dt] = mfma(vf, pf[sb][s], o[dt]);
+      }
+    }
+  }
+}
+
+// K/V tile staging through registers (T14 split: issue before compute, write after)
+#define NSA_FWD_STAGE_LOAD(J)                                                                   \
+  _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
+    const int e = tid + 256 * c;                                                                \
+    const int row = e / CPR, ch = e % CPR;                                                      \
+    int key = (J) * BN + row;                                                                   \
+    key = key < T ? key : T - 1;                                                                \
+    kst[c] = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);       \
+    vst[c] = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * row_stride + ch * 8);       \
+  }
+#define NSA_FWD_STAGE_WRITE(BUF)                                                                \
+  _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
+    const int e = tid + 256 * c;                                                                \
+    const int row = e / CPR, ch = e % CPR;                                                      \
+    *reinterpret_cast<uint4*>(smem + (BUF) * TILE_BYTES + swz<D>(row, ch)) = kst[c];            \
+    *reinterpret_cast<uint4*>(smem + (2 + (BUF)) * TILE_BYTES + swz<D>(row, ch)) = vst[c];      \
+  }
+
+// workgroup = 4 waves x 32 queries; K/V tiles of 64 keys double-buffered in LDS
+// (32 KB at D = 64, so LDS admits 4 workgroups per CU; VGPRs set the occupancy).
+template <int D, bool DROP>
+__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_kernel(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, float* __restrict__ lse_out, int B, int T, int H,
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
   constexpr int BN = 64;
   constexpr int TILE_BYTES = BN * D * 2;
   constexpr int CPR = D / 8;
@@ -137,6 +256,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
   const bf16_t* qbase = base + hh * D;
   const bf16_t* kbase = base + C + hh * D;
   const bf16_t* vbase = base + 2 * C + hh * D;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
 
   // Q^T fragments (B operand): lane holds Q[qpos][16ks + 8h .. +8]
   bf16x8 qf[NKS];
@@ -156,107 +276,23 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
   const int n_tiles = (kv_end + BN - 1) / BN;
 
   uint4 kst[CHUNKS_PER_THREAD], vst[CHUNKS_PER_THREAD];
-  auto stage_load = [&](int j) {
-#pragma unroll
-    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
-      const int e = tid + 256 * c;
-      const int row = e / CPR, ch = e % CPR;
-      int key = j * BN + row;
-      key = key < T ? key : T - 1;
-      kst[c] = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);
-      vst[c] = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * row_stride + ch * 8);
-    }
-  };
-  auto stage_write = [&](int buf) {
-    char* kt = smem + buf * TILE_BYTES;
-    char* vt = smem + (2 + buf) * TILE_BYTES;
-#pragma unroll
-    for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {
-      const int e = tid + 256 * c;
-      const int row = e / CPR, ch = e % CPR;
-      *reinterpret_cast<uint4*>(kt + swz<D>(row, ch)) = kst[c];
-      *reinterpret_cast<uint4*>(vt + swz<D>(row, ch)) = vst[c];
-    }
-  };
-
-  stage_load(0);
-  stage_write(0);
+  NSA_FWD_STAGE_LOAD(0)
+  NSA_FWD_STAGE_WRITE(0)
   __syncthreads();
 
   for (int j = 0; j < n_tiles; ++j) {
     const int cur = j & 1;
     const int kv0 = j * BN;
-    if (j + 1 < n_tiles) stage_load(j + 1);
-    if (kv0 <= q0w + 31) {  // wave-uniform: tile has at least one visible key for this wave
-      const char* kt = smem + cur * TILE_BYTES;
-      const char* vt = smem + (2 + cur) * TILE_BYTES;
-      f32x16 st[2];
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        st[sb] = f32x16{};
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
-          st[sb] = mfma(kf, qf[ks], st[sb]);
-        }
-      }
-      // causal mask + tile max
-      const bool diag = kv0 + BN - 1 > q0w;
-      float mt = -1e30f;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float s = st[sb][i];
-          if (diag) {
-            const int kpos = kv0 + 32 * sb + acc_row(i, h);
-            if (kpos > qpos) s = -INFINITY;
-          }
-          st[sb][i] = s;
-          mt = fmaxf(mt, s);
-        }
-      }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float m_new = fmaxf(m_i, mt);
-      const float alpha = fast_exp2((m_i - m_new) * scale_log2);
-      const float mc = m_new * scale_log2;
-      float rs = 0.0f;
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(st[sb][i] * scale_log2 - mc);
-          rs += p;
-          float pv = p;
-          if (drop_thresh) {
-            const int kpos = kv0 + 32 * sb + acc_row(i, h);
-            const uint64_t id = ((uint64_t)bh * T + (uint64_t)qpos) * (uint64_t)T + (uint64_t)kpos;
-            pv = nsa_keep(seed, id, drop_thresh) ? p * drop_scale : 0.0f;
-          }
-          pf[sb][i >> 3][i & 7] = (__bf16)pv;
-        }
-      }
-      rs += __shfl_xor(rs, 32, 64);
-      l_i = l_i * alpha + rs;
-      m_i = m_new;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
-      // O^T += V^T · P^T
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) {
-            const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
-            o[dt] = mfma(vf, pf[sb][s], o[dt]);
-          }
-        }
-      }
-    }
-    if (j + 1 < n_tiles) stage_write(cur ^ 1);
+    // unconditional staging (the last iteration re-stages its own tile into the idle
+    // buffer): conditional register staging makes hipcc keep kst/vst in scratch
+    { NSA_FWD_STAGE_LOAD(min(j + 1, n_tiles - 1)) }
+    const char* kt = smem + cur * TILE_BYTES;
+    const char* vt = smem + (2 + cur) * TILE_BYTES;
+    if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+      fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+    else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+      fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+    { NSA_FWD_STAGE_WRITE(cur ^ 1) }
     __syncthreads();
   }
 
@@ -278,6 +314,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
     if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
   }
 }
+#undef NSA_FWD_STAGE_LOAD
+#undef NSA_FWD_STAGE_WRITE
 
 // =============================================================================
 // backward preprocessing: delta = rowsum(dO * O)   ([B, H, T] fp32)
@@ -306,30 +344,113 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 }
 
 // =============================================================================
-// backward main kernel: one workgroup = 128 keys (4 waves x 32) of one (b, h)
+// backward main kernel: one workgroup = KB keys (KB/32 waves x 32) of one (b, h)
 // =============================================================================
+// Geometry: KB = 256 keys (8 waves) for D = 64 (GPT-2), 128 (4 waves) for D = 32
+// (Q-tile staging needs >= 1 chunk per thread) and D = 128 (LDS).
+// dQ leaves the workgroup as fp32 atomics, one 64 x D tile per (q-block, key-block)
+// pair; the chip-wide atomic rate (~1.3 TB/s, MI355X_MICROARCH.md) made those the
+// bound at 128 keys, so the larger key block halves the atomic bytes.  The dQ tile
+// of a q-block is split over the waves by (q-half, d-tile) and, when there are more
+// waves than tiles, by key range; key-range partials are summed in LDS so only one
+// wave per tile issues atomics.
 template <int D>
-__global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B,
-                                                          int T, int H, float scale, float scale_log2,
-                                                          uint32_t drop_thresh, float drop_scale, uint64_t seed) {
-  constexpr int QB = 64;                    // queries per block iteration
-  constexpr int KB = 128;                   // keys per workgroup
+struct BwdGeo {
+  static constexpr int QB = 64;
+  static constexpr int KB = D == 64 ? 256 : 128;
+  static constexpr int NW = KB / 32;
+  static constexpr int NTILES = 2 * (D / 32);            // (q-half, d-tile) pairs of the dQ tile
+  static constexpr int SPLIT = NW > NTILES ? NW / NTILES : 1;
+  static constexpr int TPW = NTILES > NW ? NTILES / NW : 1;
+  static constexpr int QT_BYTES = QB * D * 2;
+  static constexpr int K_BYTES = KB * D * 2;
+  static constexpr int DS_BYTES = KB * QB * 2;
+  static constexpr int RED_BYTES = (SPLIT - 1) * NTILES * 64 * 16 * 4;
+  static constexpr int LDS_BYTES = 4 * QT_BYTES + K_BYTES + DS_BYTES + RED_BYTES + 4 * QB * 4;
+};
+
+// P and dS of one 32-query half for this lane's key -> bf16 MFMA fragments (i order).
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpacc, const float* lse2_s,
+                                          const float* delta_s, int qrow0, int qbase_pos, int kpos, int h,
+                                          float scale_log2, const DropArgs& dr, bf16x8 (&pfr)[2],
+                                          bf16x8 (&dsfr)[2]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 l4 = *reinterpret_cast<const float4*>(lse2_s + qrow0 + 8 * g + 4 * h);
+    const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qrow0 + 8 * g + 4 * h);
+    const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+    const float dlv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g + e;
+      const int q = qbase_pos + 8 * g + 4 * h + e;
+      float p = fast_exp2(sacc[i] * scale_log2 - lv[e]);
+      if constexpr (MASK) {
+        if (kpos > q || q >= dr.T) p = 0.0f;
+      }
+      float dp = dpacc[i];
+      float pd = p;
+      if constexpr (DROP) {
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)q) * (uint64_t)dr.T + (uint64_t)kpos;
+        const bool keep = nsa_keep(dr.seed, id, dr.thresh);
+        pd = keep ? p * dr.scale : 0.0f;
+        dp = keep ? dp * dr.scale : 0.0f;
+      }
+      pfr[i >> 3][i & 7] = (__bf16)pd;
+      dsfr[i >> 3][i & 7] = (__bf16)(p * (dp - dlv[e]));
+    }
+  }
+}
+
+#define NSA_BWD_STAGE_LOAD(QBI)                                                          \
+  _Pragma("unroll") for (int c = 0; c < QCH; ++c) {                                      \
+    const int e = tid + NT * c;                                                          \
+    const int row = e / CPR, ch = e % CPR;                                               \
+    int q = (QBI) * QB + row;                                                            \
+    q = q < T ? q : T - 1;                                                               \
+    qst[c] = *reinterpret_cast<const uint4*>(qbase + (int64_t)q * row_stride + ch * 8);  \
+    dost[c] = *reinterpret_cast<const uint4*>(dobase + (int64_t)q * C + ch * 8);         \
+  }                                                                                      \
+  {                                                                                      \
+    int q = (QBI) * QB + (tid & (QB - 1));                                               \
+    q = q < T ? q : T - 1;                                                               \
+    lst = lse_bh[q] * kLog2e;                                                            \
+    dst = delta_bh[q];                                                                   \
+  }
+#define NSA_BWD_STAGE_WRITE(BUF)                                                         \
+  _Pragma("unroll") for (int c = 0; c < QCH; ++c) {                                      \
+    const int e = tid + NT * c;                                                          \
+    const int row = e / CPR, ch = e % CPR;                                               \
+    *reinterpret_cast<uint4*>(qs_lds + (BUF) * QT_BYTES + swz<D>(row, ch)) = qst[c];     \
+    *reinterpret_cast<uint4*>(do_lds + (BUF) * QT_BYTES + swz<D>(row, ch)) = dost[c];    \
+  }                                                                                      \
+  if (tid < QB) {                                                                        \
+    ld_lds[(BUF) * QB + tid] = lst;                                                      \
+    ld_lds[2 * QB + (BUF) * QB + tid] = dst;                                             \
+  }
+
+template <int D, bool DROP>
+__global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
+    float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+  using G = BwdGeo<D>;
+  constexpr int QB = G::QB, KB = G::KB, NT = G::NW * 64;
   constexpr int CPR = D / 8;
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  constexpr int QT_BYTES = QB * D * 2;      // one Q (or dO) tile
-  constexpr int K_BYTES = KB * D * 2;       // workgroup's K tile (for dQ)
-  constexpr int DS_BYTES = KB * QB * 2;     // dS^T [128 keys][64 q]
-  constexpr int QCH = QB * CPR / 256;       // 16-byte chunks per thread per Q (or dO) tile
-  constexpr int KCH = KB * CPR / 256;
-  __shared__ __attribute__((aligned(16))) char smem[4 * QT_BYTES + K_BYTES + DS_BYTES + 4 * QB * 4];
-  char* const qs_lds = smem;                            // Q[2]
-  char* const do_lds = smem + 2 * QT_BYTES;             // dO[2]
-  char* const k_lds = smem + 4 * QT_BYTES;              // K (workgroup keys)
-  char* const ds_lds = k_lds + K_BYTES;                 // dS^T
-  float* const ld_lds = reinterpret_cast<float*>(ds_lds + DS_BYTES);  // lse2[2][QB], delta[2][QB]
+  constexpr int QT_BYTES = G::QT_BYTES;
+  constexpr int QCH = QB * CPR / NT;  // 16-byte chunks per thread per Q (or dO) tile
+  constexpr int KCH = KB * CPR / NT;
+  static_assert(QCH >= 1 && QB * CPR == QCH * NT, "Q tile staging must divide evenly");
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS_BYTES];
+  char* const qs_lds = smem;                         // Q[2]
+  char* const do_lds = smem + 2 * QT_BYTES;          // dO[2]
+  char* const k_lds = smem + 4 * QT_BYTES;           // K (workgroup keys)
+  char* const ds_lds = k_lds + G::K_BYTES;           // dS^T [KB keys][QB q]
+  float* const red_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES);            // split-K dQ partials
+  float* const ld_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES + G::RED_BYTES);  // lse2[2][QB], delta[2][QB]
 
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
@@ -349,6 +470,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
   const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
   const float* lse_bh = lse + (int64_t)bh * T;
   const float* delta_bh = delta + (int64_t)bh * T;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
 
   // K^T / V^T fragments for S = Q·K^T and dP = dO·V^T (B operands): K[kpos][16ks+8h..]
   bf16x8 kf[NKS], vf[NKS];
@@ -363,7 +485,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
   // workgroup K tile -> LDS (B operand of dQ = dS·K by transposed reads)
 #pragma unroll
   for (int c = 0; c < KCH; ++c) {
-    const int e = tid + 256 * c;
+    const int e = tid + NT * c;
     const int row = e / CPR, ch = e % CPR;
     int key = k0 + row;
     key = key < T ? key : T - 1;
@@ -382,47 +504,10 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
   const int n_qb = (T + QB - 1) / QB;
 
   uint4 qst[QCH], dost[QCH];
-  float lst = 0.0f, dst = 0.0f;
-  auto stage_load = [&](int qb) {
-#pragma unroll
-    for (int c = 0; c < QCH; ++c) {
-      const int e = tid + 256 * c;
-      const int row = e / CPR, ch = e % CPR;
-      int q = qb * QB + row;
-      q = q < T ? q : T - 1;
-      qst[c] = *reinterpret_cast<const uint4*>(qbase + (int64_t)q * row_stride + ch * 8);
-      dost[c] = *reinterpret_cast<const uint4*>(dobase + (int64_t)q * C + ch * 8);
-    }
-    if (tid < QB) {
-      int q = qb * QB + tid;
-      q = q < T ? q : T - 1;
-      lst = lse_bh[q] * kLog2e;
-      dst = delta_bh[q];
-    }
-  };
-  auto stage_write = [&](int buf) {
-    char* qt = qs_lds + buf * QT_BYTES;
-    char* dt_ = do_lds + buf * QT_BYTES;
-#pragma unroll
-    for (int c = 0; c < QCH; ++c) {
-      const int e = tid + 256 * c;
-      const int row = e / CPR, ch = e % CPR;
-      *reinterpret_cast<uint4*>(qt + swz<D>(row, ch)) = qst[c];
-      *reinterpret_cast<uint4*>(dt_ + swz<D>(row, ch)) = dost[c];
-    }
-    if (tid < QB) {
-      ld_lds[buf * QB + tid] = lst;
-      ld_lds[2 * QB + buf * QB + tid] = dst;
-    }
-  };
-
-  stage_load(qb_first);
-  stage_write(0);
+  float lst, dst;
+  NSA_BWD_STAGE_LOAD(qb_first)
+  NSA_BWD_STAGE_WRITE(0)
   __syncthreads();
-
-  // dQ tiles of the 64 x D output per q-block: (q-half, d-tile) pairs spread over the 4 waves
-  constexpr int NTILES = 2 * NDT;
-  constexpr int TPW = NTILES >= 4 ? NTILES / 4 : 1;
 
   for (int qb = qb_first; qb < n_qb; ++qb) {
     const int cur = (qb - qb_first) & 1;
@@ -430,7 +515,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
     const char* dot = do_lds + cur * QT_BYTES;
     const float* lse2_s = ld_lds + cur * QB;
     const float* delta_s = ld_lds + 2 * QB + cur * QB;
-    if (qb + 1 < n_qb) stage_load(qb + 1);
+    // unconditional (clamped) staging keeps qst/dost in registers (see forward)
+    { NSA_BWD_STAGE_LOAD(min(qb + 1, n_qb - 1)) }
 
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
@@ -449,33 +535,12 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
         dpacc = mfma(da, vf[ks], dpacc);
       }
       bf16x8 pfr[2], dsfr[2];
-      float dsv[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *reinterpret_cast<const float4*>(lse2_s + qs * 32 + 8 * g + 4 * h);
-        const float4 d4 = *reinterpret_cast<const float4*>(delta_s + qs * 32 + 8 * g + 4 * h);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float dlv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          const int q = qbase_pos + 8 * g + 4 * h + e;
-          float p = fast_exp2(sacc[i] * scale_log2 - lv[e]);
-          if (kpos > q || q >= T) p = 0.0f;
-          float dp = dpacc[i];
-          float pd = p;
-          if (drop_thresh) {
-            const uint64_t id = ((uint64_t)bh * T + (uint64_t)q) * (uint64_t)T + (uint64_t)kpos;
-            const bool keep = nsa_keep(seed, id, drop_thresh);
-            pd = keep ? p * drop_scale : 0.0f;
-            dp = keep ? dp * drop_scale : 0.0f;
-          }
-          const float ds = p * (dp - dlv[e]);
-          dsv[i] = ds;
-          pfr[i >> 3][i & 7] = (__bf16)pd;
-          dsfr[i >> 3][i & 7] = (__bf16)ds;
-        }
-      }
+      // wave-uniform: some (query, key) pair of this 32 x 32 block is masked / out of range
+      if (qbase_pos < kw0 + 31 || qbase_pos + 32 > T)
+        bwd_probs<true, DROP>(sacc, dpacc, lse2_s, delta_s, qs * 32, qbase_pos, kpos, h, scale_log2, dr, pfr, dsfr);
+      else
+        bwd_probs<false, DROP>(sacc, dpacc, lse2_s, delta_s, qs * 32, qbase_pos, kpos, h, scale_log2, dr, pfr,
+                               dsfr);
       // dV^T += dO^T · P  and  dK^T += Q^T · dS   (accumulators as B operands)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -488,40 +553,70 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
           dk[dt] = mfma(qa, dsfr[s], dk[dt]);
         }
       }
-      // dS^T -> LDS: row = key (32w + r), columns = q (qs*32 + 8g + 4h + 0..3)
+      // dS^T -> LDS: row = key (32w + r), columns = q (qs*32 + 8g + 4h + 0..3); the bf16
+      // values are the dK operand's, 4 per g: dsfr[g >> 1] elements 4(g & 1) .. +3
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qcol = qs * 32 + 8 * g + 4 * h;
+        const uint4 u4 = __builtin_bit_cast(uint4, dsfr[g >> 1]);
         uint2 u;
-        u.x = pack2(dsv[4 * g + 0], dsv[4 * g + 1]);
-        u.y = pack2(dsv[4 * g + 2], dsv[4 * g + 3]);
+        u.x = (g & 1) ? u4.z : u4.x;
+        u.y = (g & 1) ? u4.w : u4.y;
         *reinterpret_cast<uint2*>(ds_lds + swz<QB>(32 * w + r, qcol >> 3) + ((qcol >> 2) & 1) * 8) = u;
       }
     }
     __syncthreads();
     // stage the next Q/dO tile now: buffer cur^1 was last read before the previous
     // barrier, and doing it before the dQ atomics keeps their vmcnt out of its wait
-    if (qb + 1 < n_qb) stage_write(cur ^ 1);
+    { NSA_BWD_STAGE_WRITE(cur ^ 1) }
 
-    // dQ[64 x D] += dS[64 x 128] · K[128 x D]  (scaled), fp32 atomics
+    // dQ[64 x D] += dS[64 x KB] · K[KB x D]  (scaled)
+    constexpr int KSPAN = KB / G::SPLIT;  // keys per split part
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const int tile = w + 4 * t;
-      if (tile < NTILES) {
-        const int qh = tile & 1, dt = tile >> 1;
-        f32x16 dqa = f32x16{};
+    for (int t = 0; t < G::TPW; ++t) {
+      const int tile = (w % G::NTILES) + G::NW * t;
+      const int part = w / G::NTILES;  // 0 .. SPLIT-1 (0 when TPW > 1)
+      const int qh = tile & 1, dt = tile >> 1;
+      f32x16 dqa = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < KB / 16; ++ks) {
-          const int kr = 16 * ks + 8 * h;
-          const bf16x8 a = tr_frag<QB>(ds_lds, kr, kr + 4, qh * 32, lane);
-          const bf16x8 bk = tr_frag<D>(k_lds, kr, kr + 4, 32 * dt, lane);
-          dqa = mfma(a, bk, dqa);
+      for (int ks = 0; ks < KSPAN / 16; ++ks) {
+        const int kr = part * KSPAN + 16 * ks + 8 * h;
+        const bf16x8 a = tr_frag<QB>(ds_lds, kr, kr + 4, qh * 32, lane);
+        const bf16x8 bk = tr_frag<D>(k_lds, kr, kr + 4, 32 * dt, lane);
+        dqa = mfma(a, bk, dqa);
+      }
+      if constexpr (G::SPLIT > 1) {
+        if (part > 0) {
+          f32x4* dst4 = reinterpret_cast<f32x4*>(red_lds) + (((part - 1) * G::NTILES + tile) * 64 + lane) * 4;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) dst4[v] = f32x4{dqa[4 * v], dqa[4 * v + 1], dqa[4 * v + 2], dqa[4 * v + 3]};
         }
+        __syncthreads();
+        if (part == 0) {
+#pragma unroll
+          for (int p2 = 1; p2 < G::SPLIT; ++p2) {
+            const f32x4* src4 = reinterpret_cast<const f32x4*>(red_lds) + (((p2 - 1) * G::NTILES + tile) * 64 + lane) * 4;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const f32x4 x = src4[v];
+              dqa[4 * v] += x[0];
+              dqa[4 * v + 1] += x[1];
+              dqa[4 * v + 2] += x[2];
+              dqa[4 * v + 3] += x[3];
+            }
+          }
+        }
+      }
+      if (part == 0) {
         float* dqrow = dq_acc + (int64_t)b * T * C + hh * D + 32 * dt + r;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int q = qb * QB + qh * 32 + acc_row(i, h);
+#ifdef NSA_PROBE_DQ_STORE  // A/B timing probe only (see build.build_variant): wrong dQ
+          if (q < T) dqrow[(int64_t)q * C] = dqa[i] * scale;
+#else
           if (q < T) atomicAdd(dqrow + (int64_t)q * C, dqa[i] * scale);
+#endif
         }
       }
     }
@@ -548,6 +643,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_kernel(const bf16_t* __restr
     }
   }
 }
+#undef NSA_BWD_STAGE_LOAD
+#undef NSA_BWD_STAGE_WRITE
 
 // dq_acc (fp32 [B, T, C]) -> dqkv[:, :, 0:C] (bf16)
 __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv,
@@ -569,8 +666,12 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
   const int n_qt = (T + 127) / 128;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  flash_fwd_kernel<D><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                   scale * kLog2e, th, dscale, seed);
+  if (th)
+    flash_fwd_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+                                                           scale * kLog2e, th, dscale, seed);
+  else
+    flash_fwd_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
+                                                            H, scale * kLog2e, th, dscale, seed);
   return hipGetLastError();
 }
 
@@ -585,10 +686,15 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
   if (e != hipSuccess) return e;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  const int n_kb = (T + 127) / 128;
-  flash_bwd_kernel<D><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse,
-                                                   (const float*)delta, (float*)dq_acc, (bf16_t*)dqkv, B, T, H, scale,
-                                                   scale * kLog2e, th, dscale, seed);
+  const int n_kb = (T + BwdGeo<D>::KB - 1) / BwdGeo<D>::KB;
+  if (th)
+    flash_bwd_kernel<D, true><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
+        (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
+  else
+    flash_bwd_kernel<D, false><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
+        (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int C = H * D;

@@ -50,19 +50,19 @@ def _run(cmd):
     return r
 
 
-def build_kernels(force=False, jobs=8, verbose=True):
+def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL_LIB, obj_dir=BUILD_DIR):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
-    if not force and not _newer(KERNEL_LIB, srcs + headers):
-        return KERNEL_LIB
-    os.makedirs(BUILD_DIR, exist_ok=True)
-    os.makedirs(LIB_DIR, exist_ok=True)
+    if not force and not _newer(lib_path, srcs + headers):
+        return lib_path
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     hipcc = _hipcc()
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-             "-munsafe-fp-atomics", "-I", os.path.join(CSRC, "kernels")]
+             "-munsafe-fp-atomics", "-I", os.path.join(CSRC, "kernels"), *[f"-D{d}" for d in defines]]
 
     def compile_one(src):
-        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         if force or _newer(obj, [src] + headers):
             _run([hipcc, *flags, "-c", src, "-o", obj])
             if verbose:
@@ -71,12 +71,24 @@ def build_kernels(force=False, jobs=8, verbose=True):
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = KERNEL_LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
-    os.replace(tmp, KERNEL_LIB)
+    os.replace(tmp, lib_path)
     if verbose:
-        print(f"built {os.path.relpath(KERNEL_LIB, ROOT)}")
-    return KERNEL_LIB
+        print(f"built {os.path.relpath(lib_path, ROOT)}")
+    return lib_path
+
+
+def build_variant(name, defines, force=False, jobs=8, verbose=True):
+    """Build the kernel library with extra -D flags into ``build/variants/<name>/``.
+
+    Used for A/B probes (``NSA_KERNEL_LIB=<path>`` selects it at import time), e.g.
+    ``NSA_PROBE_DQ_STORE`` replaces the attention backward's dQ atomics by plain
+    stores to measure what the atomics cost (wrong results; timing only).
+    """
+    vdir = os.path.join(ROOT, "build", "variants", name)
+    return build_kernels(force=force, jobs=jobs, verbose=verbose, defines=defines,
+                         lib_path=os.path.join(vdir, "libnsa_kernels.so"), obj_dir=os.path.join(vdir, "obj"))
 
 
 def build_runtime(force=False, verbose=True):
@@ -104,7 +116,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--variant", nargs="+", metavar=("NAME", "DEFINE"),
+                    help="build an A/B probe variant: NAME followed by preprocessor defines")
     a = ap.parse_args(argv)
+    if a.variant:
+        print(build_variant(a.variant[0], a.variant[1:], force=a.force, jobs=a.jobs))
+        return 0
     build_all(force=a.force, jobs=a.jobs)
 
 

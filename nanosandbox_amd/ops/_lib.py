@@ -20,7 +20,9 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
-LIB_PATH = os.path.join(_LIB_DIR, "libnsa_kernels.so")
+# NSA_KERNEL_LIB points at an alternative build (e.g. an A/B probe variant from
+# ``nanosandbox_amd.build.build_variant``); default is the in-tree library.
+LIB_PATH = os.environ.get("NSA_KERNEL_LIB") or os.path.join(_LIB_DIR, "libnsa_kernels.so")
 
 _lock = threading.Lock()
 _lib = None

@@ -169,6 +169,51 @@ def test_flash_attention(kernels, B, T, H, D):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
+@pytest.mark.parametrize("pattern", ["rising", "falling", "spikes"])
+def test_flash_attention_deferred_rescale(kernels, pattern):
+    """Score patterns that drive the forward's deferred max-rescale branch.
+
+    "rising": every tile's max exceeds the running max by more than the defer
+    threshold (rescale on every tile); "falling": only the first tile sets the max;
+    "spikes": a few isolated large logits at random keys (the branch fires on some
+    tiles and for some lanes of a wave only).  Forward and all three gradients are
+    compared with the fp32 reference.
+    """
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(1)
+    B, T, H, D = 1, 512, 2, 64
+    C = H * D
+    q = torch.randn(B, T, H, D, device=DEV)
+    k = torch.randn(B, T, H, D, device=DEV)
+    v = torch.randn(B, T, H, D, device=DEV)
+    u = torch.nn.functional.normalize(torch.randn(D, device=DEV), dim=0)
+    q = q + 4.0 * u
+    if pattern == "rising":
+        ramp = torch.linspace(0, 1, T, device=DEV)
+        k = k + (ramp * 40.0)[None, :, None, None] * u  # score/sqrt(D) grows ~20 over the sequence
+    elif pattern == "falling":
+        ramp = torch.linspace(1, 0, T, device=DEV)
+        k = k + (ramp * 40.0)[None, :, None, None] * u
+    else:
+        idx = torch.randint(0, T, (24,), device=DEV)
+        k[:, idx] += 30.0 * u
+    qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(BF).requires_grad_(True)
+    y = ops.attention(qkv, H, 0.0, True)
+    dy = torch.randn(B, T, C, device=DEV).to(BF)
+    y.backward(dy)
+    xr = qkv.detach().float().requires_grad_(True)
+    yr = attn_ref(xr, H)
+    yr.backward(dy.float())
+    assert torch.isfinite(y.float()).all()
+    assert rel_err(y, yr) < 2e-2, rel_err(y, yr)
+    g = qkv.grad.float().view(B, T, 3, C)
+    gr = xr.grad.view(B, T, 3, C)
+    for i, name in enumerate("qkv"):
+        e = rel_err(g[:, :, i], gr[:, :, i])
+        assert e < 4e-2, f"{pattern}: d{name} rel err {e}"
+
+
 def test_flash_attention_dropout_statistics(kernels):
     """With dropout the kernel output is an unbiased estimate of the no-dropout output."""
     from nanosandbox_amd import ops
