@@ -4,6 +4,8 @@
   ``hipcc --offload-arch=gfx950 -O3`` (CDNA4 only; no CUDA / multi-arch paths)
 * ``lib/libnsa_runtime.so`` — the C++ host runtime (``csrc/runtime/*.cpp``:
   prefetching data loader), built with g++
+* ``bin/rccl_bench`` — RCCL collective micro-benchmark (``csrc/comm/rccl_bench.cpp``)
+  used to size DDP gradient buckets over xGMI
 
 Usage: ``python -m nanosandbox_amd.build [--force] [--jobs N]``.
 Objects are rebuilt only when a source or header is newer than the library.
@@ -27,6 +29,8 @@ ARCH = os.environ.get("NSA_OFFLOAD_ARCH", "gfx950")
 
 KERNEL_LIB = os.path.join(LIB_DIR, "libnsa_kernels.so")
 RUNTIME_LIB = os.path.join(LIB_DIR, "libnsa_runtime.so")
+BIN_DIR = os.path.join(ROOT, "nanosandbox_amd", "bin")
+RCCL_BENCH = os.path.join(BIN_DIR, "rccl_bench")
 
 
 def _hipcc():
@@ -107,8 +111,27 @@ def build_runtime(force=False, verbose=True):
     return RUNTIME_LIB
 
 
+def build_tools(force=False, verbose=True):
+    """Native command-line tools (host code linked against RCCL / the HIP runtime)."""
+    src = os.path.join(CSRC, "comm", "rccl_bench.cpp")
+    if not os.path.exists(src):
+        return None
+    if not force and not _newer(RCCL_BENCH, [src]):
+        return RCCL_BENCH
+    os.makedirs(BIN_DIR, exist_ok=True)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = RCCL_BENCH + ".tmp"
+    _run([_hipcc(), "-O2", "-std=c++17", "-I", os.path.join(rocm, "include"), src, "-L", os.path.join(rocm, "lib"),
+          "-lrccl", f"-Wl,-rpath,{os.path.join(rocm, 'lib')}", "-o", tmp])
+    os.replace(tmp, RCCL_BENCH)
+    if verbose:
+        print(f"built {os.path.relpath(RCCL_BENCH, ROOT)}")
+    return RCCL_BENCH
+
+
 def build_all(force=False, jobs=8, verbose=True):
     build_runtime(force=force, verbose=verbose)
+    build_tools(force=force, verbose=verbose)
     return build_kernels(force=force, jobs=jobs, verbose=verbose)
 
 
