@@ -310,101 +310,12 @@ __device__ __forceinline__ bf16x8 ring_frag(const char* tile, int r0, int lane) 
   }
 }
 
-template <bool A_K, bool B_K, int EPI, int RSLOTS, bool DIRECT>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_ring_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[RingGeo<RSLOTS>::SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int nwg = g.tiles_m * g.tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-  }
-  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int k_begin = blockIdx.z * g.k_per_split;
-  const int nk = g.k_per_split / RBK;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-
-  // per thread and slice: 2 DMA pieces of A and 2 of B (16 KiB each / 512 lanes / 16 B)
-  auto issue = [&](int s) {
-    const int k0 = k_begin + s * RBK;
-    const uint32_t slot = lds0 + (uint32_t)((s % RSLOTS) * RSLOT_BYTES);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int e = j * NTHREADS + tid;  // 16-byte piece index == LDS byte offset / 16
-      const uint32_t wbase = (uint32_t)((j * NTHREADS + wave * 64) * 16);
-      const bf16_t* srcA;
-      const bf16_t* srcB;
-      if constexpr (A_K) {
-        const int row = e >> 2, pc = e & 3;
-        const int c = pc ^ (((row >> 3) & 1) << 1);
-        srcA = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
-      } else {
-        const int row = e >> 5, pc = e & 31;
-        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
-        const int c = pc ^ (2 * gg);
-        srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
-      }
-      if constexpr (B_K) {
-        const int row = e >> 2, pc = e & 3;
-        const int c = pc ^ (((row >> 3) & 1) << 1);
-        srcB = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + c * 8;
-      } else {
-        const int row = e >> 5, pc = e & 31;
-        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
-        const int c = pc ^ (2 * gg);
-        srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
-      }
-      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
-      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + RSLOT_A + wbase));
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  constexpr int AHEAD = RSLOTS - 2;  // slices in flight beyond the one being multiplied
-  // prologue: slices 0 .. AHEAD-1; the loop issues slice k + AHEAD at iteration k
-#pragma unroll
-  for (int a = 0; a < AHEAD; ++a)
-    if (nk > a) issue(a);
-  for (int k = 0; k < nk; ++k) {
-    // wait for slice k; the younger slices (up to AHEAD, 4 DMA pieces each) may stay in flight
-    const int younger = min(AHEAD, nk - 1 - k);
-    if (k + AHEAD < nk) issue(k + AHEAD);
-    if constexpr (AHEAD == 3) {
-      if (younger == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
-      else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    const char* ta = smem + (k % RSLOTS) * RSLOT_BYTES;
-    const char* tb = ta + RSLOT_A;
-    bf16x8 af[FM], bfr[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j] = ring_frag<B_K>(tb, wn * WTN + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = ring_frag<A_K>(ta, wm * WTM + 16 * i, lane);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)  // swapped operands: acc[i][j][e] = C[16i + (l&15)][16j + 4(l>>4) + e]
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
+// Epilogue shared by the ring kernels.  fp32 atomics (and the non-DIRECT bf16
+// variants) re-shape through LDS so that each wave instruction covers whole
+// contiguous rows; DIRECT stores each lane's 4 consecutive columns from registers.
+template <int EPI, bool DIRECT>
+__device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
+                                              int wm, int wn, int lane, int wave) {
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
   if constexpr (EPI == EPI_ATOMIC_F32 || !DIRECT) {
     // re-shape through LDS so each atomic wave-instruction covers one 256-B row
@@ -501,6 +412,275 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring_kernel(GemmArgs g) {
   }
 }
 
+// PIPE = true ("pipelined ring", variants 5/6): besides the slice DMA, the MFMA
+// operand fragments are software-pipelined too.  Iteration k multiplies slice k
+// from registers while it reads slice k+1's fragments out of LDS, interleaved with
+// the MFMAs: A fragments are reloaded in place right after their last use, B
+// fragments are double-buffered (named sets, unrolled by 2: no dynamic register
+// indexing).  PMC counters of the plain ring showed every wave stalling on LDS
+// reads right after each barrier (SQ_WAIT_INST_LDS ~5x hipBLASLt's); here the read
+// latency hides under the MFMAs of the previous slice.  Slot reuse: the DMA of
+// slice k+RSLOTS goes into slice k's slot, whose fragment reads every wave finished
+// (lgkmcnt(0) folded into the barrier) before the barrier of iteration k.
+template <bool A_K, bool B_K, int EPI, int RSLOTS, bool DIRECT, bool PIPE = false>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_ring_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[RingGeo<RSLOTS>::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k_begin = blockIdx.z * g.k_per_split;
+  const int nk = g.k_per_split / RBK;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // per thread and slice: 2 DMA pieces of A and 2 of B (16 KiB each / 512 lanes / 16 B)
+  auto issue = [&](int s) {
+    const int k0 = k_begin + s * RBK;
+    const uint32_t slot = lds0 + (uint32_t)((s % RSLOTS) * RSLOT_BYTES);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = j * NTHREADS + tid;  // 16-byte piece index == LDS byte offset / 16
+      const uint32_t wbase = (uint32_t)((j * NTHREADS + wave * 64) * 16);
+      const bf16_t* srcA;
+      const bf16_t* srcB;
+      if constexpr (A_K) {
+        const int row = e >> 2, pc = e & 3;
+        const int c = pc ^ (((row >> 3) & 1) << 1);
+        srcA = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
+      } else {
+        const int row = e >> 5, pc = e & 31;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = pc ^ (2 * gg);
+        srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
+      }
+      if constexpr (B_K) {
+        const int row = e >> 2, pc = e & 3;
+        const int c = pc ^ (((row >> 3) & 1) << 1);
+        srcB = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + c * 8;
+      } else {
+        const int row = e >> 5, pc = e & 31;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = pc ^ (2 * gg);
+        srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
+      }
+      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + RSLOT_A + wbase));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (PIPE) {
+    // prologue: slices 0 .. RSLOTS-1 in flight, slice 0's fragments into registers
+#pragma unroll
+    for (int a = 0; a < RSLOTS; ++a)
+      if (nk > a) issue(a);
+    {
+      const int younger0 = min(RSLOTS - 1, nk - 1);
+      if (younger0 >= 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+      else if (younger0 == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if (younger0 == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    bf16x8 af[FM], b0[FN], b1[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b0[j] = ring_frag<B_K>(smem + RSLOT_A, wn * WTN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = ring_frag<A_K>(smem, wm * WTM + 16 * i, lane);
+
+// one pipelined iteration: wait for slice K+1 (own DMA) and every wave's reads of
+// slice K, barrier, refill slice K's slot with slice K+RSLOTS, then MFMAs of slice K
+// (registers BC / af) interleaved with the reads of slice K+1 (into af / BNX).
+// Reads past the last slice hit a valid slot and are discarded (pad, don't branch).
+#define NSA_PIPE_ITER(KK, BC, BNX)                                                              \
+  {                                                                                           \
+    const int k_ = (KK);                                                                      \
+    const int younger = min(k_ + RSLOTS - 1, nk - 1) - (k_ + 1);                              \
+    if (younger >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");  \
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");              \
+    if (k_ + RSLOTS < nk) issue(k_ + RSLOTS);                                                 \
+    const char* ta_ = smem + ((k_ + 1) % RSLOTS) * RSLOT_BYTES;                               \
+    const char* tb_ = ta_ + RSLOT_A;                                                          \
+    __builtin_amdgcn_s_setprio(1);                                                            \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i) {                                          \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                          \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BC[j], af[i], acc[i][j], 0, 0, 0); \
+      af[i] = ring_frag<A_K>(ta_, wm * WTM + 16 * i, lane);                                   \
+      if (i < FN) BNX[i] = ring_frag<B_K>(tb_, wn * WTN + 16 * i, lane);                      \
+    }                                                                                         \
+    __builtin_amdgcn_s_setprio(0);                                                            \
+  }
+
+    for (int k = 0; k < nk; k += 2) {
+      NSA_PIPE_ITER(k, b0, b1)
+      if (k + 1 < nk) NSA_PIPE_ITER(k + 1, b1, b0)
+    }
+#undef NSA_PIPE_ITER
+  } else {
+  constexpr int AHEAD = RSLOTS - 2;  // slices in flight beyond the one being multiplied
+    // prologue: slices 0 .. AHEAD-1; the loop issues slice k + AHEAD at iteration k
+  #pragma unroll
+    for (int a = 0; a < AHEAD; ++a)
+      if (nk > a) issue(a);
+    for (int k = 0; k < nk; ++k) {
+      // wait for slice k; the younger slices (up to AHEAD, 4 DMA pieces each) may stay in flight
+      const int younger = min(AHEAD, nk - 1 - k);
+      if (k + AHEAD < nk) issue(k + AHEAD);
+      if constexpr (AHEAD == 3) {
+        if (younger == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        if (younger == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      const char* ta = smem + (k % RSLOTS) * RSLOT_BYTES;
+      const char* tb = ta + RSLOT_A;
+      bf16x8 af[FM], bfr[FN];
+  #pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = ring_frag<B_K>(tb, wn * WTN + 16 * j, lane);
+  #pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = ring_frag<A_K>(ta, wm * WTM + 16 * i, lane);
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int i = 0; i < FM; ++i)
+  #pragma unroll
+        for (int j = 0; j < FN; ++j)  // swapped operands: acc[i][j][e] = C[16i + (l&15)][16j + 4(l>>4) + e]
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ring_epilogue<EPI, DIRECT>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+}
+
+
+// ---------------------------------------------------------------------------
+// Variants 7/8 ("ring64"): LDS-DMA slots 64 deep in K, so every DMA row of a
+// K-contiguous operand is a whole 128-B line (the 32-deep ring fetches 64-B
+// half-lines: twice the TA work, measured as the NT forward's deficit), laid out
+// as the register-staged kernel's images (kimg / rimg<256>, swizzle applied to
+// the per-lane global source).  Two 64 KiB slots; each slot is multiplied as two
+// 32-deep sub-slices with the fragment pipeline (reads of the next sub-slice
+// under the MFMAs of the current one: A in place, B double-buffered):
+//   phase A: MFMA(k, 0) | read (k, 1)           (same slot, no barrier)
+//   wait own DMA of slot k+1 + lgkmcnt(0), barrier, DMA slot k+2 -> slot k's buffer
+//   phase B: MFMA(k, 1) | read (k+1, 0)
+// Slot k's buffer is free at that barrier: its (k,0) reads completed before phase
+// A's MFMAs and its (k,1) reads before the barrier, in every wave.
+// ---------------------------------------------------------------------------
+constexpr int R64_SLOT_A = BM * 64 * 2;   // 32 KiB
+constexpr int R64_SLOT = 2 * R64_SLOT_A;  // A + B
+constexpr int R64_SMEM = 2 * R64_SLOT > EP_BYTES ? 2 * R64_SLOT : EP_BYTES;
+
+template <bool A_K, bool B_K, int EPI, bool DIRECT>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_ring64_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[R64_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k_begin = blockIdx.z * g.k_per_split;
+  const int nk = g.k_per_split / 64;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // per thread and slot: 4 DMA pieces of A and 4 of B (32 KiB each / 512 lanes / 16 B)
+  auto issue = [&](int s) {
+    const int k0 = k_begin + s * 64;
+    const uint32_t slot = lds0 + (uint32_t)((s & 1) * R64_SLOT);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = j * NTHREADS + tid;
+      const uint32_t wbase = (uint32_t)((j * NTHREADS + wave * 64) * 16);
+      const bf16_t* srcA;
+      const bf16_t* srcB;
+      if constexpr (A_K) {
+        const int row = e >> 3, c = (e & 7) ^ ((row >> 1) & 7);
+        srcA = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
+      } else {
+        const int row = e >> 5;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = (e & 31) ^ (2 * gg);
+        srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
+      }
+      if constexpr (B_K) {
+        const int row = e >> 3, c = (e & 7) ^ ((row >> 1) & 7);
+        srcB = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + c * 8;
+      } else {
+        const int row = e >> 5;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = (e & 31) ^ (2 * gg);
+        srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
+      }
+      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + R64_SLOT_A + wbase));
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nk > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  bf16x8 af[FM], b0[FN], b1[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) b0[j] = load_frag<B_K, BN>(smem + R64_SLOT_A, wn * WTN + 16 * j, 0, lane);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) af[i] = load_frag<A_K, BM>(smem, wm * WTM + 16 * i, 0, lane);
+
+#define NSA_R64_PHASE(BC, BNX, TA, TB, KKN)                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                              \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) {                                            \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j)                                            \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BC[j], af[i], acc[i][j], 0, 0, 0);   \
+    af[i] = load_frag<A_K, BM>((TA), wm * WTM + 16 * i, (KKN), lane);                         \
+    if (i < FN) BNX[i] = load_frag<B_K, BN>((TB), wn * WTN + 16 * i, (KKN), lane);            \
+  }                                                                                           \
+  __builtin_amdgcn_s_setprio(0);
+
+  for (int k = 0; k < nk; ++k) {
+    const char* ta = smem + (k & 1) * R64_SLOT;
+    const char* tn = smem + ((k + 1) & 1) * R64_SLOT;  // next slot (garbage reads past the end: discarded)
+    NSA_R64_PHASE(b0, b1, ta, ta + R64_SLOT_A, 1)
+    if (k + 1 < nk) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (k + 2 < nk) issue(k + 2);
+    NSA_R64_PHASE(b1, b0, tn, tn + R64_SLOT_A, 0)
+  }
+#undef NSA_R64_PHASE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ring_epilogue<EPI, DIRECT>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+}
+
 template <bool A_K, bool B_K, int EPI>
 hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   GemmArgs a = a0;
@@ -516,6 +696,14 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
     gemm_ring_kernel<A_K, B_K, EPI, 4, true><<<grid, NTHREADS, 0, s>>>(a);
   else if (variant == 4)
     gemm_ring_kernel<A_K, B_K, EPI, 5, true><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 5)
+    gemm_ring_kernel<A_K, B_K, EPI, 4, false, true><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 6)
+    gemm_ring_kernel<A_K, B_K, EPI, 4, true, true><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 7)
+    gemm_ring64_kernel<A_K, B_K, EPI, false><<<grid, NTHREADS, 0, s>>>(a);
+  else if (variant == 8)
+    gemm_ring64_kernel<A_K, B_K, EPI, true><<<grid, NTHREADS, 0, s>>>(a);
   else
     gemm_kernel<A_K, B_K, EPI><<<grid, NTHREADS, 0, s>>>(a);
   return hipGetLastError();
@@ -529,7 +717,9 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
 //      3 store acc * gelu'(U)
 // bits 8..15 of `epi` select the pipeline: 0 = register-staged BK=64 double buffer,
 // 1..4 = LDS-DMA ring (BK=32 slices): 1 = 4 slots (2 in flight) + LDS epilogue,
-// 2 = 5 slots + LDS epilogue, 3 = 4 slots + direct stores, 4 = 5 slots + direct stores
+// 2 = 5 slots + LDS epilogue, 3 = 4 slots + direct stores, 4 = 5 slots + direct stores,
+// 5/6 = pipelined ring (fragments of slice k+1 read under slice k's MFMAs), LDS / direct epilogue,
+// 7/8 = ring64 (64-deep slots, whole-line DMA rows, pipelined sub-slices), LDS / direct epilogue
 // (fragment double-buffering across slices was tried: 256 registers + 468 B/lane of
 // scratch at 2 waves/SIMD, so it is not kept)
 NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,

@@ -389,10 +389,10 @@ def linear(x, w, b=None, residual=None):
 # MLP: c_proj(gelu(c_fc(x))) with GELU fused into GEMM epilogues (MI355X path)
 # ----------------------------------------------------------------------------
 
-# GEMM-epilogue GELU fusion is correct (tests/test_kernels_gpu.py::test_fused_mlp) but
-# measured slower than hipBLASLt + the standalone GELU kernels at GPT-2 shapes
-# (profiles/: the erf tail runs with the MFMA pipes idle at 1 workgroup/CU), so it
-# is opt-in until the GEMM main loop overtakes hipBLASLt.
+# Whether the GELU rides in a GEMM epilogue is decided per shape by the tuner
+# (gemm_tune.fwd_gelu / dgrad_dgelu time the fused epilogues against the best GEMM +
+# the standalone GELU kernel).  FUSE_GELU_EPILOGUE=True forces the fused form
+# (tests/test_kernels_gpu.py::test_fused_mlp covers both).
 FUSE_GELU_EPILOGUE = False
 
 
@@ -412,9 +412,7 @@ class MLPFn(torch.autograd.Function):
         if FUSE_GELU_EPILOGUE:
             u, g = _gemm.fwd_gelu(x2, wf)
         else:
-            u = _tune.fwd(x2, wf)
-            g = torch.empty_like(u)
-            _lib.call("nsa_gelu_fwd", _lib.ptr(u), _lib.ptr(g), u.numel(), _lib.stream())
+            u, g = _tune.fwd_gelu(x2, wf)
         y = _tune.fwd(g, compute_weight(w_proj, x.dtype))
         ctx.save_for_backward(x2, u, g, w_fc, w_proj)
         ctx.xshape = x.shape
@@ -428,9 +426,7 @@ class MLPFn(torch.autograd.Function):
         if FUSE_GELU_EPILOGUE:
             du = _gemm.dgrad(dy2, wp, u=u)
         else:
-            dg = _tune.dgrad(dy2, wp)
-            du = torch.empty_like(dg)
-            _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
+            du = _tune.dgrad_dgelu(dy2, wp, u)
         gw_proj = weight_grad(w_proj, dy2, g)
         dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
         gw_fc = weight_grad(w_fc, du, x2)

@@ -24,8 +24,9 @@ LAYOUT_NT, LAYOUT_NN, LAYOUT_TN = 0, 1, 2
 EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
 BK = 64
 TILE = 256
-# pipeline variant: 0 = register-staged BK=64 double buffer, 1 = LDS-DMA ring (2 slices in flight)
-VARIANT = int(os.environ.get("NSA_GEMM_VARIANT", "1"))
+# pipeline variant (csrc/kernels/gemm.hip nsa_gemm): 0 = register-staged, 1-4 = 32-deep LDS-DMA ring,
+# 5/6 = pipelined ring, 7/8 = ring64 (default 7)
+VARIANT = int(os.environ.get("NSA_GEMM_VARIANT", "7"))
 
 
 def _check(t, name):

@@ -9,9 +9,17 @@ linear, the LDS-DMA ring kernel wins some input-gradient shapes (K-contiguous B
 operand, e.g. c_attn and the 50304-wide lm_head), and hipBLASLt wins the plain
 forwards — so the choice is per shape, not per op.
 
-Weight-gradient candidates are timed into a scratch buffer so the real
-accumulator is touched exactly once.  ``NSA_GEMM_BACKEND=nsa|hipblaslt`` pins a
-backend (tests, A/B runs).
+The MLP's activation can ride in a GEMM epilogue: ``fwd_gelu`` (u and gelu(u)
+from one pass) and ``dgrad_dgelu`` (dY·W scaled by gelu'(u)) time the fused
+epilogue variants of our kernel against "best GEMM + standalone GELU kernel",
+so a fusion is used exactly where it measures faster.
+
+Candidate names: ``hipblaslt``, ``nsa<v>`` (our kernel, pipeline variant v of
+``csrc/kernels/gemm.hip``: 1 = 32-deep LDS-DMA ring, 7/8 = 64-deep ring64 with
+LDS-staged / direct-store epilogue),
+``fused<v>`` (our kernel with the GELU epilogue).  Weight-gradient candidates are
+timed into a scratch buffer so the real accumulator is touched exactly once.
+``NSA_GEMM_BACKEND=nsa|hipblaslt`` pins a backend family (tests, A/B runs).
 """
 
 from __future__ import annotations
@@ -26,7 +34,7 @@ from . import gemm as _gemm
 
 F32 = torch.float32
 _table: dict = {}
-_lock = threading.Lock()
+_lock = threading.RLock()  # re-entrant: a "split" candidate tunes its inner GEMM while timed
 _loaded = False
 FORCE = os.environ.get("NSA_GEMM_BACKEND", "")
 
@@ -58,28 +66,48 @@ def _save():
         pass
 
 
-def _time(fn, reps=3):
-    fn()  # warm (first launch / JIT of kernels, cache state)
+NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
+WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
+
+
+def _time_all(candidates: dict, rounds=3, reps=3):
+    """Median-of-rounds time per candidate, rounds interleaved across candidates.
+
+    A candidate timed alone in a short burst runs at the boost clock the idle chip
+    grants; interleaving puts every candidate in the same power/thermal state, so
+    compute-bound and memory-bound candidates compare fairly.
+    """
+    names = list(candidates)
+    for n in names:  # warm: first launch, cache state
+        candidates[n]()
+    samples = {n: [] for n in names}
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps
+    for _ in range(rounds):
+        for n in names:
+            fn = candidates[n]
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            samples[n].append(e0.elapsed_time(e1) / reps)
+    return {n: sorted(v)[len(v) // 2] for n, v in samples.items()}
 
 
 def choose(key, candidates: dict) -> str:
     """Return the name of the fastest candidate for ``key`` (timed once, then cached)."""
     if FORCE:
-        return FORCE if FORCE in candidates else next(iter(candidates))
+        for name in candidates:
+            if name.startswith(FORCE) or (FORCE == "nsa" and name.startswith("fused")):
+                return name
+        return next(iter(candidates))
     _load()
     hit = _table.get(key)
     if hit in candidates:
         return hit
     with _lock:
-        times = {name: _time(fn) for name, fn in candidates.items()}
+        times = _time_all(candidates)
         best = min(times, key=times.get)
         _table[key] = best
         _save()
@@ -95,14 +123,20 @@ def _nsa_ok(*ts):
     return all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
 
 
+def _variant(name):
+    return int(name[-1])
+
+
 def fwd(x2, w):
     """y = x2 @ w^T (bf16)."""
     M, K = x2.shape
     N = w.shape[0]
     if not (_nsa_ok(x2, w) and _gemm.supported(M, N, K)):
         return x2 @ w.t()
-    name = choose(("fwd", M, N, K), {"hipblaslt": lambda: x2 @ w.t(), "nsa": lambda: _gemm.fwd(x2, w)})
-    return _gemm.fwd(x2, w) if name == "nsa" else x2 @ w.t()
+    cands = {"hipblaslt": lambda: x2 @ w.t()}
+    cands.update({f"nsa{v}": (lambda v=v: _gemm.fwd(x2, w, variant=v)) for v in NSA_VARIANTS})
+    name = choose(("fwd", M, N, K), cands)
+    return x2 @ w.t() if name == "hipblaslt" else _gemm.fwd(x2, w, variant=_variant(name))
 
 
 def dgrad(dy2, w):
@@ -111,8 +145,60 @@ def dgrad(dy2, w):
     K = w.shape[1]
     if not (_nsa_ok(dy2, w) and _gemm.supported(M, K, N)):
         return dy2 @ w
-    name = choose(("dgrad", M, N, K), {"hipblaslt": lambda: dy2 @ w, "nsa": lambda: _gemm.dgrad(dy2, w)})
-    return _gemm.dgrad(dy2, w) if name == "nsa" else dy2 @ w
+    cands = {"hipblaslt": lambda: dy2 @ w}
+    cands.update({f"nsa{v}": (lambda v=v: _gemm.dgrad(dy2, w, variant=v)) for v in NSA_VARIANTS})
+    name = choose(("dgrad", M, N, K), cands)
+    return dy2 @ w if name == "hipblaslt" else _gemm.dgrad(dy2, w, variant=_variant(name))
+
+
+def _gelu_fwd(u):
+    from . import _lib
+
+    g = torch.empty_like(u)
+    _lib.call("nsa_gelu_fwd", _lib.ptr(u), _lib.ptr(g), u.numel(), _lib.stream())
+    return g
+
+
+def _gelu_bwd(dg, u):
+    from . import _lib
+
+    du = torch.empty_like(dg)
+    _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
+    return du
+
+
+def fwd_gelu(x2, w):
+    """(u, gelu(u)) with u = x2 @ w^T: fused GEMM epilogue or GEMM + GELU kernel, whichever is faster."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if not (_nsa_ok(x2, w) and _gemm.supported(M, N, K)):
+        u = x2 @ w.t()
+        return u, _gelu_fwd(u)
+
+    def split():
+        u = fwd(x2, w)
+        return u, _gelu_fwd(u)
+
+    cands = {"split": split}
+    cands.update({f"fused{v}": (lambda v=v: _gemm.fwd_gelu(x2, w, variant=v)) for v in NSA_VARIANTS})
+    name = choose(("fwd_gelu", M, N, K), cands)
+    return split() if name == "split" else _gemm.fwd_gelu(x2, w, variant=_variant(name))
+
+
+def dgrad_dgelu(dy2, w, u):
+    """(dy2 @ w) * gelu'(u): fused GEMM epilogue or GEMM + GELU-backward kernel."""
+    M, N = dy2.shape
+    K = w.shape[1]
+    if not (_nsa_ok(dy2, w, u) and _gemm.supported(M, K, N)):
+        return _gelu_bwd(dy2 @ w, u)
+
+    def split():
+        return _gelu_bwd(dgrad(dy2, w), u)
+
+    cands = {"split": split}
+    cands.update({f"fused{v}": (lambda v=v: _gemm.dgrad(dy2, w, u=u, variant=v)) for v in NSA_VARIANTS})
+    name = choose(("dgrad_dgelu", M, N, K), cands)
+    return split() if name == "split" else _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
 
 
 def _hip_wgrad(dy2, x2, g32):
@@ -137,8 +223,10 @@ def wgrad_acc(dy2, x2, g32):
             fn(dy2, x2, scratch)
         return run
 
-    name = choose(("wgrad", T, N, K), {"hipblaslt": cand(_hip_wgrad), "nsa": cand(_gemm.wgrad_acc)})
-    if name == "nsa":
-        _gemm.wgrad_acc(dy2, x2, g32)
-    else:
+    cands = {"hipblaslt": cand(_hip_wgrad)}
+    cands.update({f"nsa{v}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, variant=v)) for v in WGRAD_VARIANTS})
+    name = choose(("wgrad", T, N, K), cands)
+    if name == "hipblaslt":
         _hip_wgrad(dy2, x2, g32)
+    else:
+        _gemm.wgrad_acc(dy2, x2, g32, variant=_variant(name))

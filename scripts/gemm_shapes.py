@@ -67,7 +67,7 @@ def main():
             "ours_fwd": lambda: nsa_gemm.fwd(x, w, variant=0),
             "ours_dx": lambda: nsa_gemm.dgrad(dy, w, variant=0),
             "ours_dW_acc": lambda: nsa_gemm.wgrad_acc(dy, x, mg, variant=0),
-            **{f"v{v}_{n}": f for v in (1, 2, 3, 4) for n, f in (
+            **{f"v{v}_{n}": f for v in (1, 2, 3, 4, 5, 6, 7, 8) for n, f in (
                 ("fwd", lambda v=v: nsa_gemm.fwd(x, w, variant=v)),
                 ("dx", lambda v=v: nsa_gemm.dgrad(dy, w, variant=v)),
                 ("dW", lambda v=v: nsa_gemm.wgrad_acc(dy, x, mg, variant=v)))},
