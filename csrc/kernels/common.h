@@ -38,6 +38,17 @@ struct __attribute__((aligned(16))) bf16v8 {
   bf16_t v[8];
 };
 
+__device__ __forceinline__ void unpack8(uint4 u, float (&f)[8]) {
+  f[0] = __uint_as_float(u.x << 16);
+  f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16);
+  f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16);
+  f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16);
+  f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
 __device__ __forceinline__ void load8(const bf16_t* p, float (&f)[8]) {
   uint4 u = *reinterpret_cast<const uint4*>(p);
   f[0] = __uint_as_float(u.x << 16);

@@ -1,6 +1,8 @@
 // Memory-bound elementwise kernels: exact-erf GELU fwd/bwd, hash dropout,
-// fp32 -> bf16 cast.  16-byte vector access per lane (8 bf16), grid capped at
-// 256 CUs x 8 blocks and grid-strided (cdna_hip_programming.md Guideline 11).
+// fp32 -> bf16 cast.  16-byte vector access per lane (8 bf16); each thread keeps
+// kUnroll independent 16-byte loads in flight (all loads of an iteration are
+// issued before any math), which lifted GELU from ~4.4 to HBM-rate; grid-strided
+// over 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11).
 //
 // nanoGPT MLP uses nn.GELU() — the exact erf form, not the tanh approximation
 // (SURVEY.md §2.3 U-M3, K4).
@@ -9,9 +11,10 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
 
 inline int grid_for(int64_t n_vec) {
-  int64_t g = (n_vec + kBlock - 1) / kBlock;
+  int64_t g = (n_vec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;
   return (int)g;
@@ -23,12 +26,25 @@ __device__ __forceinline__ float gelu_grad(float x) { return nsa_gelu_grad(x); }
 __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          int64_t n) {
   const int64_t nv = n / 8;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
-    float f[8];
-    load8(x + i * 8, f);
+  const int64_t stride = (int64_t)gridDim.x * kBlock * kUnroll;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock * kUnroll + threadIdx.x; i0 < nv; i0 += stride) {
+    uint4 u[kUnroll];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-    store8(y + i * 8, f);
+    for (int r = 0; r < kUnroll; ++r) {
+      const int64_t i = min(i0 + (int64_t)r * kBlock, nv - 1);
+      u[r] = *reinterpret_cast<const uint4*>(x + i * 8);
+    }
+#pragma unroll
+    for (int r = 0; r < kUnroll; ++r) {
+      const int64_t i = i0 + (int64_t)r * kBlock;
+      if (i < nv) {
+        float f[8];
+        unpack8(u[r], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+        store8(y + i * 8, f);
+      }
+    }
   }
   // scalar tail
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
@@ -38,13 +54,27 @@ __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restri
 __global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          bf16_t* __restrict__ dx, int64_t n) {
   const int64_t nv = n / 8;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
-    float g[8], f[8];
-    load8(dy + i * 8, g);
-    load8(x + i * 8, f);
+  const int64_t stride = (int64_t)gridDim.x * kBlock * kUnroll;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock * kUnroll + threadIdx.x; i0 < nv; i0 += stride) {
+    uint4 ug[kUnroll], ux[kUnroll];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = g[j] * gelu_grad(f[j]);
-    store8(dx + i * 8, f);
+    for (int r = 0; r < kUnroll; ++r) {
+      const int64_t i = min(i0 + (int64_t)r * kBlock, nv - 1);
+      ug[r] = *reinterpret_cast<const uint4*>(dy + i * 8);
+      ux[r] = *reinterpret_cast<const uint4*>(x + i * 8);
+    }
+#pragma unroll
+    for (int r = 0; r < kUnroll; ++r) {
+      const int64_t i = i0 + (int64_t)r * kBlock;
+      if (i < nv) {
+        float g[8], f[8];
+        unpack8(ug[r], g);
+        unpack8(ux[r], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = g[j] * gelu_grad(f[j]);
+        store8(dx + i * 8, f);
+      }
+    }
   }
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
     dx[i] = f2bf(bf2f(dy[i]) * gelu_grad(bf2f(x[i])));

@@ -11,8 +11,9 @@
 // dw = sum_rows dy*xhat, db = sum_rows dy are accumulated per lane in
 // registers across the rows a block visits, reduced across the block's 4
 // waves in LDS and written as one partial row per block; nsa_colsum_accum then
-// adds the partials into the fp32 flat gradient buffer (deterministic, no
-// atomics).
+// reduces the partial rows (split over row ranges, fp32 atomics) into the flat
+// gradient buffer.  Backward rows are software-pipelined (next row's loads in
+// flight while the current row is reduced).
 #include "common.h"
 
 namespace {
@@ -112,9 +113,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       dba[k][j] = 0.0f;
     }
   }
-  for (int row = blockIdx.x * 4 + wv; row < N; row += gridDim.x * 4) {
+  // Rows are software-pipelined: the next row's x / dy / dres vectors are loaded
+  // (as raw 16-byte words) while the current row is reduced and written, so each
+  // row costs one overlapped memory round trip instead of two dependent ones.
+  const int row_step = gridDim.x * 4;
+  int row = blockIdx.x * 4 + wv;
+  uint4 nx[NK], nd[NK], nr[NK];
+#define NSA_LNB_LOAD(R)                                                                  \
+  _Pragma("unroll") for (int k = 0; k < NK; ++k) {                                       \
+    const int c = min((k * 64 + lane) * 8, C - 8);                                       \
+    const int64_t off = (int64_t)min((R), N - 1) * C + c;                                \
+    nx[k] = *reinterpret_cast<const uint4*>(x + off);                                    \
+    nd[k] = *reinterpret_cast<const uint4*>(dy + off);                                   \
+    if (dres) nr[k] = *reinterpret_cast<const uint4*>(dres + off);                       \
+  }
+  NSA_LNB_LOAD(row)
+  for (; row < N; row += row_step) {
     const float mean = mean_in[row];
     const float rstd = rstd_in[row];
+    uint4 cx[NK], cd[NK], cr[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      cx[k] = nx[k];
+      cd[k] = nd[k];
+      cr[k] = nr[k];
+    }
+    NSA_LNB_LOAD(row + row_step)
     float xh[NK][8], g[NK][8];
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
@@ -122,8 +146,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
         float xv[8], dv[8];
-        load8(x + (int64_t)row * C + c, xv);
-        load8(dy + (int64_t)row * C + c, dv);
+        unpack8(cx[k], xv);
+        unpack8(cd[k], dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = (xv[j] - mean) * rstd;
@@ -146,7 +170,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
         if (dres) {  // gradient arriving through the residual path of the fused add
           float rv[8];
-          load8(dres + (int64_t)row * C + c, rv);
+          unpack8(cr[k], rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
@@ -154,6 +178,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
+#undef NSA_LNB_LOAD
   // block reduction of the per-lane dw/db partials (4 waves -> 1 row)
   for (int pass = 0; pass < 2; ++pass) {
     float* dst = pass == 0 ? dw_part : db_part;

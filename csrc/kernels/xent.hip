@@ -11,6 +11,12 @@
 //           small [N, C] side of the lm_head GEMMs).
 // row_loss[r] = logsumexp - logit[target] (0 for ignored rows, whose gradient
 // row is zeroed).  The [N, V] fp32 softmax never exists.
+//
+// For V <= 256 x 8 x kRegChunks (GPT-2's 50304) the row is held in registers
+// (xent_reg_kernel): every thread issues all its 16-byte loads at once (deep
+// memory parallelism), the reductions and the gradient come from registers, and
+// HBM sees exactly one read and one write of the logits (the streaming kernel
+// re-reads the row and depends on it still being in L2).
 #include "common.h"
 
 namespace {
@@ -95,11 +101,96 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
   }
 }
 
+constexpr int kRegChunks = 25;  // 16-byte chunks per thread: rows up to 51200 bf16 logits
+
+__device__ __forceinline__ float block_reduce_max(float v, float* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+
+__device__ __forceinline__ float block_reduce_sum(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) r += red[w];
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void xent_reg_kernel(bf16_t* __restrict__ logits,
+                                                         const int64_t* __restrict__ targets,
+                                                         float* __restrict__ row_loss, int V, int write_grad) {
+  const int row = blockIdx.x;
+  bf16_t* lr = logits + (int64_t)row * V;
+  const int64_t tgt = targets[row];
+  const bool valid = tgt >= 0 && tgt < V;
+  const int nv = V / 8;
+  __shared__ float red[kBlock / 64];
+  // all loads first (clamped index, no branch around a load), then compute
+  uint4 r[kRegChunks];
+#pragma unroll
+  for (int c = 0; c < kRegChunks; ++c) {
+    const int i = min((int)threadIdx.x + c * kBlock, nv - 1);
+    r[c] = *reinterpret_cast<const uint4*>(lr + (int64_t)i * 8);
+  }
+  const float tgt_logit = valid ? bf2f(lr[tgt]) : 0.0f;
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < kRegChunks; ++c) {
+    if ((int)threadIdx.x + c * kBlock < nv) {
+      const uint32_t w4[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        m = fmaxf(m, fmaxf(__uint_as_float(w4[q] << 16), __uint_as_float(w4[q] & 0xffff0000u)));
+    }
+  }
+  const float M = block_reduce_max(m, red);
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < kRegChunks; ++c) {
+    if ((int)threadIdx.x + c * kBlock < nv) {
+      const uint32_t w4[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        s += __expf(__uint_as_float(w4[q] << 16) - M) + __expf(__uint_as_float(w4[q] & 0xffff0000u) - M);
+    }
+  }
+  const float S = block_reduce_sum(s, red);
+  if (threadIdx.x == 0) row_loss[row] = valid ? M + __logf(S) - tgt_logit : 0.0f;
+  if (!write_grad) return;
+  const float invS = 1.0f / S;
+#pragma unroll
+  for (int c = 0; c < kRegChunks; ++c) {
+    const int i = (int)threadIdx.x + c * kBlock;
+    if (i < nv) {
+      const uint32_t w4[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+      float f[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f[2 * q] = valid ? __expf(__uint_as_float(w4[q] << 16) - M) * invS : 0.0f;
+        f[2 * q + 1] = valid ? __expf(__uint_as_float(w4[q] & 0xffff0000u) - M) * invS : 0.0f;
+      }
+      if (valid && (tgt >> 3) == i) f[tgt & 7] -= 1.0f;
+      store8(lr + (int64_t)i * 8, f);
+    }
+  }
+}
+
 }  // namespace
 
 NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int write_grad,
                                 hipStream_t s) {
-  if (V % 8 == 0)
+  if (V % 8 == 0 && V <= kBlock * 8 * kRegChunks)
+    xent_reg_kernel<<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
+  else if (V % 8 == 0)
     xent_kernel<true><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
   else
     xent_kernel<false><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V,
