@@ -50,7 +50,7 @@ TRAIN_DEFAULTS = dict(
     # system
     device="cuda",
     dtype="bfloat16",
-    compile=True,  # no Triton/Inductor here: True = capture the optimizer step in a HIP graph
+    compile=True,  # no Triton/Inductor here: True = capture the fwd+bwd micro-step as a HIP graph
     # ---- keys added by nanosandbox_amd (all typed) ----
     data_dir="",  # root holding <dataset>/train.bin; '' -> ./data (nanoGPT) ; k8s: /data/datasets
     seed=1337,

@@ -1,0 +1,72 @@
+"""HIP-graph capture of one training micro-step (``compile=True``).
+
+nanoGPT's ``compile=True`` runs ``torch.compile`` (Inductor/Triton).  This stack
+has no tracing compiler: the hot ops are already fused HIP kernels.  What a
+compiler would still buy is the removal of per-kernel host overhead, and on
+MI355X that is exactly what a HIP graph does.  The forward, the loss scaling and
+the backward of one micro-step (~1,000 kernel launches at GPT-2 124M) are
+captured once into a ``torch.cuda.CUDAGraph`` (hipGraph on ROCm) and replayed
+for every micro-step, with the batch copied into static input buffers.
+
+Why it is sound here:
+* every parameter gradient accumulates into the flat fp32 buffer
+  (``param.main_grad``) from inside our autograd ops; torch's AccumulateGrad is
+  never involved, so replaying the captured backward gas times accumulates
+  exactly like gas eager backwards;
+* weights are read through the static bf16 shadow buffer that the optimizer
+  refreshes in place, and the learning rate lives in the (eager) optimizer step;
+* the GEMM autotuner is warmed up before capture, so no timing runs are captured.
+
+When it is not used (eager fallback, decided by ``graph_capture_supported``):
+dropout > 0 (the counter-based dropout seeds are host values and would be baked
+into the graph), more than one rank (bucket-ready hooks are Python callbacks),
+CPU devices.
+"""
+
+from __future__ import annotations
+
+import torch
+
+
+def graph_capture_supported(device: str, dropout: float, world_size: int) -> tuple[bool, str]:
+    if not str(device).startswith("cuda") or not torch.cuda.is_available():
+        return False, "graph capture needs a GPU device"
+    if dropout > 0.0:
+        return False, "dropout > 0: per-step dropout seeds cannot be baked into a graph"
+    if world_size > 1:
+        return False, "world_size > 1: gradient-bucket hooks run in Python during backward"
+    return True, ""
+
+
+class MicroStepGraph:
+    """Captured ``loss = model(X, Y)[1] / gas; loss.backward()``, replayed per micro-step."""
+
+    def __init__(self, model, X: torch.Tensor, Y: torch.Tensor, gas: int, warmup: int = 2, zero_grad=None):
+        self.model = model
+        self.gas = gas
+        self.X = X.detach().clone()
+        self.Y = Y.detach().clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):  # tuner timing runs, allocator warm-up, lazy init
+                _, loss = model(self.X, self.Y)
+                (loss / gas).backward()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if zero_grad is not None:
+            zero_grad()  # the warm-up backwards accumulated into the gradient buffer
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            _, loss = model(self.X, self.Y)
+            self.loss = loss / gas
+            self.loss.backward()
+        self.replays = 0
+
+    def run(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+        """Copy the batch into the static inputs and replay; returns the (static) scaled loss."""
+        self.X.copy_(X, non_blocking=True)
+        self.Y.copy_(Y, non_blocking=True)
+        self.graph.replay()
+        self.replays += 1
+        return self.loss

@@ -29,6 +29,7 @@ import torch
 
 from .config import TRAIN_DEFAULTS, config_keys, parse_argv
 from .data import load_meta, make_batch_source, resolve_data_dir
+from .runtime import MicroStepGraph, graph_capture_supported
 from .models import GPT, GPTConfig
 from .optim import FlatParamStore
 from .parallel import FlatBucketReducer, destroy, init_distributed
@@ -125,8 +126,15 @@ class Trainer:
         if init_from == "resume" and checkpoint is not None:
             self.optimizer.load_state_dict(checkpoint["optimizer"])
         checkpoint = None  # free up memory
+        # compile=True: no Triton/Inductor on this stack; the micro-step (forward +
+        # backward) is captured once as a HIP graph and replayed (runtime/hipgraph.py)
+        self.graph = None
+        self.use_graph = False
         if c["compile"]:
-            print("compile=True: no Triton/Inductor on this stack; hot ops already run as fused HIP kernels")
+            ok, why = graph_capture_supported(self.device, c["dropout"], info.world_size)
+            self.use_graph = ok
+            print("compile=True: micro-step captured as a HIP graph" if ok
+                  else f"compile=True: eager micro-steps ({why})")
 
         # ----------------------------------------------------------------- DDP
         self.raw_model = model
@@ -185,6 +193,17 @@ class Trainer:
 
         Returns (last micro-step loss tensor, grad-norm tensor or None, next X, next Y)."""
         c = self.cfg
+        if self.use_graph:
+            if self.graph is None:
+                self.graph = MicroStepGraph(self.model, X, Y, self.gas,
+                                            zero_grad=lambda: self.optimizer.zero_grad(set_to_none=True))
+            for _ in range(self.gas):
+                loss = self.graph.run(X, Y)
+                X, Y = self.batches.get_batch("train")
+            norm = self.optimizer.clip_grad_norm_(c["grad_clip"]) if c["grad_clip"] != 0.0 else None
+            self.optimizer.step()
+            self.optimizer.zero_grad(set_to_none=True)
+            return loss, norm, X, Y
         for micro_step in range(self.gas):
             sync = micro_step == self.gas - 1
             if self.reducer is not None:

@@ -50,3 +50,29 @@ def test_train_and_resume(kernels, tmp_path):
     for i, s in sd["optimizer"]["state"].items():
         assert torch.equal(st[i]["exp_avg"].cpu(), s["exp_avg"])
     tr2.fit()
+
+
+def test_compile_hip_graph_matches_eager(kernels, tmp_path):
+    """compile=True captures the fwd+bwd micro-step as a HIP graph; training must track eager."""
+    from nanosandbox_amd.train import Trainer
+
+    def run(compile_):
+        torch.manual_seed(0)
+        tr = Trainer(_cfg(tmp_path, compile=compile_, dropout=0.0, bias=False, max_iters=8, eval_interval=1000,
+                          out_dir=str(tmp_path / f"o{int(compile_)}"), seed=1234))
+        X, Y = tr.batches.get_batch("train")
+        losses = []
+        for it in range(6):
+            for g in tr.optimizer.param_groups:
+                g["lr"] = 1e-3
+            loss, _, X, Y = tr.train_step(X, Y)
+            losses.append(loss.item() * tr.gas)
+        return tr, losses
+
+    tg, lg = run(True)
+    te, le = run(False)
+    assert tg.use_graph and tg.graph is not None and tg.graph.replays == 6 * tg.gas
+    assert not te.use_graph
+    for a, b in zip(lg, le):
+        assert abs(a - b) < 2e-2 * abs(b), (lg, le)
+    assert lg[-1] < lg[0]
