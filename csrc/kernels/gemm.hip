@@ -681,6 +681,245 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring64_kernel(GemmArgs g) {
   ring_epilogue<EPI, DIRECT>(g, acc, smem, m0, n0, wm, wn, lane, wave);
 }
 
+// ---------------------------------------------------------------------------
+// Variants 9/10 ("p8": phase-paired, persistent).  cdna_hip_programming.md §5's
+// 256² 8-phase structure, re-derived for the GPT layouts (A K-contiguous:
+// forward NT and input-grad NN):
+//  * a K-tile (64 deep, 64 KiB: A image [256][64] kimg + B image) is computed in
+//    4 PHASES of 16 MFMAs, one 64x32 output quadrant (qm, qn) per phase, in the
+//    order (0,0) (0,1) (1,1) (1,0); fragments are read from LDS at the head of
+//    the phase that uses them: p0 A[qm0]+B[qn0], p1 B[qn1], p2 A[qm1], p3 none
+//    (B[qn0] kept in a second register set);
+//  * each K-tile is staged as 4 HALF-TILES of 16 KiB (2 LDS-DMA per thread), one
+//    per phase, issued 6 phases ahead in the order  A0 B0 B1 A1  where A0/A1 are
+//    the rows of quadrant qm = 0/1 and B0/B1 the columns of qn = 0/1 (K-contiguous
+//    B) or the k rows 0-31/32-63 (B stored [K][N]) — every DMA row a whole line.
+//    A half-tile's slot was last read 2+ phases before its refill is issued
+//    (A0 <- p0, B0 <- p0 / p1, B1 <- p1, A1 <- p2), and every phase ends its DMA
+//    issue with a counted vmcnt that retires the half-tile issued 4 phases
+//    earlier (3 stay in flight); a half-tile is read >= 1 phase after that wait;
+//  * 8 waves = 2 groups (wm = 0/1, one wave of each per SIMD) staggered by one
+//    barrier: each phase is [reads + DMA + vmcnt | barrier | 16 MFMA | barrier],
+//    so one group's LDS reads run beside the other group's MFMAs on every SIMD
+//    (MI355X_MICROARCH.md "Two waves per SIMD"); raw s_barrier only (a
+//    __syncthreads would drain the DMA with vmcnt(0));
+//  * persistent: grid = min(tiles, 256); the next tile's first 6 half-tiles are
+//    issued before this tile's epilogue, which stores straight from registers,
+//    so the K-loop prologue hides under the stores.  Tiles are walked in a
+//    grouped order (GM row-blocks x all columns) inside each XCD's contiguous
+//    share (bijective remap: blocks b, b+8, ... share an XCD).
+// Measured (scripts/gemm_ab.py, M = 122880, random operands, profiles/r1_gemm_p8_probes.md):
+// the structure alone (NSA_P8_PROBE_NODMA) runs 1650 TF/s at K = 3072, but with
+// the LDS-DMA staging it is ~1000 TF/s (hipBLASLt 1300); not waiting on vmcnt
+// (NSA_P8_PROBE_NOWAIT) or L2-resident operands (NSA_P8_PROBE_L2) recover <5 %,
+// one DMA piece per phase instead of two (NSA_P8_PIECES=1) ~8 %: the cost is
+// the DMA's presence in the read segments, not its latency or HBM traffic.
+// Kept as an autotuner candidate / experiment, not selected by default.
+// ---------------------------------------------------------------------------
+#ifndef NSA_P8_PIECES
+#define NSA_P8_PIECES 2  // DMA pieces per wave and half-tile (1 = timing probe, half the bytes)
+#endif
+constexpr int P8_HALF = 16384;               // bytes per half-tile
+constexpr int P8_BUF = 4 * P8_HALF;          // one K-tile: A image (32 KiB) + B image (32 KiB)
+constexpr int P8_SMEM = 2 * P8_BUF;          // 128 KiB
+constexpr int P8_GM = 4;                     // grouped tile order: row-blocks per group
+
+__device__ __forceinline__ void p8_wait(int inflight) {
+#ifdef NSA_P8_PROBE_NOWAIT
+  if (inflight > 0) return;  // timing probe: only the drains at the end of a tile wait
+#endif
+  // vmcnt = 2 DMA instructions per half-tile still allowed in flight
+  if (inflight >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (inflight == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (inflight == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (inflight == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void p8_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool B_K, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[P8_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nk = g.K / 64;
+  const int nh = 4 * nk;  // half-tiles per output tile
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // DMA geometry of the 4 half-tile kinds (2 pieces of 1 KiB per wave each),
+  // computed per issue (wave-uniform bases + lane bits: no live registers).
+  // A (kimg [256][64], 128-B rows): half qh = rows (r >> 6 & 1) == qh, piece pc
+  // (16 per half) = 8 rows.  B K-contiguous: half qh = rows wn*64 + qh*32 + [0,32).
+  // B [K][N] (rimg<256>, 512-B rows): half kh = k rows kh*32 + [0,32), 2 rows/piece.
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int G = gridDim.x;
+  auto tile_of = [&](int seq, int& m0, int& n0) {
+    // bijective XCD remap of the virtual grid [0, tiles), then grouped order
+    const int xcd = seq % 8, q = tiles / 8, r = tiles % 8;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + seq / 8;
+    const int grp = t / (P8_GM * g.tiles_n);
+    const int first = grp * P8_GM;
+    const int gm = min(P8_GM, g.tiles_m - first);
+    const int in = t - grp * P8_GM * g.tiles_n;
+    m0 = (first + in % gm) * BM;
+    n0 = (in / gm) * BN;
+  };
+
+  // issue half-tile h (= 4 * ktile + kind) of the tile at (m0, n0)
+  auto issue = [&](int h, int m0, int n0) {
+    const int kt = h >> 2, kind = h & 3;
+#ifdef NSA_P8_PROBE_L2
+    const int k0 = 0;  // timing probe: every K-tile re-reads the first one (L2-resident operands)
+#else
+    const int k0 = kt * 64;
+#endif
+    const uint32_t buf = lds0 + (uint32_t)((kt & 1) * P8_BUF);
+#ifdef NSA_P8_PROBE_NODMA
+    return;  // timing probe: no staging at all (wrong results)
+#endif
+    if (kind == 0 || kind == 3) {
+      const int qh = kind == 3;
+#pragma unroll
+      for (int j = 0; j < NSA_P8_PIECES; ++j) {
+        const int pc = wave * 2 + j;
+        const int rb = (pc >> 3) * 128 + qh * 64 + (pc & 7) * 8;  // wave-uniform
+        const int row = rb + (lane >> 3);
+        const int col = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+        const bf16_t* src = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + col;
+        glds16(src, __builtin_amdgcn_readfirstlane(buf + (uint32_t)(rb * 128)));
+      }
+    } else {
+      const int qh = kind == 2;
+#pragma unroll
+      for (int j = 0; j < NSA_P8_PIECES; ++j) {
+        const int pc = wave * 2 + j;
+        const bf16_t* src;
+        uint32_t off;
+        if constexpr (B_K) {
+          const int rb = (pc >> 2) * 64 + qh * 32 + (pc & 3) * 8;
+          const int row = rb + (lane >> 3);
+          const int col = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+          src = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + col;
+          off = (uint32_t)(rb * 128);
+        } else {
+          const int kb = qh * 32 + pc * 2;
+          const int krow = kb + (lane >> 5);
+          const int gg = (krow & 3) | (((krow >> 3) & 1) << 2);
+          const int col = ((lane & 31) ^ (2 * gg)) * 8;
+          src = g.B + (int64_t)(k0 + krow) * g.ldb + min(n0 + col, g.N - 8);
+          off = (uint32_t)(kb * 512);
+        }
+        glds16(src, __builtin_amdgcn_readfirstlane(buf + 2 * P8_HALF + off));
+      }
+    }
+  };
+  auto prologue = [&](int m0, int n0) {
+    const int pre = min(6, nh);
+    for (int h = 0; h < pre; ++h) issue(h, m0, n0);
+  };
+
+  int seq = blockIdx.x;
+  if (seq >= tiles) return;
+  int m0, n0;
+  tile_of(seq, m0, n0);
+  prologue(m0, n0);
+
+  while (true) {
+    // K-tile 0 resident (half-tiles 0..3); 4 and 5 may stay in flight
+    p8_wait(min(6, nh) - 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    p8_barrier();
+    if (wm == 1) p8_barrier();  // stagger: group 1 runs one barrier behind group 0
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* ta = smem + (kt & 1) * P8_BUF;
+      const char* tb = ta + 2 * P8_HALF;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int P = 4 * kt + p;
+        // ---- LDS reads of this phase's fragments
+        if (p == 0 || p == 2) {
+          const int qm = p >> 1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              af[i][kk] = load_frag<true, BM>(ta, wm * WTM + qm * 64 + 16 * i, kk, lane);
+        }
+        if (p == 0) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) b0f[j][kk] = load_frag<B_K, BN>(tb, wn * WTN + 16 * j, kk, lane);
+        }
+        if (p == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              b1f[j][kk] = load_frag<B_K, BN>(tb, wn * WTN + 32 + 16 * j, kk, lane);
+        }
+        // ---- DMA of half-tile P + 6, then retire what phase P + 1 reads: half-tile
+        // P + 2 (issued 4 phases ago; 3 stay in flight) — or P + 3 when B is stored
+        // [K][N]: its k-halves are kinds 1 and 2 and phase 0 reads both
+        if (P + 6 < nh) issue(P + 6, m0, n0);
+        if constexpr (B_K)
+          p8_wait(min(4, max(0, nh - P - 3)));
+        else
+          p8_wait(min(3, max(0, nh - P - 4)));
+        p8_barrier();
+        // ---- 16 MFMAs of quadrant (qm, qn): (0,0) (0,1) (1,1) (1,0)
+        __builtin_amdgcn_s_setprio(1);
+        {
+          const int qm = p >> 1;
+          const bool q1 = (p == 1 || p == 2);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int kk = 0; kk < 2; ++kk) {
+                const bf16x8 bb = q1 ? b1f[j][kk] : b0f[j][kk];
+                acc[qm * 4 + i][(q1 ? 2 : 0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    bb, af[i][kk], acc[qm * 4 + i][(q1 ? 2 : 0) + j], 0, 0, 0);
+              }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        p8_barrier();
+      }
+    }
+    if (wm == 0) p8_barrier();  // close the stagger: both groups at the same barrier count
+    // every wave's reads of both buffers are complete: the next tile may refill them
+    const int nseq = seq + G;
+    int nm0 = 0, nn0 = 0;
+    const bool more = nseq < tiles;
+    if (more) {
+      tile_of(nseq, nm0, nn0);
+      prologue(nm0, nn0);
+    }
+    ring_epilogue<EPI, true>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+    if (!more) break;
+    // stores and the prologue DMA share vmcnt: retire everything before the loop's wait
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    seq = nseq;
+    m0 = nm0;
+    n0 = nn0;
+  }
+}
+
 template <bool A_K, bool B_K, int EPI>
 hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   GemmArgs a = a0;
@@ -688,6 +927,16 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.k_per_split = a.K / splits;
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
+  if constexpr (A_K && EPI != EPI_ATOMIC_F32) {
+    if (variant == 9 || variant == 10) {
+      if (splits != 1) return hipErrorInvalidValue;
+      const int tiles = a.tiles_m * a.tiles_n;
+      const int g = variant == 9 ? (tiles < 256 ? tiles : 256) : tiles;
+      gemm_p8_kernel<B_K, EPI><<<dim3(g), NTHREADS, 0, s>>>(a);
+      return hipGetLastError();
+    }
+  }
+  if (variant == 9 || variant == 10) variant = 7;  // TN (weight grad): the ring64 kernel
   if (variant == 1)
     gemm_ring_kernel<A_K, B_K, EPI, 4, false><<<grid, NTHREADS, 0, s>>>(a);
   else if (variant == 2)
