@@ -716,6 +716,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring64_kernel(GemmArgs g) {
 // the DMA's presence in the read segments, not its latency or HBM traffic.
 // Kept as an autotuner candidate / experiment, not selected by default.
 // ---------------------------------------------------------------------------
+#ifndef NSA_P8_DMA_POS
+#define NSA_P8_DMA_POS 0  // where a phase issues its DMA: 0 after its LDS reads, 1 before them, 2 in its MFMAs
+#endif
 #ifndef NSA_P8_PIECES
 #define NSA_P8_PIECES 2  // DMA pieces per wave and half-tile (1 = timing probe, half the bytes)
 #endif
@@ -850,6 +853,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int P = 4 * kt + p;
+#if NSA_P8_DMA_POS == 1
+        if (P + 6 < nh) issue(P + 6, m0, n0);  // probe: DMA ahead of the fragment reads
+#endif
         // ---- LDS reads of this phase's fragments
         if (p == 0 || p == 2) {
           const int qm = p >> 1;
@@ -875,11 +881,25 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
         // ---- DMA of half-tile P + 6, then retire what phase P + 1 reads: half-tile
         // P + 2 (issued 4 phases ago; 3 stay in flight) — or P + 3 when B is stored
         // [K][N]: its k-halves are kinds 1 and 2 and phase 0 reads both
+#if NSA_P8_DMA_POS == 0
         if (P + 6 < nh) issue(P + 6, m0, n0);
         if constexpr (B_K)
           p8_wait(min(4, max(0, nh - P - 3)));
         else
           p8_wait(min(3, max(0, nh - P - 4)));
+#elif NSA_P8_DMA_POS == 1
+        if constexpr (B_K)
+          p8_wait(min(4, max(0, nh - P - 3)));
+        else
+          p8_wait(min(3, max(0, nh - P - 4)));
+#else
+        // probe: this phase's DMA is issued inside its MFMA cluster (below), so it is
+        // not yet among the younger operations here
+        if constexpr (B_K)
+          p8_wait(min(3, max(0, nh - P - 3)));
+        else
+          p8_wait(min(2, max(0, nh - P - 4)));
+#endif
         p8_barrier();
         // ---- 16 MFMAs of quadrant (qm, qn): (0,0) (0,1) (1,1) (1,0)
         __builtin_amdgcn_s_setprio(1);
@@ -895,6 +915,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
                 const bf16x8 bb = q1 ? b1f[j][kk] : b0f[j][kk];
                 acc[qm * 4 + i][(q1 ? 2 : 0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                     bb, af[i][kk], acc[qm * 4 + i][(q1 ? 2 : 0) + j], 0, 0, 0);
+#if NSA_P8_DMA_POS == 2
+                if (i == 0 && j == 1 && kk == 1 && P + 6 < nh) issue(P + 6, m0, n0);
+#endif
               }
         }
         __builtin_amdgcn_s_setprio(0);

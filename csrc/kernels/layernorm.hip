@@ -86,36 +86,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int NK>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+#ifndef NSA_LNB_MINW
+#define NSA_LNB_MINW 1  // min waves per SIMD (a tighter budget spills: the kernel needs ~130 VGPRs)
+#endif
+// PIPE: the next row's x / dy / dres vectors are loaded (as raw 16-byte words)
+// while the current row is reduced and written (one overlapped memory round trip
+// per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
+// xhat and dy*w are recomputed from the raw words in the second pass rather than
+// kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
+template <int NK, bool PIPE>
+__global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
                                                     const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
                                                     bf16_t* __restrict__ dx,
                                                     float* __restrict__ dw_part, float* __restrict__ db_part, int N,
                                                     int C) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
+  // dw / db partial sums live in LDS, one [C] slice per wave (no sharing inside
+  // the row loop): 2 x [4][C] fp32.  Keeping them in registers cost 32 VGPRs.
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  float* accw = red + (threadIdx.x >> 6) * C;
+  float* accb = red + 4 * C + (threadIdx.x >> 6) * C;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  float wf[NK][8];
-  float dwa[NK][8], dba[NK][8];
+  uint4 wraw[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    const int c = (k * 64 + lane) * 8;
-    if (c < C) {
-      load8(w + c, wf[k]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) wf[k][j] = 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dwa[k][j] = 0.0f;
-      dba[k][j] = 0.0f;
+    const int c = min((k * 64 + lane) * 8, C - 8);
+    wraw[k] = *reinterpret_cast<const uint4*>(w + c);
+    if ((k * 64 + lane) * 8 < C) {
+      *reinterpret_cast<float4*>(accw + (k * 64 + lane) * 8) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(accw + (k * 64 + lane) * 8 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(accb + (k * 64 + lane) * 8) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(accb + (k * 64 + lane) * 8 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // Rows are software-pipelined: the next row's x / dy / dres vectors are loaded
-  // (as raw 16-byte words) while the current row is reduced and written, so each
-  // row costs one overlapped memory round trip instead of two dependent ones.
   const int row_step = gridDim.x * 4;
   int row = blockIdx.x * 4 + wv;
   uint4 nx[NK], nd[NK], nr[NK];
@@ -127,8 +131,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     nd[k] = *reinterpret_cast<const uint4*>(dy + off);                                   \
     if (dres) nr[k] = *reinterpret_cast<const uint4*>(dres + off);                       \
   }
-  NSA_LNB_LOAD(row)
+  if (PIPE) NSA_LNB_LOAD(row)
   for (; row < N; row += row_step) {
+    if (!PIPE) NSA_LNB_LOAD(row)
     const float mean = mean_in[row];
     const float rstd = rstd_in[row];
     uint4 cx[NK], cd[NK], cr[NK];
@@ -138,25 +143,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       cd[k] = nd[k];
       cr[k] = nr[k];
     }
-    NSA_LNB_LOAD(row + row_step)
-    float xh[NK][8], g[NK][8];
+    if (PIPE) NSA_LNB_LOAD(row + row_step)
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
-        float xv[8], dv[8];
+        float xv[8], dv[8], wf[8], aw[8], ab[8];
         unpack8(cx[k], xv);
         unpack8(cd[k], dv);
+        unpack8(wraw[k], wf);
+        float4* pw = reinterpret_cast<float4*>(accw + c);
+        float4* pb = reinterpret_cast<float4*>(accb + c);
+        *reinterpret_cast<float4*>(aw) = pw[0];
+        *reinterpret_cast<float4*>(aw + 4) = pw[1];
+        *reinterpret_cast<float4*>(ab) = pb[0];
+        *reinterpret_cast<float4*>(ab + 4) = pb[1];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[k][j] = (xv[j] - mean) * rstd;
-          g[k][j] = dv[j] * wf[k][j];
-          s1 += g[k][j];
-          s2 += g[k][j] * xh[k][j];
-          dwa[k][j] += dv[j] * xh[k][j];
-          dba[k][j] += dv[j];
+          const float xh = (xv[j] - mean) * rstd;
+          const float g = dv[j] * wf[j];
+          s1 += g;
+          s2 += g * xh;
+          aw[j] += dv[j] * xh;
+          ab[j] += dv[j];
         }
+        pw[0] = *reinterpret_cast<float4*>(aw);
+        pw[1] = *reinterpret_cast<float4*>(aw + 4);
+        pb[0] = *reinterpret_cast<float4*>(ab);
+        pb[1] = *reinterpret_cast<float4*>(ab + 4);
       }
     }
     const float m1 = wave_sum(s1) / (float)C;
@@ -165,9 +180,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int k = 0; k < NK; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
-        float o[8];
+        float xv[8], dv[8], wf[8], o[8];
+        unpack8(cx[k], xv);
+        unpack8(cd[k], dv);
+        unpack8(wraw[k], wf);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[j] * wf[j] - m1 - (xv[j] - mean) * rstd * m2);
         if (dres) {  // gradient arriving through the residual path of the fused add
           float rv[8];
           unpack8(cr[k], rv);
@@ -179,22 +197,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
   }
 #undef NSA_LNB_LOAD
-  // block reduction of the per-lane dw/db partials (4 waves -> 1 row)
-  for (int pass = 0; pass < 2; ++pass) {
-    float* dst = pass == 0 ? dw_part : db_part;
-    if (dst == nullptr) continue;
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      const int c = (k * 64 + lane) * 8;
-      if (c < C) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) red[wv * C + c + j] = pass == 0 ? dwa[k][j] : dba[k][j];
-      }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256)
-      dst[(int64_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
-    __syncthreads();
+  (void)wv;
+  // block reduction of the per-wave dw/db slices (4 waves -> 1 partial row)
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    dw_part[(int64_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
+    if (db_part)
+      db_part[(int64_t)blockIdx.x * C + c] = red[4 * C + c] + red[5 * C + c] + red[6 * C + c] + red[7 * C + c];
   }
 }
 
@@ -211,10 +220,17 @@ template <int NK>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd,
                       const void* dres, void* dx, void* dw_part, void* db_part, int N, int C, int nblk,
                       hipStream_t s) {
-  ln_bwd_kernel<NK><<<nblk, 256, 4 * C * sizeof(float), s>>>(
-      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-      (const bf16_t*)dres, (bf16_t*)dx,
-      (float*)dw_part, (float*)db_part, N, C);
+  // bit 30 of nblk selects the non-pipelined body (A/B timing)
+  const bool pipe = !(nblk & (1 << 30));
+  nblk &= ~(1 << 30);
+  if (pipe)
+    ln_bwd_kernel<NK, true><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+        (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+        (const bf16_t*)dres, (bf16_t*)dx, (float*)dw_part, (float*)db_part, N, C);
+  else
+    ln_bwd_kernel<NK, false><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+        (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+        (const bf16_t*)dres, (bf16_t*)dx, (float*)dw_part, (float*)db_part, N, C);
   return hipGetLastError();
 }
 

@@ -101,8 +101,13 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
   }
 }
 
-constexpr int kRegChunks = 25;  // 16-byte chunks per thread: rows up to 51200 bf16 logits
+// Register-resident variants: RB threads per row, RC 16-byte chunks per thread
+// (rows up to RB * 8 * RC logits).  Fewer chunks per thread = fewer VGPRs = more
+// rows in flight per CU: the load phase of one row overlaps the exp / store phase
+// of the others (a 256 x 25 block is VGPR-limited to 2 rows per CU).
+constexpr int kRegChunks = 25;  // 256 threads: rows up to 51200 bf16 logits
 
+template <int RB>
 __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   v = wave_max(v);
   __syncthreads();
@@ -110,10 +115,11 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   __syncthreads();
   float r = red[0];
 #pragma unroll
-  for (int w = 1; w < kBlock / 64; ++w) r = fmaxf(r, red[w]);
+  for (int w = 1; w < RB / 64; ++w) r = fmaxf(r, red[w]);
   return r;
 }
 
+template <int RB>
 __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   v = wave_sum(v);
   __syncthreads();
@@ -121,13 +127,16 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   __syncthreads();
   float r = red[0];
 #pragma unroll
-  for (int w = 1; w < kBlock / 64; ++w) r += red[w];
+  for (int w = 1; w < RB / 64; ++w) r += red[w];
   return r;
 }
 
-__global__ __launch_bounds__(kBlock) void xent_reg_kernel(bf16_t* __restrict__ logits,
-                                                         const int64_t* __restrict__ targets,
-                                                         float* __restrict__ row_loss, int V, int write_grad) {
+template <int RB, int RC>
+__global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logits,
+                                                     const int64_t* __restrict__ targets,
+                                                     float* __restrict__ row_loss, int V, int write_grad) {
+  constexpr int kBlock = RB;
+  constexpr int kRegChunks = RC;
   const int row = blockIdx.x;
   bf16_t* lr = logits + (int64_t)row * V;
   const int64_t tgt = targets[row];
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void xent_reg_kernel(bf16_t* __restrict__ l
         m = fmaxf(m, fmaxf(__uint_as_float(w4[q] << 16), __uint_as_float(w4[q] & 0xffff0000u)));
     }
   }
-  const float M = block_reduce_max(m, red);
+  const float M = block_reduce_max<RB>(m, red);
   float s = 0.0f;
 #pragma unroll
   for (int c = 0; c < kRegChunks; ++c) {
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void xent_reg_kernel(bf16_t* __restrict__ l
         s += __expf(__uint_as_float(w4[q] << 16) - M) + __expf(__uint_as_float(w4[q] & 0xffff0000u) - M);
     }
   }
-  const float S = block_reduce_sum(s, red);
+  const float S = block_reduce_sum<RB>(s, red);
   if (threadIdx.x == 0) row_loss[row] = valid ? M + __logf(S) - tgt_logit : 0.0f;
   if (!write_grad) return;
   const float invS = 1.0f / S;
@@ -186,10 +195,22 @@ __global__ __launch_bounds__(kBlock) void xent_reg_kernel(bf16_t* __restrict__ l
 
 }  // namespace
 
+// write_grad bits 8..15 select the register-resident geometry (A/B timing,
+// scripts/membound_ab.py at 122880 x 50304: 1024 x 7 4.55 ms = 5.4 TB/s,
+// 512 x 13 4.59 ms, 256 x 25 4.86 ms): 0 = default (1024 x 7), 1 = 256 x 25, 2 = 512 x 13
 NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int write_grad,
                                 hipStream_t s) {
-  if (V % 8 == 0 && V <= kBlock * 8 * kRegChunks)
-    xent_reg_kernel<<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
+  const int variant = (write_grad >> 8) & 0xff;
+  write_grad &= 0xff;
+  bf16_t* lg = (bf16_t*)logits;
+  const int64_t* tg = (const int64_t*)targets;
+  float* rl = (float*)row_loss;
+  if (V % 8 == 0 && variant == 1 && V <= 256 * 8 * 25)
+    xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, write_grad);
+  else if (V % 8 == 0 && variant == 2 && V <= 512 * 8 * 13)
+    xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, write_grad);
+  else if (V % 8 == 0 && V <= 1024 * 8 * 7)
+    xent_reg_kernel<1024, 7><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
   else if (V % 8 == 0)
     xent_kernel<true><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
   else

@@ -224,7 +224,11 @@ def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32):
 # ----------------------------------------------------------------------------
 
 LN_EPS = 1e-5
-_LN_BWD_BLOCKS = 2048  # ~2 rows per wave at N = 12288: enough waves to hide HBM latency
+# LayerNorm backward grid: every block resident at once (3 x 256-thread blocks per
+# CU at the kernel's ~146 VGPRs, 256 CUs), rows strided over the blocks; measured
+# 144 us at 122880 x 768 (5.2 TB/s) vs 148-168 us for 1024-3072 blocks
+# (scripts/membound_ab.py)
+_LN_BWD_BLOCKS = 768
 
 
 class LayerNormFn(torch.autograd.Function):

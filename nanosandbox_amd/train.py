@@ -65,6 +65,10 @@ class Trainer:
             os.makedirs(c["out_dir"], exist_ok=True)
         torch.manual_seed(c["seed"] + info.seed_offset)
         self.compute_dtype = _compute_dtype(self.device_type, c["dtype"])
+        if self.device_type == "cuda":
+            from .ops import blas_tuning
+            if blas_tuning.enable():
+                print(f"library GEMMs: tuned solution table {os.path.basename(blas_tuning.DEFAULT_FILE)}")
 
         # ---------------------------------------------------------------- data
         self.data_dir = resolve_data_dir(c["dataset"], c["data_dir"])
