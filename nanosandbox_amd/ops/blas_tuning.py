@@ -11,7 +11,7 @@ measured faster in the same process, and writes them to ``tuned/*.csv``.
 solution, every other GEMM keeps torch's default (TunableOp falls back to it when
 a shape has no entry).  The file carries TunableOp's validator lines (torch /
 HIP / hipBLASLt / rocBLAS versions, gfx arch); on a mismatch TunableOp ignores it.
-Set ``NSA_TUNED_BLAS=0`` to disable.
+Set ``NSA_TUNED_BLAS=0`` to disable, ``NSA_TUNED_BLAS_FILE`` to load another table.
 """
 
 from __future__ import annotations
@@ -30,7 +30,7 @@ def enable(path: str | None = None) -> bool:
         return True
     if os.environ.get("NSA_TUNED_BLAS", "1") == "0":
         return False
-    path = path or DEFAULT_FILE
+    path = path or os.environ.get("NSA_TUNED_BLAS_FILE") or DEFAULT_FILE
     if not os.path.exists(path):
         return False
     import torch

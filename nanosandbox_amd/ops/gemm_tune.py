@@ -205,6 +205,12 @@ def _hip_wgrad(dy2, x2, g32):
     torch.addmm(g32, dy2.t(), x2, out_dtype=F32, out=g32)
 
 
+def _hip_wgrad_bf16(dy2, x2, g32):
+    """bf16 library GEMM, then fp32 accumulate: the rounding nanoGPT's autocast
+    weight grads get (bf16 matmul output added into the fp32 .grad)."""
+    g32.add_(dy2.t() @ x2)
+
+
 def wgrad_acc(dy2, x2, g32):
     """g32 += dy2^T @ x2 in fp32."""
     T, N = dy2.shape
@@ -223,10 +229,12 @@ def wgrad_acc(dy2, x2, g32):
             fn(dy2, x2, scratch)
         return run
 
-    cands = {"hipblaslt": cand(_hip_wgrad)}
+    cands = {"hipblaslt": cand(_hip_wgrad), "hipblaslt_bf16": cand(_hip_wgrad_bf16)}
     cands.update({f"nsa{v}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, variant=v)) for v in WGRAD_VARIANTS})
     name = choose(("wgrad", T, N, K), cands)
     if name == "hipblaslt":
         _hip_wgrad(dy2, x2, g32)
+    elif name == "hipblaslt_bf16":
+        _hip_wgrad_bf16(dy2, x2, g32)
     else:
         _gemm.wgrad_acc(dy2, x2, g32, variant=_variant(name))

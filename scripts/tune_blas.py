@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--m", default="122880,61440")
     ap.add_argument("--c", type=int, default=768)
     ap.add_argument("--v", type=int, default=50304)
-    ap.add_argument("--ops", default="fwd,dx")
+    ap.add_argument("--ops", default="fwd,dx,dw")
     ap.add_argument("--min-gain", type=float, default=0.02)
     ap.add_argument("--iters", type=int, default=20, help="TunableOp max tuning iterations per solution")
     ap.add_argument("--out", default="nanosandbox_amd/ops/tuned/gfx950_gpt2.csv")
@@ -64,6 +64,9 @@ def main():
                 fns["fwd"] = lambda: x @ w.t()
             if "dx" in a.ops.split(","):
                 fns["dx"] = lambda: dy @ w
+            if "dw" in a.ops.split(","):
+                # weight grad with a bf16 result (nanoGPT + autocast semantics), dY^T X
+                fns["dw"] = lambda: dy.t() @ x
             for op, fn in fns.items():
                 tn.enable(False)
                 fn()
