@@ -48,6 +48,12 @@ def main():
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--real-data", default="",
+                    help="dataset name or directory with train.bin/val.bin (nanoGPT bench.py real_data); "
+                         "default: synthetic uniform tokens")
+    ap.add_argument("--profile", action="store_true",
+                    help="nanoGPT bench.py profile mode: torch.profiler over the timed steps "
+                         "(schedule wait 1 / warmup 1 / active rest), TensorBoard trace under ./bench_log")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -70,7 +76,13 @@ def main():
     # keep nanoGPT's 491,520 tokens/step whatever the micro-batch
     total_micro = per_rank_seqs // args.micro_batch * world
     cfg = dict(TRAIN_DEFAULTS)
-    cfg.update(dataset="synthetic", batch_size=args.micro_batch, block_size=args.block_size,
+    dataset, data_dir = "synthetic", ""
+    if args.real_data:
+        if os.path.isdir(args.real_data):
+            dataset, data_dir = os.path.basename(os.path.normpath(args.real_data)), args.real_data
+        else:
+            dataset = args.real_data
+    cfg.update(dataset=dataset, data_dir=data_dir, batch_size=args.micro_batch, block_size=args.block_size,
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
                dropout=0.0, bias=False, compile=False, device="cuda", dtype="bfloat16", backend="nccl",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
@@ -90,10 +102,22 @@ def main():
         torch.cuda.synchronize()
         if dist.is_initialized():
             dist.barrier()
+        prof = None
+        if args.profile and tr.info.rank == 0:
+            from torch.profiler import ProfilerActivity, profile, schedule, tensorboard_trace_handler
+            active = max(1, args.steps - 2)
+            prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                           schedule=schedule(wait=1 if args.steps > 2 else 0, warmup=1 if args.steps > 1 else 0,
+                                             active=active, repeat=1),
+                           on_trace_ready=tensorboard_trace_handler("./bench_log"), record_shapes=True,
+                           profile_memory=False, with_stack=False)
+            prof.start()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss, _, X, Y = tr.train_step(X, Y)
+            if prof is not None:
+                prof.step()
         torch.cuda.synchronize()
         if dist.is_initialized():
             dist.barrier()
@@ -104,6 +128,9 @@ def main():
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         dt = float(dt_t.item())
         lossf = float(loss.item()) * tr.gas
+        if prof is not None:
+            prof.stop()
+            print("profiler trace written under ./bench_log (not a clean timing: profiled steps)")
 
     tokens_per_step = tokens_per_micro * tr.gas * world
     value = tokens_per_step * args.steps / dt
@@ -111,6 +138,8 @@ def main():
     flops_per_token = tr.raw_model.flops_per_token(args.block_size)
     mfu = value * flops_per_token / (world * 2.5e15)
     if tr.info.rank == 0:
+        # nanoGPT bench.py's summary line (stderr; stdout carries only the JSON record)
+        print(f"time per iteration: {ms:.4f}ms, MFU: {mfu * 100:.2f}%", file=sys.stderr)
         print(json.dumps({
             "metric": METRIC if args.model == "gpt2" else f"tokens/sec (whole node) {args.model} DDP",
             "value": round(value, 1),
@@ -123,7 +152,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (uniform random tokens, vocab 50304); random-init weights",
+            "data": (f"real ({dataset}); random-init weights" if args.real_data else
+                     "synthetic (uniform random tokens, vocab 50304); random-init weights"),
             "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,
                        "global_batch": tokens_per_step // args.block_size, "seq_len": args.block_size,
                        "tokens_per_step": tokens_per_step, "micro_batch": args.micro_batch,

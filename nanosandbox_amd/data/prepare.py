@@ -11,11 +11,19 @@ local text file (``--input``) or, by default, from a deterministic synthetic
 English-like corpus of the same size as tinyshakespeare (1,115,394 chars).
 ``tokens`` writes a GPT-2-vocabulary token stream (the offline stand-in for the
 OpenWebText subset job, reference ``scripts/gh_sync.ps1:145-147``).
+``bpe`` is upstream ``data/shakespeare/prepare.py`` / ``data/openwebtext/prepare.py``:
+byte-level BPE encoding of a local text (tiktoken's GPT-2 ``encode_ordinary``
+there; here the HF ``tokenizers`` library with a local GPT-2 ``tokenizer.json``
+or ``vocab.json`` + ``merges.txt`` — no network, tiktoken is not installed), a
+90/10 split (``--docs``: one document per line, each followed by <|endoftext|>
+50256, split by ``--val_frac`` as the OWT script does).  Parity with tiktoken's
+ids holds for the same GPT-2 vocab/merges files; it is not pinned by a test here.
 
 CLI::
 
     python -m nanosandbox_amd.data.prepare char   --out data/shakespeare_char [--input input.txt]
     python -m nanosandbox_amd.data.prepare tokens --out data/openwebtext --n_tokens 10000000
+    python -m nanosandbox_amd.data.prepare bpe    --out data/shakespeare --input input.txt --tokenizer gpt2/
 """
 
 from __future__ import annotations
@@ -107,6 +115,42 @@ def write_token_dataset(out_dir: str, n_tokens: int, vocab: int = 50257, seed: i
     print(f"train has {n_tokens - n_val:,} tokens, val has {n_val:,} tokens")
 
 
+def load_bpe(path: str):
+    """A byte-level BPE tokenizer from a ``tokenizer.json`` or a dir with it / vocab.json + merges.txt."""
+    from tokenizers import Tokenizer
+    from tokenizers.implementations import ByteLevelBPETokenizer
+
+    if os.path.isdir(path):
+        tj = os.path.join(path, "tokenizer.json")
+        if os.path.exists(tj):
+            return Tokenizer.from_file(tj)
+        return ByteLevelBPETokenizer(os.path.join(path, "vocab.json"), os.path.join(path, "merges.txt"))
+    return Tokenizer.from_file(path)
+
+
+def write_bpe_dataset(out_dir: str, text: str, tokenizer, docs: bool = False, val_frac: float = 0.0005,
+                      eot: int = 50256) -> dict:
+    """Encode ``text`` (nanoGPT shakespeare: 90/10 split; ``docs``: OWT-style EOT after each line)."""
+    os.makedirs(out_dir, exist_ok=True)
+    if docs:
+        lines = [ln for ln in text.splitlines() if ln.strip()]
+        enc = tokenizer.encode_batch(lines)
+        n_val_docs = max(1, int(round(len(lines) * val_frac))) if len(lines) > 1 else 0
+        split_at = len(lines) - n_val_docs
+        ids = [[*e.ids, eot] for e in enc]
+        train = np.array([t for d in ids[:split_at] for t in d], dtype=np.uint16)
+        val = np.array([t for d in ids[split_at:] for t in d], dtype=np.uint16)
+    else:
+        n = len(text)
+        train = np.array(tokenizer.encode(text[: int(n * 0.9)]).ids, dtype=np.uint16)
+        val = np.array(tokenizer.encode(text[int(n * 0.9):]).ids, dtype=np.uint16)
+    train.tofile(os.path.join(out_dir, "train.bin"))
+    val.tofile(os.path.join(out_dir, "val.bin"))
+    print(f"train has {len(train):,} tokens")
+    print(f"val has {len(val):,} tokens")
+    return {"train": len(train), "val": len(val)}
+
+
 def _download(url: str, timeout: float = 30.0):
     import urllib.request
 
@@ -120,14 +164,23 @@ def _download(url: str, timeout: float = 30.0):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["char", "tokens"])
+    ap.add_argument("kind", choices=["char", "tokens", "bpe"])
     ap.add_argument("--out", required=True)
     ap.add_argument("--input", default="")
     ap.add_argument("--url", default="", help="download the text (through HTTP(S)_PROXY); falls back to "
                                               "the synthetic corpus when unreachable (air-gapped clusters)")
     ap.add_argument("--n_tokens", type=int, default=10_000_000)
     ap.add_argument("--seed", type=int, default=1337)
+    ap.add_argument("--tokenizer", default="", help="bpe: tokenizer.json, or a dir with it / vocab.json + merges.txt")
+    ap.add_argument("--docs", action="store_true", help="bpe: one document per line, EOT-separated (OWT style)")
+    ap.add_argument("--val_frac", type=float, default=0.0005)
     a = ap.parse_args(argv)
+    if a.kind == "bpe":
+        if not a.input or not a.tokenizer:
+            ap.error("bpe needs --input and --tokenizer (no network: tiktoken's GPT-2 files must be local)")
+        with open(a.input) as f:
+            write_bpe_dataset(a.out, f.read(), load_bpe(a.tokenizer), docs=a.docs, val_frac=a.val_frac)
+        return
     if a.kind == "char":
         text = None
         if a.input:

@@ -126,3 +126,52 @@ def test_lr_schedule():
     # monotone decay after warmup
     vals = [get_lr(i, lr, wu, dec, mn) for i in range(10, 101)]
     assert all(a >= b for a, b in zip(vals, vals[1:]))
+
+
+def _tiny_bpe(tmp_path):
+    """Train a small byte-level BPE in-process (GPT-2's files are not available offline)."""
+    from tokenizers import ByteLevelBPETokenizer
+
+    from nanosandbox_amd.data.prepare import synthetic_corpus
+
+    text = synthetic_corpus(n_chars=20000, seed=3)
+    tok = ByteLevelBPETokenizer()
+    tok.train_from_iterator([text], vocab_size=400, min_frequency=2, special_tokens=["<|endoftext|>"])
+    d = tmp_path / "tok"
+    d.mkdir()
+    tok.save_model(str(d))  # vocab.json + merges.txt, the GPT-2 release layout
+    return text, d
+
+
+def test_bpe_dataset_split_and_roundtrip(tmp_path):
+    """nanoGPT data/shakespeare/prepare.py semantics: 90/10 char split, uint16 ids, lossless decode."""
+    import numpy as np
+
+    from nanosandbox_amd.data.prepare import load_bpe, main
+
+    text, d = _tiny_bpe(tmp_path)
+    inp = tmp_path / "input.txt"
+    inp.write_text(text)
+    out = tmp_path / "bpe"
+    main(["bpe", "--out", str(out), "--input", str(inp), "--tokenizer", str(d)])
+    train = np.fromfile(out / "train.bin", dtype=np.uint16)
+    val = np.fromfile(out / "val.bin", dtype=np.uint16)
+    tok = load_bpe(str(d))
+    n = len(text)
+    assert tok.decode(train.tolist()) == text[: int(n * 0.9)]
+    assert tok.decode(val.tolist()) == text[int(n * 0.9):]
+
+
+def test_bpe_docs_mode_eot(tmp_path):
+    """OWT-style: every document is followed by <|endoftext|> (id 50256 in GPT-2's vocab)."""
+    import numpy as np
+
+    from nanosandbox_amd.data.prepare import load_bpe, write_bpe_dataset
+
+    text, d = _tiny_bpe(tmp_path)
+    flat = text.replace("\n", " ")
+    docs = "\n".join(flat[i:i + 500] for i in range(0, 5000, 500))
+    stats = write_bpe_dataset(str(tmp_path / "owt"), docs, load_bpe(str(d)), docs=True, val_frac=0.1, eot=50256)
+    train = np.fromfile(tmp_path / "owt" / "train.bin", dtype=np.uint16)
+    assert (train == 50256).sum() == 9 and train[-1] == 50256
+    assert stats["val"] > 0
