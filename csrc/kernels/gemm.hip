@@ -92,7 +92,7 @@ struct GemmArgs {
   const bf16_t* U;  // EPI_DGELU: pre-activation whose gelu' scales acc
   int M, N, K;
   int lda, ldb, ldc;
-  int k_per_split;
+  int k_per_split;  // unused by the kernels (kept for layout); splits cover 64-deep K blocks unevenly
   int tiles_m, tiles_n;
 };
 
@@ -111,8 +111,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
   }
   const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int k_begin = blockIdx.z * g.k_per_split;
-  const int nk = g.k_per_split / BK;
+  // split z owns K blocks [z*nkb/S, (z+1)*nkb/S): any split count, no K % (64*S) rule
+  const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
+  const int k_begin = kb0 * 64;
+  const int nk = (((int)blockIdx.z + 1) * nkb / (int)gridDim.z - kb0) * (64 / BK);
 
   // ---- global -> register staging: 4 x 16 B of A and 4 x 16 B of B per thread
   // (plain code, no lambdas: a by-reference capture of ra/rb sends them to scratch)
@@ -435,8 +437,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring_kernel(GemmArgs g) {
   }
   const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int k_begin = blockIdx.z * g.k_per_split;
-  const int nk = g.k_per_split / RBK;
+  const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
+  const int k_begin = kb0 * 64;
+  const int nk = (((int)blockIdx.z + 1) * nkb / (int)gridDim.z - kb0) * (64 / RBK);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
@@ -601,8 +604,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring64_kernel(GemmArgs g) {
   }
   const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int k_begin = blockIdx.z * g.k_per_split;
-  const int nk = g.k_per_split / 64;
+  const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
+  const int k_begin = kb0 * 64;
+  const int nk = ((int)blockIdx.z + 1) * nkb / (int)gridDim.z - kb0;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
@@ -998,7 +1002,7 @@ NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const v
                             void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
   const int variant = (epi >> 8) & 0xff;
   epi &= 0xff;
-  if (K % (BK * splits) != 0 || M < 8 || N < 8 || M % 8 || N % 8) return hipErrorInvalidValue;
+  if (K % BK != 0 || splits < 1 || splits > K / BK || M < 8 || N < 8 || M % 8 || N % 8) return hipErrorInvalidValue;
   if (layout == 2 && M % 8) return hipErrorInvalidValue;
   if (epi != EPI_ATOMIC_F32 && splits != 1) return hipErrorInvalidValue;
   GemmArgs a{};

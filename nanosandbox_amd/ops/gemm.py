@@ -81,13 +81,35 @@ def dgrad(dy2, w, u=None, variant=None):
 
 
 def wgrad_splits(n_out, n_in, tokens, cus=256):
+    """Largest split count with at most two rounds of blocks (one 512-thread block per CU)."""
     tiles = -(-n_out // TILE) * -(-n_in // TILE)
+    nkb = max(1, tokens // BK)
     best = 1
-    for s in range(1, 65):
-        if tokens % (BK * s):
-            continue
+    for s in range(1, min(64, nkb) + 1):
         if tiles * s <= 2 * cus:
             best = s
+    return best
+
+
+def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=4):
+    """Split count whose block count fills whole rounds of the CUs best.
+
+    The kernels take any split count (split z owns K blocks [z*n/S, (z+1)*n/S)),
+    so e.g. 27 output tiles x 28 splits = 756 blocks = 2.95 rounds (98 % of the
+    last round busy) instead of 27 x 16 = 432 = 1.69 rounds (the default rule).
+    Ties go to fewer splits (fewer fp32 atomics).
+    """
+    tiles = -(-n_out // TILE) * -(-n_in // TILE)
+    nkb = max(1, tokens // BK)
+    best, best_eff = 1, -1.0
+    for s in range(1, min(128, nkb) + 1):
+        blocks = tiles * s
+        rounds = -(-blocks // cus)
+        if rounds > max_rounds:
+            break
+        eff = blocks / (rounds * cus)
+        if eff > best_eff + 1e-9:
+            best, best_eff = s, eff
     return best
 
 

@@ -124,7 +124,12 @@ def _nsa_ok(*ts):
 
 
 def _variant(name):
-    return int(name[-1])
+    """'nsa7' -> 7, 'nsa7/s28' -> 7, 'fused8' -> 8."""
+    return int(name.split("/")[0].lstrip("abcdefghijklmnopqrstuvwxyz_"))
+
+
+def _splits(name):
+    return int(name.split("/s")[1]) if "/s" in name else None
 
 
 def fwd(x2, w):
@@ -231,10 +236,15 @@ def wgrad_acc(dy2, x2, g32):
 
     cands = {"hipblaslt": cand(_hip_wgrad), "hipblaslt_bf16": cand(_hip_wgrad_bf16)}
     cands.update({f"nsa{v}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, variant=v)) for v in WGRAD_VARIANTS})
+    # the same kernels with a split count that fills whole rounds of CUs
+    sb = _gemm.wgrad_splits_balanced(N, K, T)
+    if sb != _gemm.wgrad_splits(N, K, T):
+        cands.update({f"nsa{v}/s{sb}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v))
+                      for v in WGRAD_VARIANTS})
     name = choose(("wgrad", T, N, K), cands)
     if name == "hipblaslt":
         _hip_wgrad(dy2, x2, g32)
     elif name == "hipblaslt_bf16":
         _hip_wgrad_bf16(dy2, x2, g32)
     else:
-        _gemm.wgrad_acc(dy2, x2, g32, variant=_variant(name))
+        _gemm.wgrad_acc(dy2, x2, g32, splits=_splits(name), variant=_variant(name))

@@ -46,7 +46,8 @@ def test_dgrad(kernels, M, N, K, variant):
 
 
 @pytest.mark.parametrize("T,N,K,splits", [(1024, 768, 768, None), (4096, 2304, 768, None), (512, 520, 200, 2),
-                                          (2048, 768, 3072, 4), (1024, 50304, 768, 1)])
+                                          (2048, 768, 3072, 4), (1024, 50304, 768, 1),
+                                          (1024, 768, 768, 3), (4096, 2304, 768, 28)])  # uneven K splits
 @pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10])
 def test_wgrad_acc(kernels, T, N, K, splits, variant):
     from nanosandbox_amd.ops import gemm
