@@ -39,6 +39,7 @@ import torch.nn.functional as F
 from . import _lib
 from . import gemm as _gemm
 from . import gemm_tune as _tune
+from . import streams as _streams
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -104,7 +105,8 @@ def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
         dy2 = dy2.contiguous()
         x2 = x2.contiguous()
         if mg is not None:
-            _tune.wgrad_acc(dy2, x2, mg)
+            with _streams.fork(dy2, x2):  # beside the serial input-gradient chain
+                _tune.wgrad_acc(dy2, x2, mg)
             notify_grad_ready(p)
             return None
         g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
@@ -188,6 +190,7 @@ class EmbeddingFn(torch.autograd.Function):
         B, T, V, C = ctx.shape
         if dx.is_cuda:
             dx = dx.contiguous()
+            _streams.join(dx.device)  # the tied lm_head weight gradient may still be on the side stream
             gwte = getattr(wte, "main_grad", None)
             gwpe = getattr(wpe, "main_grad", None)
             ret_wte = gwte is None
@@ -372,12 +375,14 @@ class LinearFn(torch.autograd.Function):
         x2, w, b = ctx.saved_tensors
         Nout = w.shape[0]
         d2 = dout.reshape(-1, Nout)
+        # weight gradient first: on the side stream it then waits only for dout, and
+        # the input-gradient GEMM below runs beside it (ops/streams.py)
+        gw = weight_grad(w, d2, x2)
         dx = None
         if ctx.needs_input_grad[0]:
             wc = compute_weight(w, d2.dtype)
             dx = _tune.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
             dx = dx.view(*dout.shape[:-1], x2.shape[-1])
-        gw = weight_grad(w, d2, x2)
         gb = None
         if ctx.has_bias:
             gb = _accumulate(b, d2.sum(0, dtype=F32))
@@ -427,13 +432,15 @@ class MLPFn(torch.autograd.Function):
         x2, u, g, w_fc, w_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         wp = compute_weight(w_proj, dy.dtype)
+        # each weight gradient is issued before the input-gradient GEMM that runs
+        # beside it on the main stream (ops/streams.py)
+        gw_proj = weight_grad(w_proj, dy2, g)
         if FUSE_GELU_EPILOGUE:
             du = _gemm.dgrad(dy2, wp, u=u)
         else:
             du = _tune.dgrad_dgelu(dy2, wp, u)
-        gw_proj = weight_grad(w_proj, dy2, g)
-        dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
         gw_fc = weight_grad(w_fc, du, x2)
+        dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
         return dx.view(ctx.xshape), gw_fc, gw_proj
 
 
@@ -599,10 +606,10 @@ class LMHeadLossFn(torch.autograd.Function):
         g = (gl.float() / n_valid)
         wc = compute_weight(w, x2.dtype)
         if x2.is_cuda:
-            dx = _tune.dgrad(dlogits, wc)
-            dx.mul_(g.to(dx.dtype))
             xs = x2 * g.to(x2.dtype)
             gw = weight_grad(w, dlogits, xs)
+            dx = _tune.dgrad(dlogits, wc)
+            dx.mul_(g.to(dx.dtype))
             return dx.view(ctx.xshape), gw, None, None
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)

@@ -104,6 +104,9 @@ class FlatParamStore:
 
     @torch.no_grad()
     def zero_grad(self):
+        if self.grad.is_cuda:
+            from ..ops import streams
+            streams.join(self.grad.device)  # no side-stream accumulate may land after the zero
         self.grad.zero_()
         if not self.fused_grad:
             # torch DDP / plain autograd path: keep .grad pointing at the flat buffer
