@@ -35,7 +35,15 @@ Protocol (all calls are no-ops on CPU tensors and during HIP-graph capture):
   ``zero_grad``.  Bucket all-reduces are issued from the side stream itself
   (parallel/reducer.py), so they never stall the main stream.
 
-``NSA_WGRAD_STREAM=0`` keeps every weight gradient on the main stream.
+Opt-in (``NSA_WGRAD_STREAM=1``); the default keeps every weight gradient on
+the main stream.  Measured on MI355X (GPT-2 124M, micro-batch 120): 497 vs
+501 ms/step (-0.8 %), but hipBLASLt's gfx950 solutions for these shapes are
+Stream-K kernels (``_SK3``: a persistent grid whose workgroups spin on each
+other's partial-tile flags), and side-stream workgroups occupying CUs they
+expect to be co-resident stretched individual steps to 3.6-4.2 s and once
+stalled a run for minutes.  Library Stream-K kernels and a concurrent compute
+stream do not mix safely, so the overlap stays off unless every main-stream
+GEMM is our own (non-persistent) kernel.
 """
 
 from __future__ import annotations
@@ -45,7 +53,7 @@ import os
 
 import torch
 
-ENABLED = os.environ.get("NSA_WGRAD_STREAM", "1") != "0"
+ENABLED = os.environ.get("NSA_WGRAD_STREAM", "0") == "1"
 
 _side: dict = {}
 _pending: set = set()

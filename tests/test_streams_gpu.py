@@ -19,6 +19,7 @@ def _grads(enabled, steps=3):
     from nanosandbox_amd.ops import streams
     from nanosandbox_amd.optim import FlatParamStore
 
+    saved = streams.ENABLED
     streams.ENABLED = enabled
     try:
         torch.manual_seed(0)
@@ -41,7 +42,7 @@ def _grads(enabled, steps=3):
         torch.cuda.synchronize()
         return [t.cpu() for t in out], store.master.detach().cpu().clone()
     finally:
-        streams.ENABLED = True
+        streams.ENABLED = saved
 
 
 def _rels(a_list, b_list):
