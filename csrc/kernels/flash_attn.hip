@@ -318,6 +318,41 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_ker
 #undef NSA_FWD_STAGE_WRITE
 
 // =============================================================================
+// backward preprocessing, one pass over [B, T, C]:
+//   delta[b, h, t] = rowsum(dO * O)  (fp32)   and   dq_acc[b, t, :] = 0
+// The zeroing rides along with the delta reads (same rows, same threads), so the
+// fp32 dQ accumulator needs no separate fill launch.
+// =============================================================================
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ o,
+                                                           const bf16_t* __restrict__ dout,
+                                                           float* __restrict__ delta, float* __restrict__ dq_acc,
+                                                           int B, int T, int H) {
+  constexpr int LPR = D / 8;  // lanes per (b, t, h) row, 8 elements each
+  const int C = H * D;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / LPR;  // row = (b*T + t)*H + h  -> contiguous [B, T, C] walk
+  const int sub = gid % LPR;
+  if (row >= (int64_t)B * T * H) return;
+  const int hh = row % H;
+  const int64_t bt = row / H;
+  const int t = bt % T, b = bt / T;
+  const int64_t off = bt * C + hh * D + sub * 8;
+  float a[8], g[8];
+  load8(o + off, a);
+  load8(dout + off, g);
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += a[j] * g[j];
+#pragma unroll
+  for (int k = LPR / 2; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
+  if (sub == 0) delta[((int64_t)b * H + hh) * T + t] = s;
+  float4* z = reinterpret_cast<float4*>(dq_acc + off);
+  z[0] = float4{0.f, 0.f, 0.f, 0.f};
+  z[1] = float4{0.f, 0.f, 0.f, 0.f};
+}
+
+// =============================================================================
 // backward main kernel: one workgroup = KB keys (KB/32 waves x 32) of one (b, h)
 // =============================================================================
 // Geometry: KB = 256 keys (8 waves) for D = 64 (GPT-2), 128 (4 waves) for D = 32
@@ -331,7 +366,10 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_ker
 template <int D>
 struct BwdGeo {
   static constexpr int QB = 64;
-  static constexpr int KB = D == 64 ? 256 : 128;
+#ifndef NSA_BWD_KB64
+#define NSA_BWD_KB64 256  // keys per workgroup at D = 64 (A/B probe: build_variant with -DNSA_BWD_KB64=128)
+#endif
+  static constexpr int KB = D == 64 ? NSA_BWD_KB64 : 128;
   static constexpr int NW = KB / 32;
   static constexpr int NTILES = 2 * (D / 32);            // (q-half, d-tile) pairs of the dQ tile
   static constexpr int SPLIT = NW > NTILES ? NW / NTILES : 1;
@@ -385,19 +423,12 @@ __device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpac
     q = q < T ? q : T - 1;                                                               \
     qst[c] = *reinterpret_cast<const uint4*>(qbase + (int64_t)q * row_stride + ch * 8);  \
     dost[c] = *reinterpret_cast<const uint4*>(dobase + (int64_t)q * C + ch * 8);         \
-    const uint4 ov_ = *reinterpret_cast<const uint4*>(obase + (int64_t)q * C + ch * 8);  \
-    float of_[8], gf_[8];                                                                \
-    unpack8(ov_, of_);                                                                   \
-    unpack8(dost[c], gf_);                                                               \
-    float s_ = 0.0f;                                                                     \
-    _Pragma("unroll") for (int j = 0; j < 8; ++j) s_ += of_[j] * gf_[j];                 \
-    _Pragma("unroll") for (int off = CPR / 2; off > 0; off >>= 1) s_ += __shfl_xor(s_, off, 64); \
-    dlt[c] = s_;                                                                         \
   }                                                                                      \
   {                                                                                      \
     int q = (QBI) * QB + (tid & (QB - 1));                                               \
     q = q < T ? q : T - 1;                                                               \
     lst = lse_bh[q] * kLog2e;                                                            \
+    dst = delta_bh[q];                                                                   \
   }
 #define NSA_BWD_STAGE_WRITE(BUF)                                                         \
   _Pragma("unroll") for (int c = 0; c < QCH; ++c) {                                      \
@@ -406,16 +437,15 @@ __device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpac
     *reinterpret_cast<uint4*>(qs_lds + (BUF) * QT_BYTES + swz<D>(row, ch)) = qst[c];     \
     *reinterpret_cast<uint4*>(do_lds + (BUF) * QT_BYTES + swz<D>(row, ch)) = dost[c];    \
   }                                                                                      \
-  if (tid < QB) ld_lds[(BUF) * QB + tid] = lst;                                           \
-  _Pragma("unroll") for (int c = 0; c < QCH; ++c) {                                      \
-    const int e = tid + NT * c;                                                          \
-    if (e % CPR == 0) ld_lds[2 * QB + (BUF) * QB + e / CPR] = dlt[c];                   \
+  if (tid < QB) {                                                                        \
+    ld_lds[(BUF) * QB + tid] = lst;                                                      \
+    ld_lds[2 * QB + (BUF) * QB + tid] = dst;                                             \
   }
 
 template <int D, bool DROP>
 __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
-    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-    const float* __restrict__ lse, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
     float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
   using G = BwdGeo<D>;
   constexpr int QB = G::QB, KB = G::KB, NT = G::NW * 64;
@@ -450,8 +480,8 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
   const bf16_t* kbase = base + C + hh * D;
   const bf16_t* vbase = base + 2 * C + hh * D;
   const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
-  const bf16_t* obase = o + (int64_t)b * T * C + hh * D;
   const float* lse_bh = lse + (int64_t)bh * T;
+  const float* delta_bh = delta + (int64_t)bh * T;
   const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
 
   // K^T / V^T fragments for S = Q·K^T and dP = dO·V^T (B operands): K[kpos][16ks+8h..]
@@ -485,12 +515,10 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
   const int qb_first = k0 / QB;
   const int n_qb = (T + QB - 1) / QB;
 
-  // delta = rowsum(dO * O) of each staged query row is formed while staging: the
-  // dO chunks are in registers already, O costs one more 16-byte load per chunk and
-  // a CPR-lane shuffle reduction (replaces a separate preprocessing launch)
+  // delta = rowsum(dO * O) comes precomputed (flash_bwd_pre_kernel): forming it while
+  // staging re-read O once per key block, inside the loop (measured 1154 -> 1335 us)
   uint4 qst[QCH], dost[QCH];
-  float dlt[QCH];
-  float lst;
+  float lst, dst;
   NSA_BWD_STAGE_LOAD(qb_first)
   NSA_BWD_STAGE_WRITE(0)
   __syncthreads();
@@ -664,18 +692,22 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
 template <int D>
 hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const void* lse, void* delta, void* dq_acc,
                       void* dqkv, int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
-  (void)delta;  // delta = rowsum(dO * O) is formed inside flash_bwd_kernel's Q/dO staging
-  hipError_t e;
+  const int64_t rows = (int64_t)B * T * H;
+  const int64_t threads = rows * (D / 8);
+  flash_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+      (const bf16_t*)o, (const bf16_t*)dout, (float*)delta, (float*)dq_acc, B, T, H);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_kb = (T + BwdGeo<D>::KB - 1) / BwdGeo<D>::KB;
   if (th)
     flash_bwd_kernel<D, true><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
-        (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, (float*)dq_acc,
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
         (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
   else
     flash_bwd_kernel<D, false><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
-        (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, (float*)dq_acc,
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
         (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -538,9 +538,10 @@ class AttentionFn(torch.autograd.Function):
             qkv, y, lse = ctx.saved_tensors
             dy = dy.contiguous()
             dqkv = torch.empty_like(qkv)
-            dq_acc = torch.zeros(B, T, C, device=dy.device, dtype=F32)
-            # delta = rowsum(dO * O) is computed inside the kernel (delta argument unused)
-            _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), None,
+            # zeroed and delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing
+            dq_acc = torch.empty(B, T, C, device=dy.device, dtype=F32)
+            delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
+            _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
                       _lib.ptr(dq_acc), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
             return dqkv, None, None
         (qkv,) = ctx.saved_tensors

@@ -76,8 +76,7 @@ def main():
         def fwd():
             _lib.call("nsa_flash_fwd", qkv.data_ptr(), y.data_ptr(), lse.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
-        def bwd():
-            dq.zero_()
+        def bwd():  # the kernel's preprocessing pass zeroes dq itself
             _lib.call("nsa_flash_bwd", qkv.data_ptr(), y.data_ptr(), dy.data_ptr(), lse.data_ptr(), delta.data_ptr(),
                       dq.data_ptr(), dqkv.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
