@@ -601,18 +601,21 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
       }
       if constexpr (G::SPLIT > 1) {
         if (part > 0) {
-          f32x4* dst4 = reinterpret_cast<f32x4*>(red_lds) + (((part - 1) * G::NTILES + tile) * 64 + lane) * 4;
+          // [v][lane] layout: a wave's 16-byte stores / loads are 64 consecutive chunks
+          // (a [lane][v] layout put lanes 64 B apart: 4-way bank conflicts, PMC-measured)
+          f32x4* dst4 = reinterpret_cast<f32x4*>(red_lds) + ((part - 1) * G::NTILES + tile) * 256 + lane;
 #pragma unroll
-          for (int v = 0; v < 4; ++v) dst4[v] = f32x4{dqa[4 * v], dqa[4 * v + 1], dqa[4 * v + 2], dqa[4 * v + 3]};
+          for (int v = 0; v < 4; ++v)
+            dst4[64 * v] = f32x4{dqa[4 * v], dqa[4 * v + 1], dqa[4 * v + 2], dqa[4 * v + 3]};
         }
         __syncthreads();
         if (part == 0) {
 #pragma unroll
           for (int p2 = 1; p2 < G::SPLIT; ++p2) {
-            const f32x4* src4 = reinterpret_cast<const f32x4*>(red_lds) + (((p2 - 1) * G::NTILES + tile) * 64 + lane) * 4;
+            const f32x4* src4 = reinterpret_cast<const f32x4*>(red_lds) + ((p2 - 1) * G::NTILES + tile) * 256 + lane;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              const f32x4 x = src4[v];
+              const f32x4 x = src4[64 * v];
               dqa[4 * v] += x[0];
               dqa[4 * v + 1] += x[1];
               dqa[4 * v + 2] += x[2];
