@@ -144,16 +144,53 @@ def fwd(x2, w):
     return x2 @ w.t() if name == "hipblaslt" else _gemm.fwd(x2, w, variant=_variant(name))
 
 
+# Weight generation: bumped whenever the bf16 compute weights are rewritten outside
+# torch's in-place ops (fused AdamW kernel, FlatParamStore.refresh_compute), so cached
+# derived copies of a weight (its transpose, below) are rebuilt once per optimizer step.
+_weight_gen = 0
+
+
+def weights_changed():
+    global _weight_gen
+    _weight_gen += 1
+
+
+def _wt(w):
+    """w^T as a contiguous tensor, cached on the weight tensor for the current generation.
+
+    hipBLASLt runs dX = dY·W much faster with W stored K-contiguous (the forward's
+    "TN" layout) than as the row-major nn.Linear weight ("NN"): 652 vs ~480 us for
+    mlp.c_proj at 122880 tokens.  Transposing a weight costs microseconds and is
+    amortised over every micro-step of an optimizer step.  Inside HIP-graph capture
+    the transpose is recomputed (captured into the graph) instead of cached."""
+    if torch.cuda.is_current_stream_capturing():
+        return w.t().contiguous()
+    key = (_weight_gen, w._version, w.data_ptr())
+    hit = getattr(w, "_nsa_wt", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    t = w.t().contiguous()
+    try:
+        w._nsa_wt = (key, t)
+    except (AttributeError, RuntimeError):
+        pass
+    return t
+
+
 def dgrad(dy2, w):
     """dx = dy2 @ w (bf16)."""
     M, N = dy2.shape
     K = w.shape[1]
     if not (_nsa_ok(dy2, w) and _gemm.supported(M, K, N)):
         return dy2 @ w
-    cands = {"hipblaslt": lambda: dy2 @ w}
+    cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()}
     cands.update({f"nsa{v}": (lambda v=v: _gemm.dgrad(dy2, w, variant=v)) for v in NSA_VARIANTS})
     name = choose(("dgrad", M, N, K), cands)
-    return dy2 @ w if name == "hipblaslt" else _gemm.dgrad(dy2, w, variant=_variant(name))
+    if name == "hipblaslt":
+        return dy2 @ w
+    if name == "hipblaslt_t":
+        return dy2 @ _wt(w).t()
+    return _gemm.dgrad(dy2, w, variant=_variant(name))
 
 
 def _gelu_fwd(u):

@@ -93,6 +93,8 @@ class FlatParamStore:
     @torch.no_grad()
     def refresh_compute(self):
         """Re-derive the bf16 compute shadow from the fp32 master (after load/broadcast)."""
+        from ..ops import gemm_tune
+        gemm_tune.weights_changed()
         if self.compute is None:
             return
         if self.device.type == "cuda":

@@ -74,3 +74,28 @@ def test_asymmetric_identity(kernels, variant):
     g = torch.zeros(n, n, device=DEV)
     gemm.wgrad_acc(eye, b, g, variant=variant)                                     # I^T @ b
     assert torch.equal(g, b.float())
+
+
+def test_transposed_weight_dgrad_cache(kernels):
+    """dX = dY·W through the cached K-contiguous W^T (gemm_tune._wt): equal to the plain
+    product, rebuilt after an in-place update (version bump) and after a raw rewrite
+    announced by weights_changed() (what the fused AdamW kernel does)."""
+    from nanosandbox_amd.ops import gemm_tune
+
+    torch.manual_seed(0)
+    dy = torch.randn(512, 384, device="cuda").to(torch.bfloat16)
+    w = torch.randn(384, 256, device="cuda").to(torch.bfloat16)
+
+    def via_t():
+        return dy @ gemm_tune._wt(w).t()
+
+    assert torch.equal(via_t(), dy @ w)
+    t0 = gemm_tune._wt(w)
+    assert gemm_tune._wt(w) is t0  # cached
+    w.mul_(2.0)  # torch in-place op: version bump invalidates
+    assert torch.equal(via_t(), dy @ w)
+    w.data.copy_(torch.randn_like(w))  # raw rewrite: no version bump ...
+    stale = via_t()
+    assert not torch.equal(stale, dy @ w)  # ... so the cache is stale until announced
+    gemm_tune.weights_changed()
+    assert torch.equal(via_t(), dy @ w)
