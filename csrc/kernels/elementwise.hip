@@ -20,8 +20,13 @@ inline int grid_for(int64_t n_vec) {
   return (int)g;
 }
 
+#ifdef NSA_GELU_PROBE_COPY  // A/B probe only (build_variant): data movement without the erf math
+__device__ __forceinline__ float gelu_f(float x) { return x; }
+__device__ __forceinline__ float gelu_grad(float x) { return x; }
+#else
 __device__ __forceinline__ float gelu_f(float x) { return nsa_gelu(x); }
 __device__ __forceinline__ float gelu_grad(float x) { return nsa_gelu_grad(x); }
+#endif
 
 __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          int64_t n) {
