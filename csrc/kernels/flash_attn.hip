@@ -17,7 +17,8 @@
 //   O^T[d][q] += V^T · P^T        A = V^T (LDS, ds_read_b64_tr_b16 transposed
 //        read of the row-major V tile), B = P^T straight from the S^T
 //        accumulator registers (bf16-converted, permuted k order).
-// backward, per wave = 32 keys (workgroup = 128 keys), loop over 64-query blocks:
+// backward (default "split" mode: dK/dV kernel + separate dQ kernel, see bwd_launch;
+// the "atomic" mode below keeps dQ in the dK/dV kernel), per wave = 32 keys, loop over 64-query blocks:
 //   S = Q·K^T, dP = dO·V^T        key on the lane; K, V fragments live in registers
 //   dV^T += dO^T · P,  dK^T += Q^T · dS      accumulators as B operands, A by tr reads
 //   dQ   += dS · K                dS crosses LDS once (as dS^T), fp32 atomics whose
@@ -347,9 +348,11 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 #pragma unroll
   for (int k = LPR / 2; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
   if (sub == 0) delta[((int64_t)b * H + hh) * T + t] = s;
-  float4* z = reinterpret_cast<float4*>(dq_acc + off);
-  z[0] = float4{0.f, 0.f, 0.f, 0.f};
-  z[1] = float4{0.f, 0.f, 0.f, 0.f};
+  if (dq_acc != nullptr) {  // in-kernel-dQ mode only (the split mode writes dQ once, no accumulator)
+    float4* z = reinterpret_cast<float4*>(dq_acc + off);
+    z[0] = float4{0.f, 0.f, 0.f, 0.f};
+    z[1] = float4{0.f, 0.f, 0.f, 0.f};
+  }
 }
 
 // =============================================================================
@@ -442,8 +445,12 @@ __device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpac
     ld_lds[2 * QB + (BUF) * QB + tid] = dst;                                             \
   }
 
-template <int D, bool DROP>
-__global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
+// DQ = true: dQ is accumulated here too (dS^T through LDS, split-K over the
+// workgroup's keys, fp32 atomics into dq_acc).  DQ = false: this kernel makes only
+// dK / dV; flash_bwd_dq_kernel forms dQ per query tile with no atomics, and without
+// the K / dS / reduction LDS two workgroups fit per CU.
+template <int D, bool DROP, bool DQ>
+__global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
     float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
@@ -456,13 +463,15 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
   constexpr int QCH = QB * CPR / NT;  // 16-byte chunks per thread per Q (or dO) tile
   constexpr int KCH = KB * CPR / NT;
   static_assert(QCH >= 1 && QB * CPR == QCH * NT, "Q tile staging must divide evenly");
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS_BYTES];
+  constexpr int LDS_TOTAL = DQ ? G::LDS_BYTES : 4 * QT_BYTES + 4 * QB * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_TOTAL];
   char* const qs_lds = smem;                         // Q[2]
   char* const do_lds = smem + 2 * QT_BYTES;          // dO[2]
-  char* const k_lds = smem + 4 * QT_BYTES;           // K (workgroup keys)
-  char* const ds_lds = k_lds + G::K_BYTES;           // dS^T [KB keys][QB q]
-  float* const red_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES);            // split-K dQ partials
-  float* const ld_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES + G::RED_BYTES);  // lse2[2][QB], delta[2][QB]
+  char* const k_lds = smem + 4 * QT_BYTES;           // K (workgroup keys)           [DQ only]
+  char* const ds_lds = k_lds + G::K_BYTES;           // dS^T [KB keys][QB q]          [DQ only]
+  float* const red_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES);  // split-K dQ partials [DQ only]
+  float* const ld_lds = reinterpret_cast<float*>(DQ ? ds_lds + G::DS_BYTES + G::RED_BYTES
+                                                    : smem + 4 * QT_BYTES);  // lse2[2][QB], delta[2][QB]
 
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
@@ -495,6 +504,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
     }
   }
   // workgroup K tile -> LDS (B operand of dQ = dS·K by transposed reads)
+  if constexpr (DQ) {
 #pragma unroll
   for (int c = 0; c < KCH; ++c) {
     const int e = tid + NT * c;
@@ -503,6 +513,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
     key = key < T ? key : T - 1;
     *reinterpret_cast<uint4*>(k_lds + swz<D>(row, ch)) =
         *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);
+  }
   }
 
   f32x16 dk[NDT], dv[NDT];
@@ -569,6 +580,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
       }
       // dS^T -> LDS: row = key (32w + r), columns = q (qs*32 + 8g + 4h + 0..3); the bf16
       // values are the dK operand's, 4 per g: dsfr[g >> 1] elements 4(g & 1) .. +3
+      if constexpr (DQ)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qcol = qs * 32 + 8 * g + 4 * h;
@@ -579,6 +591,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
         *reinterpret_cast<uint2*>(ds_lds + swz<QB>(32 * w + r, qcol >> 3) + ((qcol >> 2) & 1) * 8) = u;
       }
     }
+    if constexpr (DQ) {
     __syncthreads();
     // stage the next Q/dO tile now: buffer cur^1 was last read before the previous
     // barrier, and doing it before the dQ atomics keeps their vmcnt out of its wait
@@ -641,6 +654,10 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
         }
       }
     }
+    } else {
+      // buffer cur^1 was last read in the previous iteration, which ended in a barrier
+      { NSA_BWD_STAGE_WRITE(cur ^ 1) }
+    }
     __syncthreads();
   }
 
@@ -666,6 +683,175 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 1) void flash_bwd_kernel(
 }
 #undef NSA_BWD_STAGE_LOAD
 #undef NSA_BWD_STAGE_WRITE
+
+// =============================================================================
+// dQ kernel (split mode): one workgroup = 4 waves x 32 queries of one (b, h), the
+// forward kernel's structure with the LSE known up front (no online max / rescale):
+//   S^T  = K · Q^T,  dP^T = V · dO^T     A = K / V rows from LDS, B = Q^T / dO^T registers
+//   dS^T = P^T ∘ (dP^T − delta),  P^T = exp2(S^T · scale·log2e − lse·log2e)   (lane = query)
+//   dQ^T += K^T · dS^T                  A = K^T by transposed LDS reads, B = dS^T straight
+//                                       from the accumulator registers (bf16)
+// dQ is written once, in bf16, into dqkv[:, :, 0:C]: no atomics, no fp32 accumulator.
+// =============================================================================
+template <int D, bool MASK, bool DROP>
+__device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+                                        const bf16x8 (&gf)[D / 16], f32x16 (&dq)[D / 32], float lse2, float dlt,
+                                        int kv0, int qpos, int h, int r, int lane, float scale_log2,
+                                        const DropArgs& dr) {
+  constexpr int NKS = D / 16;
+  constexpr int NDT = D / 32;
+  f32x16 st[2], pt[2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[sb] = f32x16{};
+    pt[sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
+      st[sb] = mfma(kf, qf[ks], st[sb]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 vf = as_frag(lds_b128(vt, swz<D>(32 * sb + r, 2 * ks + h)));
+      pt[sb] = mfma(vf, gf[ks], pt[sb]);
+    }
+  }
+  bf16x8 dsf[2][2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kpos = kv0 + 32 * sb + acc_row(i, h);
+      float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
+      if constexpr (MASK) {
+        if (kpos > qpos) p = 0.0f;
+      }
+      float dp = pt[sb][i];
+      if constexpr (DROP) {
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
+        dp = nsa_keep(dr.seed, id, dr.thresh) ? dp * dr.scale : 0.0f;
+      }
+      dsf[sb][i >> 3][i & 7] = (__bf16)(p * (dp - dlt));
+    }
+  }
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x8 kf = tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane);
+        dq[dt] = mfma(kf, dsf[sb][s], dq[dt]);
+      }
+    }
+  }
+}
+
+#ifndef NSA_DQK_OCC
+#define NSA_DQK_OCC 3  // waves per SIMD (A/B at B120: 2 -> 1312 us, 3 -> 1262 us, 4 spills -> 1452 us)
+#endif
+template <int D, bool DROP>
+__global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+  constexpr int BN = 64;
+  constexpr int TILE_BYTES = BN * D * 2;
+  constexpr int CPR = D / 8;
+  constexpr int CHUNKS_PER_THREAD = BN * CPR / 256;
+  constexpr int NKS = D / 16;
+  constexpr int NDT = D / 32;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K[2], V[2]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 127) / 128;
+  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int q0 = qt * 128;
+  const int q0w = q0 + 32 * w;
+  const int qpos = q0w + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* kbase = base + C + hh * D;
+  const bf16_t* vbase = base + 2 * C + hh * D;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+
+  // Q^T and dO^T fragments (B operands): lane holds row qpos, d = 16ks + 8h .. +8
+  bf16x8 qf[NKS], gf[NKS];
+  const int qc = qpos < T ? qpos : T - 1;
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
+    gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
+  }
+  const float lse2 = lse[(int64_t)bh * T + qc] * kLog2e;
+  const float dlt = delta[(int64_t)bh * T + qc];
+
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = f32x16{};
+
+  const int kv_end = min(T, q0 + 128);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+
+  uint4 kst[CHUNKS_PER_THREAD], vst[CHUNKS_PER_THREAD];
+#define NSA_DQ_STAGE_LOAD(J)                                                                    \
+  _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
+    const int e = tid + 256 * c;                                                                \
+    const int row = e / CPR, ch = e % CPR;                                                      \
+    int key = (J) * BN + row;                                                                   \
+    key = key < T ? key : T - 1;                                                                \
+    kst[c] = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);       \
+    vst[c] = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * row_stride + ch * 8);       \
+  }
+#define NSA_DQ_STAGE_WRITE(BUF)                                                                 \
+  _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
+    const int e = tid + 256 * c;                                                                \
+    const int row = e / CPR, ch = e % CPR;                                                      \
+    *reinterpret_cast<uint4*>(smem + (BUF) * TILE_BYTES + swz<D>(row, ch)) = kst[c];            \
+    *reinterpret_cast<uint4*>(smem + (2 + (BUF)) * TILE_BYTES + swz<D>(row, ch)) = vst[c];      \
+  }
+  NSA_DQ_STAGE_LOAD(0)
+  NSA_DQ_STAGE_WRITE(0)
+  __syncthreads();
+
+  for (int j = 0; j < n_tiles; ++j) {
+    const int cur = j & 1;
+    const int kv0 = j * BN;
+    { NSA_DQ_STAGE_LOAD(min(j + 1, n_tiles - 1)) }
+    const char* kt = smem + cur * TILE_BYTES;
+    const char* vt = smem + (2 + cur) * TILE_BYTES;
+    if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+      dq_tile<D, false, DROP>(kt, vt, qf, gf, dq, lse2, dlt, kv0, qpos, h, r, lane, scale_log2, dr);
+    else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+      dq_tile<D, true, DROP>(kt, vt, qf, gf, dq, lse2, dlt, kv0, qpos, h, r, lane, scale_log2, dr);
+    { NSA_DQ_STAGE_WRITE(cur ^ 1) }
+    __syncthreads();
+  }
+#undef NSA_DQ_STAGE_LOAD
+#undef NSA_DQ_STAGE_WRITE
+
+  // epilogue: dQ = scale · dQ^T^T -> dqkv[b, qpos, hh*D + d]; lane owns query qpos
+  if (qpos < T) {
+    bf16_t* qrow = dqkv + ((int64_t)b * T + qpos) * row_stride + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = pack2(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
+        u.y = pack2(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(qrow + d) = u;
+      }
+    }
+  }
+}
 
 // dq_acc (fp32 [B, T, C]) -> dqkv[:, :, 0:C] (bf16)
 __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv,
@@ -699,6 +885,8 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
 template <int D>
 hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const void* lse, void* delta, void* dq_acc,
                       void* dqkv, int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
+  // dq_acc == nullptr selects the split mode: dK/dV kernel + per-query-tile dQ kernel
+  const bool split = dq_acc == nullptr;
   const int64_t rows = (int64_t)B * T * H;
   const int64_t threads = rows * (D / 8);
   flash_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
@@ -708,16 +896,32 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_kb = (T + BwdGeo<D>::KB - 1) / BwdGeo<D>::KB;
-  if (th)
-    flash_bwd_kernel<D, true><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
-        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
-        (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
-  else
-    flash_bwd_kernel<D, false><<<n_kb * B * H, BwdGeo<D>::NW * 64, 0, s>>>(
-        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,
-        (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed);
+  const dim3 grid(n_kb * B * H), block(BwdGeo<D>::NW * 64);
+#define NSA_BWD_ARGS                                                                                  \
+  (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,  \
+      (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed
+  if (th) {
+    if (split) flash_bwd_kernel<D, true, false><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
+    else flash_bwd_kernel<D, true, true><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
+  } else {
+    if (split) flash_bwd_kernel<D, false, false><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
+    else flash_bwd_kernel<D, false, true><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
+  }
+#undef NSA_BWD_ARGS
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (split) {
+    const int n_qt = (T + 127) / 128;
+    if (th)
+      flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
+          scale, scale * kLog2e, th, dscale, seed);
+    else
+      flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>(
+          (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
+          scale, scale * kLog2e, th, dscale, seed);
+    return hipGetLastError();
+  }
   const int C = H * D;
   const int64_t work = (int64_t)B * T * (C / 8);
   dq_convert_kernel<<<(unsigned)((work + 255) / 256), 256, 0, s>>>((const float*)dq_acc, (bf16_t*)dqkv,

@@ -32,6 +32,7 @@ and the gradcheck tests).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -506,6 +507,14 @@ def _attn_reference(q, k, v, p, seed):
     return att @ v
 
 
+# Flash-attention backward dQ strategy (csrc/kernels/flash_attn.hip bwd_launch):
+#   split  — dK/dV kernel (no dQ work, 34 KB LDS) + a per-query-tile dQ kernel that
+#            recomputes S and dP and writes dQ once in bf16 (no atomics, no fp32 buffer)
+#   atomic — one kernel; dS crosses LDS, dQ partials are atomically added into an fp32
+#            accumulator, then converted
+FLASH_DQ_SPLIT = os.environ.get("NSA_FLASH_DQ", "split") == "split"
+
+
 class AttentionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, n_head, p):
@@ -538,8 +547,9 @@ class AttentionFn(torch.autograd.Function):
             qkv, y, lse = ctx.saved_tensors
             dy = dy.contiguous()
             dqkv = torch.empty_like(qkv)
-            # zeroed and delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing
-            dq_acc = torch.empty(B, T, C, device=dy.device, dtype=F32)
+            # delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing (which also
+            # zeroes dq_acc in the atomic mode; the split mode writes dQ once, in bf16)
+            dq_acc = None if FLASH_DQ_SPLIT else torch.empty(B, T, C, device=dy.device, dtype=F32)
             delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
             _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
                       _lib.ptr(dq_acc), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())

@@ -76,9 +76,11 @@ def main():
         def fwd():
             _lib.call("nsa_flash_fwd", qkv.data_ptr(), y.data_ptr(), lse.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
-        def bwd():  # the kernel's preprocessing pass zeroes dq itself
+        split = os.environ.get("NSA_FLASH_DQ", "split") == "split"
+
+        def bwd():  # the kernel's preprocessing pass zeroes dq itself (atomic mode)
             _lib.call("nsa_flash_bwd", qkv.data_ptr(), y.data_ptr(), dy.data_ptr(), lse.data_ptr(), delta.data_ptr(),
-                      dq.data_ptr(), dqkv.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
+                      None if split else dq.data_ptr(), dqkv.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
         flops = 4.0 * B * H * T * T * D / 2  # causal
         tf = timeit(fwd)

@@ -214,6 +214,29 @@ def test_flash_attention_deferred_rescale(kernels, pattern):
         assert e < 4e-2, f"{pattern}: d{name} rel err {e}"
 
 
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_flash_bwd_split_matches_atomic(kernels, monkeypatch, p):
+    """The two dQ strategies of the backward (split: separate dQ kernel, bf16 written
+    once; atomic: fp32 atomics from the dK/dV kernel) give the same gradients, with and
+    without dropout (same seed -> same regenerated mask)."""
+    from nanosandbox_amd.ops import functional as fn
+
+    torch.manual_seed(0)
+    B, T, H, D = 2, 320, 3, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
+    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
+    grads = {}
+    for split in (True, False):
+        monkeypatch.setattr(fn, "FLASH_DQ_SPLIT", split)
+        torch.manual_seed(5)  # the dropout seed is drawn from torch's CPU generator
+        x = qkv.clone().requires_grad_(True)
+        fn.attention(x, H, p, True).backward(dy)
+        grads[split] = x.grad.float().view(B, T, 3, H * D)
+    for i, name in enumerate("qkv"):
+        e = rel_err(grads[True][:, :, i], grads[False][:, :, i])
+        assert e < 1e-2, f"d{name}: split vs atomic rel err {e}"
+
+
 def test_flash_attention_dropout_statistics(kernels):
     """With dropout the kernel output is an unbiased estimate of the no-dropout output."""
     from nanosandbox_amd import ops
