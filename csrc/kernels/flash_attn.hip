@@ -455,11 +455,14 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kern
     const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
     float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
   using G = BwdGeo<D>;
-  constexpr int QB = G::QB, KB = G::KB, NT = G::NW * 64;
+#ifndef NSA_BWD_QB_SPLIT
+#define NSA_BWD_QB_SPLIT 64  // queries per staged block in the dK/dV-only kernel (128: 1288 -> 1331 us)
+#endif
+  constexpr int QB = DQ ? G::QB : NSA_BWD_QB_SPLIT, KB = G::KB, NT = G::NW * 64;
   constexpr int CPR = D / 8;
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  constexpr int QT_BYTES = G::QT_BYTES;
+  constexpr int QT_BYTES = QB * D * 2;
   constexpr int QCH = QB * CPR / NT;  // 16-byte chunks per thread per Q (or dO) tile
   constexpr int KCH = KB * CPR / NT;
   static_assert(QCH >= 1 && QB * CPR == QCH * NT, "Q tile staging must divide evenly");
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kern
     { NSA_BWD_STAGE_LOAD(min(qb + 1, n_qb - 1)) }
 
 #pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
+    for (int qs = 0; qs < QB / 32; ++qs) {
       const int qbase_pos = qb * QB + qs * 32;
       // S = Q · K^T  (rows = queries in registers, column = this lane's key)
       f32x16 sacc = f32x16{};
