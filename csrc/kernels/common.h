@@ -112,7 +112,9 @@ static inline uint32_t nsa_drop_thresh(float p) {
 // the normal pdf:  with z = x/sqrt(2), exp(-z^2) = exp(-x^2/2) = sqrt(2 pi) pdf(x).
 __device__ __forceinline__ void nsa_gelu_cdf_pdf(float x, float& cdf, float& pdf) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  // v_rcp_f32 (1 ulp) — __frcp_rn lowers to a full IEEE division sequence here
+  // (v_div_scale x2 / v_div_fmas / v_div_fixup), which made the GELU forward VALU-bound
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
   const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
   const float e = __expf(-z * z);
   const float erf_abs = 1.0f - poly * e;
