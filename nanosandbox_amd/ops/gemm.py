@@ -91,7 +91,10 @@ def wgrad_splits(n_out, n_in, tokens, cus=256):
     return best
 
 
-def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=4):
+WGRAD_MAX_ROUNDS = int(os.environ.get("NSA_WGRAD_MAX_ROUNDS", "6"))
+
+
+def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=None):
     """Split count whose block count fills whole rounds of the CUs best.
 
     The kernels take any split count (split z owns K blocks [z*n/S, (z+1)*n/S)),
@@ -99,6 +102,8 @@ def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=4):
     last round busy) instead of 27 x 16 = 432 = 1.69 rounds (the default rule).
     Ties go to fewer splits (fewer fp32 atomics).
     """
+    if max_rounds is None:
+        max_rounds = WGRAD_MAX_ROUNDS
     tiles = -(-n_out // TILE) * -(-n_in // TILE)
     nkb = max(1, tokens // BK)
     best, best_eff = 1, -1.0
