@@ -163,7 +163,7 @@ def _wt(w):
     mlp.c_proj at 122880 tokens.  Transposing a weight costs microseconds and is
     amortised over every micro-step of an optimizer step.  Inside HIP-graph capture
     the transpose is recomputed (captured into the graph) instead of cached."""
-    if torch.cuda.is_current_stream_capturing():
+    if w.is_cuda and torch.cuda.is_current_stream_capturing():
         return w.t().contiguous()
     key = (_weight_gen, w._version, w.data_ptr())
     hit = getattr(w, "_nsa_wt", None)
