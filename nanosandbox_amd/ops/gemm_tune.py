@@ -274,9 +274,13 @@ def wgrad_acc(dy2, x2, g32):
     cands = {"hipblaslt": cand(_hip_wgrad), "hipblaslt_bf16": cand(_hip_wgrad_bf16)}
     cands.update({f"nsa{v}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, variant=v)) for v in WGRAD_VARIANTS})
     # the same kernels with a split count that fills whole rounds of CUs
-    sb = _gemm.wgrad_splits_balanced(N, K, T)
-    if sb != _gemm.wgrad_splits(N, K, T):
-        cands.update({f"nsa{v}/s{sb}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v))
+    # ... and the split counts that fill 1 / 2 / 3 whole rounds as nearly as possible
+    sdef = _gemm.wgrad_splits(N, K, T)
+    tiles = -(-N // _gemm.TILE) * -(-K // _gemm.TILE)
+    extra = {_gemm.wgrad_splits_balanced(N, K, T)}
+    extra.update(r * 256 // tiles for r in (1, 2, 3))
+    for sb in sorted(x for x in extra if 1 <= x <= max(1, T // _gemm.BK) and x != sdef):
+        cands.update({f"nsa{v}/s{sb}": cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v))
                       for v in WGRAD_VARIANTS})
     name = choose(("wgrad", T, N, K), cands)
     if name == "hipblaslt":
