@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--min-gain", type=float, default=0.02)
     ap.add_argument("--iters", type=int, default=20, help="TunableOp max tuning iterations per solution")
     ap.add_argument("--out", default="nanosandbox_amd/ops/tuned/gfx950_gpt2.csv")
+    ap.add_argument("--shapes", default="c_attn,attn.c_proj,c_fc,mlp.c_proj,lm_head")
     a = ap.parse_args()
     C, V = a.c, a.v
     shapes = {"c_attn": (3 * C, C), "attn.c_proj": (C, C), "c_fc": (4 * C, C), "mlp.c_proj": (C, 4 * C),
@@ -58,12 +59,18 @@ def main():
     keep = {}
     for M in [int(m) for m in a.m.split(",")]:
         for name, (N, K) in shapes.items():
+            if name not in a.shapes.split(","):
+                continue
             x, w, dy = uni(M, K), uni(N, K, scale=0.05), uni(M, N)
+            wt = w.t().contiguous()
             fns = {}
             if "fwd" in a.ops.split(","):
                 fns["fwd"] = lambda: x @ w.t()
             if "dx" in a.ops.split(","):
                 fns["dx"] = lambda: dy @ w
+            if "dxt" in a.ops.split(","):
+                # input grad through the cached K-contiguous weight transpose (ops/gemm_tune._wt)
+                fns["dxt"] = lambda: dy @ wt.t()
             if "dw" in a.ops.split(","):
                 # weight grad with a bf16 result (nanoGPT + autocast semantics), dY^T X
                 fns["dw"] = lambda: dy.t() @ x
