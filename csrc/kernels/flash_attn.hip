@@ -703,49 +703,43 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
                                         const DropArgs& dr) {
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  f32x16 st[2], pt[2];
+  // one 32-key half at a time: S/dP accumulators and dS fragments of a single half are
+  // live at once (register pressure sets this kernel's occupancy)
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
-    st[sb] = f32x16{};
-    pt[sb] = f32x16{};
+    f32x16 st = f32x16{}, pt = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
-      st[sb] = mfma(kf, qf[ks], st[sb]);
+      st = mfma(kf, qf[ks], st);
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const bf16x8 vf = as_frag(lds_b128(vt, swz<D>(32 * sb + r, 2 * ks + h)));
-      pt[sb] = mfma(vf, gf[ks], pt[sb]);
+      pt = mfma(vf, gf[ks], pt);
     }
-  }
-  bf16x8 dsf[2][2];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
+    bf16x8 dsf[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kpos = kv0 + 32 * sb + acc_row(i, h);
-      float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
+      float p = fast_exp2(st[i] * scale_log2 - lse2);
       if constexpr (MASK) {
         if (kpos > qpos) p = 0.0f;
       }
-      float dp = pt[sb][i];
+      float dp = pt[i];
       if constexpr (DROP) {
         const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
         dp = nsa_keep(dr.seed, id, dr.thresh) ? dp * dr.scale : 0.0f;
       }
-      dsf[sb][i >> 3][i & 7] = (__bf16)(p * (dp - dlt));
+      dsf[i >> 3][i & 7] = (__bf16)(p * (dp - dlt));
     }
-  }
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int r0 = 32 * sb + 16 * s + 4 * h;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const bf16x8 kf = tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane);
-        dq[dt] = mfma(kf, dsf[sb][s], dq[dt]);
+        dq[dt] = mfma(kf, dsf[s], dq[dt]);
       }
     }
   }
