@@ -11,7 +11,10 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kUnroll = 4;
+#ifndef NSA_EW_UNROLL
+#define NSA_EW_UNROLL 4  // loads in flight per thread (A/B at 377M elements: 2 / 4 / 8 -> GELU bwd 426 / 399 / 414 us)
+#endif
+constexpr int kUnroll = NSA_EW_UNROLL;
 
 inline int grid_for(int64_t n_vec) {
   int64_t g = (n_vec + kBlock * kUnroll - 1) / (kBlock * kUnroll);

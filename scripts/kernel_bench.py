@@ -114,6 +114,9 @@ def main():
         out["gelu_fwd"] = {"us": t * 1e6, "GBps": 2 * u.numel() * 2 / t / 1e9}
         t2 = timeit(lambda: torch.autograd.backward([ops.gelu(u)], [dg]))
         out["gelu_fwd_bwd"] = {"us": t2 * 1e6, "GBps": 5 * u.numel() * 2 / t2 / 1e9}
+        du = torch.empty_like(dg)
+        t3 = timeit(lambda: _lib.call("nsa_gelu_bwd", dg.data_ptr(), u.data_ptr(), du.data_ptr(), u.numel(), st()))
+        out["gelu_bwd"] = {"us": t3 * 1e6, "GBps": 3 * u.numel() * 2 / t3 / 1e9}
 
     if only is None or "xent" in only:
         logits = torch.randn(N, V, device=dev).to(BF)
