@@ -76,3 +76,17 @@ def test_compile_hip_graph_matches_eager(kernels, tmp_path):
     for a, b in zip(lg, le):
         assert abs(a - b) < 2e-2 * abs(b), (lg, le)
     assert lg[-1] < lg[0]
+
+
+def test_sample_from_checkpoint_gpu(kernels, tmp_path):
+    """sample.py on the GPU (bf16 compute, last-position logits, top-k multinomial) from a
+    checkpoint the GPU trainer wrote; the char codec comes from the dataset's meta.pkl."""
+    from nanosandbox_amd.sample import main as sample_main
+    from nanosandbox_amd.train import Trainer
+
+    Trainer(_cfg(tmp_path, max_iters=4, eval_interval=4)).fit()
+    outs = sample_main([f"--out_dir={tmp_path}", "--num_samples=2", "--max_new_tokens=40", "--start=ab",
+                        "--device=cuda"])
+    assert len(outs) == 2
+    for text in outs:
+        assert text.startswith("ab") and len(text) == 42
