@@ -34,6 +34,23 @@ GLOBAL_MICRO_STEPS = 40  # nanoGPT train_gpt2: 5 * 8
 METRIC = "tokens/sec (whole node) GPT-2 124M DDP"
 
 
+def batch_plan(world: int, micro_batch: int = 0) -> tuple[int, int]:
+    """(micro-batch per rank, global micro-step count) for nanoGPT's fixed 480-sequence step.
+
+    Auto (micro_batch <= 0): the largest divisor of the per-rank batch (480/world
+    sequences) that is <= 120.  The global micro-step count is what the Trainer
+    takes as ``gradient_accumulation_steps`` (nanoGPT divides it by world size),
+    so micro_batch * total_micro == 480 for every world size.
+    """
+    global_seqs = GLOBAL_MICRO_STEPS * 12  # nanoGPT: 12 x 40 = 480 sequences per step
+    assert global_seqs % world == 0, "global batch must divide over the ranks"
+    per_rank_seqs = global_seqs // world
+    if micro_batch <= 0:
+        micro_batch = max(d for d in range(1, 121) if per_rank_seqs % d == 0)
+    assert per_rank_seqs % micro_batch == 0, "micro-batch must divide the per-rank batch"
+    return micro_batch, per_rank_seqs // micro_batch * world
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,14 +84,8 @@ def main():
 
     dims = {"gpt2": (12, 12, 768), "gpt2-medium": (24, 16, 1024), "gpt2-large": (36, 20, 1280),
             "gpt2-xl": (48, 25, 1600)}[args.model]
-    per_rank_seqs = GLOBAL_MICRO_STEPS * 12 // world  # nanoGPT: 12 x 40 = 480 sequences per step
-    assert GLOBAL_MICRO_STEPS * 12 % world == 0, "global batch must divide over the ranks"
-    if args.micro_batch <= 0:
-        args.micro_batch = max(d for d in range(1, 121) if per_rank_seqs % d == 0)
-    assert per_rank_seqs % args.micro_batch == 0, "micro-batch must divide the per-rank batch"
+    args.micro_batch, total_micro = batch_plan(world, args.micro_batch)
     tokens_per_micro = args.micro_batch * args.block_size
-    # keep nanoGPT's 491,520 tokens/step whatever the micro-batch
-    total_micro = per_rank_seqs // args.micro_batch * world
     cfg = dict(TRAIN_DEFAULTS)
     dataset, data_dir = "synthetic", ""
     if args.real_data:
