@@ -11,12 +11,27 @@
 //           (38 MB for GPT-2 124M) ≈ 30 us at the ~1.3 TB/s chip atomic rate.
 //           dwpe — owned per (t, column-octet): the thread sums over the batch
 //           and read-modify-writes the flat buffer, no atomics.
+//
+// The output (the residual stream) and its gradient are bf16 or fp32 (XT): fp32 is
+// nanoGPT's autocast contract (the embedding sum stays fp32), bf16 is opt-in.
 #include "common.h"
 
 namespace {
 
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&f)[8]) { load8(p, f); }
+__device__ __forceinline__ void ld8(const float* p, float (&f)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float (&f)[8]) { store8(p, f); }
+__device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+template <typename XT>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx, const bf16_t* __restrict__ wte,
-                                                     const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out, int N,
+                                                     const bf16_t* __restrict__ wpe, XT* __restrict__ out, int N,
                                                      int T, int C, uint32_t thresh, float scale, uint64_t seed) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -25,7 +40,7 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
   const int64_t tok = idx[row];
   const bf16_t* a = wte + tok * C;
   const bf16_t* p = wpe + (int64_t)t * C;
-  bf16_t* o = out + (int64_t)row * C;
+  XT* o = out + (int64_t)row * C;
   for (int c = lane * 8; c < C; c += 512) {
     float fa[8], fp[8];
     load8(a + c, fa);
@@ -36,22 +51,23 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
       if (thresh) v = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? v * scale : 0.0f;
       fa[j] = v;
     }
-    store8(o + c, fa);
+    st8(o + c, fa);
   }
 }
 
+template <typename XT>
 __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restrict__ idx,
-                                                         const bf16_t* __restrict__ dx, float* __restrict__ dwte, int N,
+                                                         const XT* __restrict__ dx, float* __restrict__ dwte, int N,
                                                          int C, uint32_t thresh, float scale, uint64_t seed) {
   extern __shared__ __attribute__((aligned(16))) float stage[];  // [4][C]
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   float* srow = stage + wv * C;
   for (int row = blockIdx.x * 4 + wv; row < N; row += gridDim.x * 4) {
-    const bf16_t* d = dx + (int64_t)row * C;
+    const XT* d = dx + (int64_t)row * C;
     for (int c = lane * 8; c < C; c += 512) {
       float f[8];
-      load8(d + c, f);
+      ld8(d + c, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float v = f[j];
@@ -69,7 +85,8 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const bf16_t* __restrict__ dx, float* __restrict__ dwpe,
+template <typename XT>
+__global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const XT* __restrict__ dx, float* __restrict__ dwpe,
                                                          int B, int T, int C, uint32_t thresh, float scale,
                                                          uint64_t seed) {
   const int octs = C / 8;
@@ -81,7 +98,7 @@ __global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const bf16_t* __restri
   for (int b = 0; b < B; ++b) {
     const int64_t row = (int64_t)b * T + t;
     float f[8];
-    load8(dx + row * C + c, f);
+    ld8(dx + row * C + c, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = f[j];
@@ -103,31 +120,55 @@ __global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const bf16_t* __restri
   g[1] = g1;
 }
 
-}  // namespace
-
-NSA_API hipError_t nsa_embedding_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
-                                     int C, float p, uint64_t seed, hipStream_t s) {
+template <typename XT>
+hipError_t launch_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T, int C, float p,
+                      uint64_t seed, hipStream_t s) {
   if (C % 8 != 0) return hipErrorInvalidValue;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  emb_fwd_kernel<<<(N + 3) / 4, 256, 0, s>>>((const int64_t*)idx, (const bf16_t*)wte, (const bf16_t*)wpe,
-                                             (bf16_t*)out, N, T, C, th, scale, seed);
+  emb_fwd_kernel<XT><<<(N + 3) / 4, 256, 0, s>>>((const int64_t*)idx, (const bf16_t*)wte, (const bf16_t*)wpe,
+                                                 (XT*)out, N, T, C, th, scale, seed);
   return hipGetLastError();
 }
 
-NSA_API hipError_t nsa_embedding_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T, int C,
-                                     float p, uint64_t seed, hipStream_t s) {
+template <typename XT>
+hipError_t launch_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T, int C, float p,
+                      uint64_t seed, hipStream_t s) {
   if (C % 8 != 0) return hipErrorInvalidValue;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int N = B * T;
   int grid = (N + 3) / 4;
   if (grid > 2048) grid = 2048;
-  emb_bwd_wte_kernel<<<grid, 256, 4 * C * sizeof(float), s>>>((const int64_t*)idx, (const bf16_t*)dx,
-                                                               (float*)dwte, N, C, th, scale, seed);
+  emb_bwd_wte_kernel<XT><<<grid, 256, 4 * C * sizeof(float), s>>>((const int64_t*)idx, (const XT*)dx,
+                                                                   (float*)dwte, N, C, th, scale, seed);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int work = T * (C / 8);
-  emb_bwd_wpe_kernel<<<(work + 255) / 256, 256, 0, s>>>((const bf16_t*)dx, (float*)dwpe, B, T, C, th, scale, seed);
+  emb_bwd_wpe_kernel<XT><<<(work + 255) / 256, 256, 0, s>>>((const XT*)dx, (float*)dwpe, B, T, C, th, scale, seed);
   return hipGetLastError();
+}
+
+}  // namespace
+
+// idx: dense int64 [B*T] (callers pass a contiguous tensor); out / dx: bf16
+NSA_API hipError_t nsa_embedding_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
+                                     int C, float p, uint64_t seed, hipStream_t s) {
+  return launch_fwd<bf16_t>(idx, wte, wpe, out, N, T, C, p, seed, s);
+}
+
+NSA_API hipError_t nsa_embedding_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T, int C,
+                                     float p, uint64_t seed, hipStream_t s) {
+  return launch_bwd<bf16_t>(idx, dx, dwte, dwpe, B, T, C, p, seed, s);
+}
+
+// the same with an fp32 residual stream (out / dx fp32)
+NSA_API hipError_t nsa_embedding_fwd_x32(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
+                                         int C, float p, uint64_t seed, hipStream_t s) {
+  return launch_fwd<float>(idx, wte, wpe, out, N, T, C, p, seed, s);
+}
+
+NSA_API hipError_t nsa_embedding_bwd_x32(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T,
+                                         int C, float p, uint64_t seed, hipStream_t s) {
+  return launch_bwd<float>(idx, dx, dwte, dwpe, B, T, C, p, seed, s);
 }

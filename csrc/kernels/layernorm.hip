@@ -1,5 +1,12 @@
-// LayerNorm forward/backward, bf16 I/O, fp32 statistics (SURVEY.md §2.7 K3;
+// LayerNorm forward/backward, fp32 statistics (SURVEY.md §2.7 K3;
 // nanoGPT LayerNorm: F.layer_norm(x, w.shape, w, b, 1e-5), optional bias).
+//
+// Residual-stream dtype XT: the normalised output h and the branch tensors are
+// bf16, the residual stream x / s = x + branch and its gradient are XT — fp32 by
+// default, which is nanoGPT's autocast contract (fp32 embedding output, fp32 + bf16
+// residual adds, fp32 LayerNorm input), or bf16 (opt-in, half the residual bytes).
+// With XT = fp32 the fused backward writes the residual gradient in fp32 and, for
+// the branch GEMMs, a bf16 copy of it in the same pass.
 //
 // Layout: one 64-lane wave owns one row; lane l holds columns
 // (k*64 + l)*8 .. +8 for k < NK, so a row of C <= 512*NK bf16 values lives in
@@ -18,29 +25,67 @@
 
 namespace {
 
-template <int NK>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                                    bf16_t* __restrict__ sum_out, const bf16_t* __restrict__ w,
+// 8 consecutive elements of a bf16 or fp32 row as raw 16-byte words
+template <typename T>
+struct Raw8 {
+  static constexpr int W = sizeof(T) / 2;  // uint4 words: 1 for bf16, 2 for fp32
+  uint4 u[W];
+};
+
+template <typename T>
+__device__ __forceinline__ Raw8<T> ld_raw(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < Raw8<T>::W; ++i) r.u[i] = reinterpret_cast<const uint4*>(p)[i];
+  return r;
+}
+
+__device__ __forceinline__ void unpack_raw(const Raw8<bf16_t>& r, float (&f)[8]) { unpack8(r.u[0], f); }
+__device__ __forceinline__ void unpack_raw(const Raw8<float>& r, float (&f)[8]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f[4 * i + 0] = __uint_as_float(r.u[i].x);
+    f[4 * i + 1] = __uint_as_float(r.u[i].y);
+    f[4 * i + 2] = __uint_as_float(r.u[i].z);
+    f[4 * i + 3] = __uint_as_float(r.u[i].w);
+  }
+}
+
+__device__ __forceinline__ void load8x(const bf16_t* p, float (&f)[8]) { load8(p, f); }
+__device__ __forceinline__ void load8x(const float* p, float (&f)[8]) { unpack_raw(ld_raw(p), f); }
+__device__ __forceinline__ void store8x(bf16_t* p, const float (&f)[8]) { store8(p, f); }
+__device__ __forceinline__ void store8x(float* p, const float (&f)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+// value as stored in the residual stream (bf16 rounding for a bf16 stream)
+__device__ __forceinline__ float as_stream(float v, bf16_t*) { return bf2f(f2bf(v)); }
+__device__ __forceinline__ float as_stream(float v, float*) { return v; }
+
+template <int NK, typename XT>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, const bf16_t* __restrict__ res,
+                                                    XT* __restrict__ sum_out, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                     int N, int C, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
-  const bf16_t* xr = x + (int64_t)row * C;
+  const XT* xr = x + (int64_t)row * C;
   float v[NK][8];
   float s = 0.0f;
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (c < C) {
-      load8(xr + c, v[k]);
-      if (res) {  // fused residual add: s = x + res, written out (bf16) and normalised
+      load8x(xr + c, v[k]);
+      if (res) {  // fused residual add: s = x + res, written out (XT) and normalised
         float rv[8];
         load8(res + (int64_t)row * C + c, rv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + rv[j]));
-        store8(sum_out + (int64_t)row * C + c, v[k]);
+        for (int j = 0; j < 8; ++j) v[k][j] = as_stream(v[k][j] + rv[j], (XT*)nullptr);
+        store8x(sum_out + (int64_t)row * C + c, v[k]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[k][j];
@@ -94,11 +139,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
 // xhat and dy*w are recomputed from the raw words in the second pass rather than
 // kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
-template <int NK, bool PIPE>
-__global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+template <int NK, bool PIPE, typename XT>
+__global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const XT* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
-                                                    const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
-                                                    bf16_t* __restrict__ dx,
+                                                    const float* __restrict__ rstd_in, const XT* __restrict__ dres,
+                                                    XT* __restrict__ dx, bf16_t* __restrict__ dx_branch,
                                                     float* __restrict__ dw_part, float* __restrict__ db_part, int N,
                                                     int C) {
   // dw / db partial sums live in LDS, one [C] slice per wave (no sharing inside
@@ -122,21 +167,23 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
   }
   const int row_step = gridDim.x * 4;
   int row = blockIdx.x * 4 + wv;
-  uint4 nx[NK], nd[NK], nr[NK];
+  Raw8<XT> nx[NK], nr[NK];
+  uint4 nd[NK];
 #define NSA_LNB_LOAD(R)                                                                  \
   _Pragma("unroll") for (int k = 0; k < NK; ++k) {                                       \
     const int c = min((k * 64 + lane) * 8, C - 8);                                       \
     const int64_t off = (int64_t)min((R), N - 1) * C + c;                                \
-    nx[k] = *reinterpret_cast<const uint4*>(x + off);                                    \
+    nx[k] = ld_raw(x + off);                                                             \
     nd[k] = *reinterpret_cast<const uint4*>(dy + off);                                   \
-    if (dres) nr[k] = *reinterpret_cast<const uint4*>(dres + off);                       \
+    if (dres) nr[k] = ld_raw(dres + off);                                                \
   }
   if (PIPE) NSA_LNB_LOAD(row)
   for (; row < N; row += row_step) {
     if (!PIPE) NSA_LNB_LOAD(row)
     const float mean = mean_in[row];
     const float rstd = rstd_in[row];
-    uint4 cx[NK], cd[NK], cr[NK];
+    Raw8<XT> cx[NK], cr[NK];
+    uint4 cd[NK];
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       cx[k] = nx[k];
@@ -150,7 +197,7 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
         float xv[8], dv[8], wf[8], aw[8], ab[8];
-        unpack8(cx[k], xv);
+        unpack_raw(cx[k], xv);
         unpack8(cd[k], dv);
         unpack8(wraw[k], wf);
         float4* pw = reinterpret_cast<float4*>(accw + c);
@@ -181,18 +228,19 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
         float xv[8], dv[8], wf[8], o[8];
-        unpack8(cx[k], xv);
+        unpack_raw(cx[k], xv);
         unpack8(cd[k], dv);
         unpack8(wraw[k], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[j] * wf[j] - m1 - (xv[j] - mean) * rstd * m2);
         if (dres) {  // gradient arriving through the residual path of the fused add
           float rv[8];
-          unpack8(cr[k], rv);
+          unpack_raw(cr[k], rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
-        store8(dx + (int64_t)row * C + c, o);
+        store8x(dx + (int64_t)row * C + c, o);
+        if (dx_branch) store8(dx_branch + (int64_t)row * C + c, o);  // bf16 copy for the branch GEMMs
       }
     }
   }
@@ -207,30 +255,30 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
   }
 }
 
-template <int NK>
+template <int NK, typename XT>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
                       void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
-  ln_fwd_kernel<NK><<<(N + 3) / 4, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, (bf16_t*)sum_out,
-                                                (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (float*)mean,
-                                                (float*)rstd, N, C, eps);
+  ln_fwd_kernel<NK, XT><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
+                                                    (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (float*)mean,
+                                                    (float*)rstd, N, C, eps);
   return hipGetLastError();
 }
 
-template <int NK>
+template <int NK, typename XT>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd,
-                      const void* dres, void* dx, void* dw_part, void* db_part, int N, int C, int nblk,
-                      hipStream_t s) {
+                      const void* dres, void* dx, void* dx_branch, void* dw_part, void* db_part, int N, int C,
+                      int nblk, hipStream_t s) {
   // bit 30 of nblk selects the non-pipelined body (A/B timing)
   const bool pipe = !(nblk & (1 << 30));
   nblk &= ~(1 << 30);
   if (pipe)
-    ln_bwd_kernel<NK, true><<<nblk, 256, 8 * C * sizeof(float), s>>>(
-        (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-        (const bf16_t*)dres, (bf16_t*)dx, (float*)dw_part, (float*)db_part, N, C);
+    ln_bwd_kernel<NK, true, XT><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
   else
-    ln_bwd_kernel<NK, false><<<nblk, 256, 8 * C * sizeof(float), s>>>(
-        (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-        (const bf16_t*)dres, (bf16_t*)dx, (float*)dw_part, (float*)db_part, N, C);
+    ln_bwd_kernel<NK, false, XT><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
   return hipGetLastError();
 }
 
@@ -251,11 +299,18 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* 
       return hipErrorInvalidValue;                          \
   }
 
-// y = LN(x [+ res]) ; with res != NULL also writes sum_out = x + res (bf16)
+// y = LN(x [+ res]) ; with res != NULL also writes sum_out = x + res.
+// x / sum_out are bf16 (nsa_layernorm_fwd) or fp32 (nsa_layernorm_fwd_x32); res, w, b, y bf16.
 NSA_API hipError_t nsa_layernorm_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b,
                                      void* y, void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
   if (C % 8 != 0) return hipErrorInvalidValue;
-  NSA_NK_SWITCH((C + 511) / 512, launch_fwd<K_>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s));
+  NSA_NK_SWITCH((C + 511) / 512, (launch_fwd<K_, bf16_t>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s)));
+}
+
+NSA_API hipError_t nsa_layernorm_fwd_x32(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                                         void* y, void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512, (launch_fwd<K_, float>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s)));
 }
 
 // dx = LN'(dy) [+ dres]; per-block dw/db partial rows for nsa_colsum_accum
@@ -263,5 +318,15 @@ NSA_API hipError_t nsa_layernorm_bwd(const void* dy, const void* x, const void* 
                                      const void* rstd, const void* dres, void* dx, void* dw_part, void* db_part,
                                      int N, int C, int nblk, hipStream_t s) {
   if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
-  NSA_NK_SWITCH((C + 511) / 512, launch_bwd<K_>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, N, C, nblk, s));
+  NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, bf16_t>(dy, x, w, mean, rstd, dres, dx, nullptr, dw_part, db_part,
+                                                         N, C, nblk, s)));
+}
+
+// fp32 residual stream: x, dres, dx fp32; dx_branch (optional) = bf16(dx) for the branch GEMMs
+NSA_API hipError_t nsa_layernorm_bwd_x32(const void* dy, const void* x, const void* w, const void* mean,
+                                         const void* rstd, const void* dres, void* dx, void* dx_branch,
+                                         void* dw_part, void* db_part, int N, int C, int nblk, hipStream_t s) {
+  if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
+                                                        N, C, nblk, s)));
 }

@@ -58,6 +58,7 @@ TRAIN_DEFAULTS = dict(
     ddp_bucket_mb=64,  # gradient bucket cap; 64 MiB suits ring all-reduce over 7 xGMI links
     grad_reduce_dtype="float32",  # 'float32' | 'bfloat16' (compressed all-reduce)
     grad_ckpt=False,  # recompute each Block in backward (activation checkpointing)
+    fp32_residual=True,  # residual stream + its gradient in fp32 (nanoGPT autocast contract); False: bf16
     metrics_jsonl=True,  # write <out_dir>/metrics.jsonl
     tensorboard_dir="",  # '' disables; else tfevents written to <tensorboard_dir>/<run>
     auto_resume=False,  # resume from <out_dir>/ckpt.pt if it exists (elastic restarts)

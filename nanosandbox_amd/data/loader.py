@@ -177,7 +177,7 @@ class SyntheticBatchSource:
     def get_batch(self, split):
         d = torch.randint(0, self.vocab_size, (self.batch_size, self.block_size + 1), device=self.device,
                           generator=self.gen)
-        return d[:, :-1], d[:, 1:]
+        return d[:, :-1].contiguous(), d[:, 1:].contiguous()
 
 
 def make_batch_source(dataset, data_dir, block_size, batch_size, device, seed, vocab_size=50304, impl="auto"):

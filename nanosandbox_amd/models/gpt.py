@@ -49,9 +49,10 @@ class LayerNorm(nn.Module):
         super().__init__()
         self.weight = nn.Parameter(torch.ones(ndim))
         self.bias = nn.Parameter(torch.zeros(ndim)) if bias else None
+        self.out_dtype = None  # compute dtype of the normalised output (None: x's dtype)
 
     def forward(self, x):
-        return ops.layer_norm(x, self.weight, self.bias)
+        return ops.layer_norm(x, self.weight, self.bias, out_dtype=self.out_dtype)
 
 
 class CausalSelfAttention(nn.Module):
@@ -124,6 +125,7 @@ class GPT(nn.Module):
         self.config = config
         self.grad_ckpt = False
         self.compute_dtype = torch.float32
+        self.residual_dtype = torch.float32
 
         self.transformer = nn.ModuleDict(dict(
             wte=nn.Embedding(config.vocab_size, config.n_embd),
@@ -160,9 +162,19 @@ class GPT(nn.Module):
         elif isinstance(module, nn.Embedding):
             torch.nn.init.normal_(module.weight, mean=0.0, std=0.02)
 
-    def set_compute_dtype(self, dtype: torch.dtype):
-        """Activation dtype of the forward pass (bf16 on MI355X, fp32 on CPU)."""
+    def set_compute_dtype(self, dtype: torch.dtype, residual_dtype: torch.dtype = torch.float32):
+        """Activation dtype of the forward pass (bf16 on MI355X, fp32 on CPU).
+
+        ``residual_dtype`` is the dtype of the residual stream (embedding sum, the
+        x of ``x = x + f(ln(x))``) and of its gradient.  fp32 by default: that is
+        nanoGPT's autocast contract, where the embedding output is fp32 and every
+        fp32 + bf16 residual add promotes to fp32.  bf16 halves the residual bytes
+        (opt-in, ``fp32_residual=False``)."""
         self.compute_dtype = dtype
+        self.residual_dtype = residual_dtype if dtype != torch.float32 else torch.float32
+        for m in self.modules():
+            if isinstance(m, LayerNorm):
+                m.out_dtype = dtype
         return self
 
     # ---------------------------------------------------------------- forward
@@ -172,7 +184,7 @@ class GPT(nn.Module):
             f"Cannot forward sequence of length {t}, block size is only {self.config.block_size}"
         tr = self.transformer
         x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, self.config.dropout, self.training,
-                          dtype=self.compute_dtype)
+                          dtype=self.residual_dtype)
         x = self._trunk(x)
 
         if targets is not None:
@@ -201,7 +213,7 @@ class GPT(nn.Module):
     def forward_logits(self, idx):
         """Full [B, T, V] fp32 logits (evaluation / tests)."""
         tr = self.transformer
-        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.compute_dtype)
+        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.residual_dtype)
         return ops.lm_head_logits(self._trunk(x), self.lm_head.weight)
 
     # ------------------------------------------------------------ surgery/api

@@ -37,6 +37,14 @@ c_float = ctypes.c_float
 _SIGNATURES = {
     "nsa_embedding_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_uint64, c_void_p],
     "nsa_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_uint64, c_void_p],
+    "nsa_embedding_fwd_x32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_uint64,
+                              c_void_p],
+    "nsa_embedding_bwd_x32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_uint64,
+                              c_void_p],
+    "nsa_layernorm_fwd_x32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_int, c_int, c_float, c_void_p],
+    "nsa_layernorm_bwd_x32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "nsa_layernorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_float, c_void_p],
     "nsa_layernorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -172,13 +172,19 @@ class EmbeddingFn(torch.autograd.Function):
         V, C = wte.shape
         seed = new_seed() if p > 0 else 0
         ctx.p, ctx.seed, ctx.shape = p, seed, (B, T, V, C)
+        # the kernels index idx as a dense [B*T] array in both passes: save the
+        # contiguous copy (a sliced batch such as d[:, :-1] has row stride T+1)
+        idx = idx.contiguous()
         ctx.save_for_backward(idx, wte, wpe)
         if idx.is_cuda:
+            # bf16 weight shadows; the sum (the residual stream) is written in ``dtype``:
+            # fp32 (nanoGPT autocast contract) or bf16
             assert C % 8 == 0, "embedding kernel needs n_embd % 8 == 0"
-            idx = idx.contiguous()
+            assert dtype in (F32, BF16)
             out = torch.empty(B, T, C, device=idx.device, dtype=dtype)
-            _lib.call("nsa_embedding_fwd", _lib.ptr(idx), _lib.ptr(compute_weight(wte, dtype)),
-                      _lib.ptr(compute_weight(wpe, dtype)), _lib.ptr(out), B * T, T, C, p, seed, _lib.stream())
+            _lib.call("nsa_embedding_fwd_x32" if dtype == F32 else "nsa_embedding_fwd", _lib.ptr(idx),
+                      _lib.ptr(compute_weight(wte, BF16)), _lib.ptr(compute_weight(wpe, BF16)), _lib.ptr(out),
+                      B * T, T, C, p, seed, _lib.stream())
             return out
         x = wte.detach()[idx] + wpe.detach()[:T].unsqueeze(0)
         if p > 0:
@@ -190,6 +196,7 @@ class EmbeddingFn(torch.autograd.Function):
         idx, wte, wpe = ctx.saved_tensors
         B, T, V, C = ctx.shape
         if dx.is_cuda:
+            assert idx.is_contiguous()
             dx = dx.contiguous()
             _streams.join(dx.device)  # the tied lm_head weight gradient may still be on the side stream
             gwte = getattr(wte, "main_grad", None)
@@ -200,8 +207,9 @@ class EmbeddingFn(torch.autograd.Function):
                 gwte = torch.zeros(V, C, device=dx.device, dtype=F32)
             if ret_wpe:
                 gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
-            _lib.call("nsa_embedding_bwd", _lib.ptr(idx), _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe),
-                      B, T, C, ctx.p, ctx.seed, _lib.stream())
+            assert dx.dtype in (F32, BF16)
+            _lib.call("nsa_embedding_bwd_x32" if dx.dtype == F32 else "nsa_embedding_bwd", _lib.ptr(idx),
+                      _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe), B, T, C, ctx.p, ctx.seed, _lib.stream())
             out_wte = gwte.to(wte.dtype) if ret_wte else None
             out_wpe = gwpe.to(wpe.dtype) if ret_wpe else None
             if not ret_wte:
@@ -233,35 +241,50 @@ LN_EPS = 1e-5
 # 144 us at 122880 x 768 (5.2 TB/s) vs 148-168 us for 1024-3072 blocks
 # (scripts/membound_ab.py)
 _LN_BWD_BLOCKS = 768
+# fp32 residual stream: ~174 VGPRs -> 2 resident 256-thread blocks per CU
+_LN_BWD_BLOCKS_X32 = 512
 
 
 class LayerNormFn(torch.autograd.Function):
     """h = LN(x [+ y]).  With ``y`` the residual add is fused: returns (s = x + y, h).
+
+    The residual stream x / s (and its gradient) keeps x's dtype; y and h are in
+    the compute dtype.  On MI355X with an fp32 residual stream (nanoGPT's autocast
+    contract: fp32 embedding sum, fp32 + bf16 residual adds) h is bf16 and the
+    backward hands y a bf16 copy of the fp32 residual gradient written by the same
+    kernel pass.
 
     Backward of the fused form: ds_total = LN'(dh) + ds (gradient that reached s
     through the residual stream), computed in one kernel pass, and returned as
     the gradient of both x and y — no separate autograd add kernel."""
 
     @staticmethod
-    def forward(ctx, x, y, w, b):
+    def forward(ctx, x, y, w, b, out_dtype):
         ctx.set_materialize_grads(False)
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         N = x2.shape[0]
         ctx.has_bias = b is not None
         ctx.fused = y is not None
+        out_dtype = out_dtype or (y.dtype if y is not None else x.dtype)
+        ctx.y_dtype = y.dtype if y is not None else None
         if x.is_cuda:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
+            x32 = x.dtype == F32
+            assert x.dtype in (F32, BF16) and out_dtype == BF16, "layernorm kernel: bf16/fp32 stream, bf16 out"
             x2 = x2.contiguous()
             y2 = y.reshape(-1, C).contiguous() if y is not None else None
+            if y2 is not None:
+                assert y2.dtype == BF16
             s2 = torch.empty_like(x2) if y is not None else None
-            h = torch.empty_like(x2)
+            h = torch.empty(N, C, device=x.device, dtype=out_dtype)
             mean = torch.empty(N, device=x.device, dtype=F32)
             rstd = torch.empty(N, device=x.device, dtype=F32)
-            wc = compute_weight(w, x.dtype)
-            bc = compute_weight(b, x.dtype) if b is not None else None
-            _lib.call("nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(y2), _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc),
-                      _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C, LN_EPS, _lib.stream())
+            wc = compute_weight(w, out_dtype)
+            bc = compute_weight(b, out_dtype) if b is not None else None
+            _lib.call("nsa_layernorm_fwd_x32" if x32 else "nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(y2),
+                      _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C,
+                      LN_EPS, _lib.stream())
             inp = s2 if y is not None else x2
         else:
             xf = x2.float()
@@ -274,11 +297,12 @@ class LayerNormFn(torch.autograd.Function):
             h = (xf - mean[:, None]) * rstd[:, None] * w.detach().float()
             if b is not None:
                 h = h + b.detach().float()
-            h = h.to(x.dtype)
+            h = h.to(out_dtype)
         ctx.save_for_backward(inp, w, b if b is not None else mean, mean, rstd)
+        hshape = (*x.shape[:-1], C)
         if y is not None:
-            return inp.view(x.shape), h.view(x.shape)
-        return h.view(x.shape)
+            return inp.view(x.shape), h.view(hshape)
+        return h.view(hshape)
 
     @staticmethod
     def backward(ctx, *grads):
@@ -290,24 +314,38 @@ class LayerNormFn(torch.autograd.Function):
         b = b_or_mean if ctx.has_bias else None
         C = x2.shape[-1]
         N = x2.shape[0]
-        shape = (dh if dh is not None else ds).shape
+        shape = (*(dh if dh is not None else ds).shape[:-1], C)
         if dh is None:  # only the residual output was used
-            return ds, (ds if ctx.fused else None), None, None
+            dyb = ds.to(ctx.y_dtype) if ctx.fused else None
+            return ds, dyb, None, None, None
         dy2 = dh.reshape(-1, C)
         if dh.is_cuda:
+            x32 = x2.dtype == F32
             dy2 = dy2.contiguous()
             ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
+            if ds2 is not None and ds2.dtype != x2.dtype:
+                ds2 = ds2.to(x2.dtype)
             dx = torch.empty_like(x2)
-            nblk = min(_LN_BWD_BLOCKS, max(1, (N + 7) // 8))
+            # the fused form also hands the branch (y) its gradient in y's dtype
+            dyb = torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype) if (ctx.fused and x32) else None
+            nblk = min(_LN_BWD_BLOCKS_X32 if x32 else _LN_BWD_BLOCKS, max(1, (N + 7) // 8))
             dw_part = torch.empty(nblk, C, device=dh.device, dtype=F32)
             db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
-            _lib.call("nsa_layernorm_bwd", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(compute_weight(w, x2.dtype)),
-                      _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dw_part),
-                      _lib.ptr(db_part), N, C, nblk, _lib.stream())
+            wc = compute_weight(w, dy2.dtype)
+            if x32:
+                _lib.call("nsa_layernorm_bwd_x32", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
+                          _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dyb), _lib.ptr(dw_part),
+                          _lib.ptr(db_part), N, C, nblk, _lib.stream())
+            else:
+                _lib.call("nsa_layernorm_bwd", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
+                          _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dw_part), _lib.ptr(db_part), N, C,
+                          nblk, _lib.stream())
             gw = _colsum_into(w, dw_part)
             gb = _colsum_into(b, db_part) if b is not None else None
             dx = dx.view(shape)
-            return dx, (dx if ctx.fused else None), gw, gb
+            if not ctx.fused:
+                return dx, None, gw, gb, None
+            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None
         xf = x2.float()
         d = dy2.float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
@@ -318,8 +356,10 @@ class LayerNormFn(torch.autograd.Function):
             dx = dx + ds.reshape(-1, C).float()
         gw = _accumulate(w, (d * xhat).sum(0))
         gb = _accumulate(b, d.sum(0)) if b is not None else None
-        dx = dx.to(dh.dtype).view(shape)
-        return dx, (dx if ctx.fused else None), gw, gb
+        dxs = dx.to(x2.dtype).view(shape)
+        if not ctx.fused:
+            return dxs, None, gw, gb, None
+        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None
 
 
 def _colsum_into(p, partial):
@@ -335,13 +375,17 @@ def _colsum_into(p, partial):
     return out.to(p.dtype)
 
 
-def layer_norm(x, w, b):
-    return LayerNormFn.apply(x, None, w, b)
+def layer_norm(x, w, b, out_dtype=None):
+    """LN(x); ``out_dtype`` (default x's dtype) is the dtype of the normalised output."""
+    return LayerNormFn.apply(x, None, w, b, out_dtype)
 
 
-def add_layer_norm(x, y, w, b):
-    """Fused residual add + LayerNorm: returns (x + y, LN(x + y))."""
-    return LayerNormFn.apply(x, y, w, b)
+def add_layer_norm(x, y, w, b, out_dtype=None):
+    """Fused residual add + LayerNorm: returns (x + y, LN(x + y)).
+
+    x + y keeps x's (residual-stream) dtype; LN(x + y) is in ``out_dtype``
+    (default y's dtype, the compute dtype)."""
+    return LayerNormFn.apply(x, y, w, b, out_dtype)
 
 
 # ----------------------------------------------------------------------------
@@ -617,10 +661,15 @@ class LMHeadLossFn(torch.autograd.Function):
         g = (gl.float() / n_valid)
         wc = compute_weight(w, x2.dtype)
         if x2.is_cuda:
-            xs = x2 * g.to(x2.dtype)
+            # the loss scale g = grad / n_valid stays fp32 (a device scalar read by the
+            # kernel): only the scaled products are rounded to bf16, not g itself
+            g = g.reshape(1).contiguous()
+            xs = torch.empty_like(x2)
+            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2.contiguous()), _lib.ptr(xs), _lib.ptr(g), xs.numel(),
+                      _lib.stream())
             gw = weight_grad(w, dlogits, xs)
             dx = _tune.dgrad(dlogits, wc)
-            dx.mul_(g.to(dx.dtype))
+            _lib.call("nsa_scale_rows_bf16", _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())
             return dx.view(ctx.xshape), gw, None, None
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)

@@ -58,7 +58,9 @@ def _save():
     if not path:
         return
     try:
-        tmp = path + ".tmp"
+        # per-process temp name: under torchrun every rank saves, and a shared
+        # temp file could interleave writes before the atomic replace
+        tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "w") as f:
             json.dump({json.dumps(list(k)): v for k, v in _table.items()}, f, indent=1)
         os.replace(tmp, path)
@@ -66,6 +68,7 @@ def _save():
         pass
 
 
+WGRAD_ALLOW_BF16 = os.environ.get("NSA_WGRAD_ALLOW_BF16", "0") == "1"
 NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
 WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
 
@@ -271,7 +274,12 @@ def wgrad_acc(dy2, x2, g32):
             fn(dy2, x2, scratch)
         return run
 
-    cands = {"hipblaslt": cand(_hip_wgrad), "hipblaslt_bf16": cand(_hip_wgrad_bf16)}
+    # every default candidate keeps dW in fp32 until it is added into the fp32
+    # accumulator; the bf16-rounding library path changes gradient precision, so a
+    # speed race never picks it unless asked for (NSA_WGRAD_ALLOW_BF16=1)
+    cands = {"hipblaslt": cand(_hip_wgrad)}
+    if WGRAD_ALLOW_BF16:
+        cands["hipblaslt_bf16"] = cand(_hip_wgrad_bf16)
     cands.update({f"nsa{v}": cand(lambda a, b, c, v=v: _gemm.wgrad_acc(a, b, c, variant=v)) for v in WGRAD_VARIANTS})
     # the same kernels with a split count that fills whole rounds of CUs
     # ... and the split counts that fill 1 / 2 / 3 whole rounds as nearly as possible

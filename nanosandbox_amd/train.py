@@ -115,7 +115,8 @@ class Trainer:
             model_args["block_size"] = c["block_size"]
         self.model_args = model_args
         model.to(self.device)
-        model.set_compute_dtype(self.compute_dtype)
+        model.set_compute_dtype(self.compute_dtype,
+                                torch.float32 if c["fp32_residual"] else self.compute_dtype)
         model.grad_ckpt = c["grad_ckpt"]
         print(f"number of parameters: {model.get_num_params() / 1e6:.2f}M")
 

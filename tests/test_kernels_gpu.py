@@ -64,6 +64,65 @@ def test_layernorm(kernels, N, C, bias, fused):
         assert rel_err(gb, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("N,C,bias", [(300, 768, True), (129, 384, False), (33, 1600, True)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_add_layernorm_fp32_stream(kernels, N, C, bias, fused):
+    """fp32 residual stream (nanoGPT autocast contract): s = x + y in fp32,
+    h = LN(s) in bf16; backward writes the fp32 residual gradient and a bf16
+    copy for the branch in one pass."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, device=DEV) * 2 + 0.5).requires_grad_(True)  # fp32 stream
+    y = torch.randn(N, C, device=DEV).to(BF).requires_grad_(True)  # bf16 branch
+    w = param(torch.randn(C, device=DEV) * 0.5 + 1, fused)
+    b = param(torch.randn(C, device=DEV) * 0.1, fused) if bias else None
+    s, h = ops.add_layer_norm(x, y, w, b)
+    assert s.dtype == torch.float32 and h.dtype == BF
+    dh = torch.randn(N, C, device=DEV).to(BF)
+    ds = torch.randn(N, C, device=DEV) * 0.1
+    torch.autograd.backward([s, h], [ds, dh])
+    assert x.grad.dtype == torch.float32 and y.grad.dtype == BF
+
+    xr = x.detach().clone().requires_grad_(True)
+    yr = y.detach().float().requires_grad_(True)
+    wr = w.compute.float().requires_grad_(True)
+    br = b.compute.float().requires_grad_(True) if bias else None
+    sr = xr + yr
+    hr = F.layer_norm(sr, (C,), wr, br, 1e-5)
+    torch.autograd.backward([sr, hr], [ds, dh.float()])
+    assert rel_err(s, sr) < 1e-6  # the sum is exact fp32
+    assert rel_err(h, hr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 1e-4
+    assert rel_err(y.grad, yr.grad) < 1e-2
+    gw = w.main_grad if fused else w.grad
+    assert rel_err(gw, wr.grad) < 1e-3
+    if bias:
+        gb = b.main_grad if fused else b.grad
+        assert rel_err(gb, br.grad) < 1e-3
+
+
+def test_layernorm_fp32_in_bf16_out(kernels):
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    N, C = 257, 768
+    x = (torch.randn(N, C, device=DEV) * 3).requires_grad_(True)
+    w = param(torch.randn(C, device=DEV) * 0.5 + 1)
+    h = ops.layer_norm(x, w, None, out_dtype=BF)
+    assert h.dtype == BF
+    dh = torch.randn(N, C, device=DEV).to(BF)
+    h.backward(dh)
+    assert x.grad.dtype == torch.float32
+    xr = x.detach().clone().requires_grad_(True)
+    wr = w.compute.float().requires_grad_(True)
+    hr = F.layer_norm(xr, (C,), wr, None, 1e-5)
+    hr.backward(dh.float())
+    assert rel_err(h, hr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 1e-4
+    assert rel_err(w.grad, wr.grad) < 1e-3
+
+
 # --------------------------------------------------------------------- gelu
 @pytest.mark.parametrize("n", [12288 * 8, 1000, 7])
 def test_gelu(kernels, n):
@@ -100,6 +159,30 @@ def test_embedding(kernels, B, T, V, C):
     gwpe[:T] = dx.float().sum(0)
     assert rel_err(wte.main_grad, gwte) < 1e-5
     assert rel_err(wpe.main_grad, gwpe) < 1e-5
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_embedding_noncontiguous_idx(kernels, fused):
+    """idx sliced out of a [B, T+1] token block (row stride T+1), as a batch
+    sampler hands it over: the wte gradient must land on the right rows."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(1)
+    B, T, V, C = 6, 64, 500, 256
+    d = torch.randint(0, V, (B, T + 1), device=DEV)
+    idx = d[:, :-1]
+    assert not idx.is_contiguous()
+    wte = param(torch.randn(V, C, device=DEV) * 0.02, fused=fused)
+    wpe = param(torch.randn(T, C, device=DEV) * 0.02, fused=fused)
+    x = ops.embedding(idx, wte, wpe, 0.0, True, dtype=BF)
+    dx = torch.randn(B, T, C, device=DEV).to(BF)
+    x.backward(dx)
+    ic = idx.contiguous()
+    ref = wte.compute.float()[ic] + wpe.compute.float()[None]
+    assert rel_err(x, ref) < 1e-2
+    gwte = torch.zeros(V, C, device=DEV).index_add_(0, ic.reshape(-1), dx.float().reshape(-1, C))
+    got = wte.main_grad if fused else wte.grad.float()
+    assert rel_err(got, gwte) < (1e-5 if fused else 1e-2)
 
 
 # ------------------------------------------------------------ cross-entropy
@@ -304,6 +387,52 @@ def test_gpt_gpu_matches_cpu_reference(kernels, bias):
     sg = FlatParamStore(mg, DEV, compute_dtype=BF)
     idx = torch.randint(0, 1000, (4, 128))
     tgt = torch.randint(0, 1000, (4, 128))
+    _, lc = mc(idx, tgt)
+    lc.backward()
+    _, lg = mg(idx.to(DEV), tgt.to(DEV))
+    lg.backward()
+    assert abs(lc.item() - lg.item()) < 2e-2
+    assert rel_err(sg.grad.cpu(), sc.grad) < 5e-2
+
+
+@pytest.mark.parametrize("fp32_residual", [True, False])
+def test_embedding_fp32_stream(kernels, fp32_residual):
+    """The embedding sum in the residual dtype (fp32 default, bf16 opt-in)."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(0)
+    B, T, V, C = 4, 96, 700, 384
+    dt = torch.float32 if fp32_residual else BF
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    wte = param(torch.randn(V, C, device=DEV) * 0.02, fused=True)
+    wpe = param(torch.randn(T, C, device=DEV) * 0.02, fused=True)
+    x = ops.embedding(idx, wte, wpe, 0.0, True, dtype=dt)
+    assert x.dtype == dt
+    dx = torch.randn(B, T, C, device=DEV).to(dt)
+    x.backward(dx)
+    ref = wte.compute.float()[idx] + wpe.compute.float()[None]
+    assert rel_err(x, ref) < (1e-6 if fp32_residual else 1e-2)
+    gwte = torch.zeros(V, C, device=DEV).index_add_(0, idx.reshape(-1), dx.float().reshape(-1, C))
+    assert rel_err(wte.main_grad, gwte) < 1e-5
+    assert rel_err(wpe.main_grad, dx.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("fp32_residual", [True, False])
+def test_gpt_residual_dtype(kernels, fp32_residual):
+    """GPU GPT with either residual-stream dtype vs the fp32 CPU path."""
+    from nanosandbox_amd.models import GPT, GPTConfig
+    from nanosandbox_amd.optim import FlatParamStore
+
+    torch.manual_seed(0)
+    cfg = GPTConfig(block_size=128, vocab_size=1000, n_layer=2, n_head=4, n_embd=256, bias=False)
+    mc = GPT(cfg)
+    mg = GPT(cfg)
+    mg.load_state_dict(mc.state_dict())
+    mg.to(DEV).set_compute_dtype(BF, torch.float32 if fp32_residual else BF)
+    sc = FlatParamStore(mc, "cpu")
+    sg = FlatParamStore(mg, DEV, compute_dtype=BF)
+    d = torch.randint(0, 1000, (4, 129))
+    idx, tgt = d[:, :-1], d[:, 1:]
     _, lc = mc(idx, tgt)
     lc.backward()
     _, lg = mg(idx.to(DEV), tgt.to(DEV))
