@@ -8,6 +8,8 @@
 // (SURVEY.md §2.3 U-M3, K4).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -16,9 +18,21 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kUnroll = NSA_EW_UNROLL;
 
+// Grid cap: 2048 blocks = 8 per CU x 4 waves fill every wave slot (fastest alone).
+// NSA_EW_MAX_BLOCKS lowers it so a concurrent stream's GEMM workgroups can be
+// resident beside the elementwise kernel (ops/streams.py).
+inline int64_t ew_grid_cap() {
+  static int64_t cap = [] {
+    const char* e = getenv("NSA_EW_MAX_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 2048);
+  }();
+  return cap;
+}
+
 inline int grid_for(int64_t n_vec) {
   int64_t g = (n_vec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
-  if (g > 2048) g = 2048;
+  if (g > ew_grid_cap()) g = ew_grid_cap();
   if (g < 1) g = 1;
   return (int)g;
 }

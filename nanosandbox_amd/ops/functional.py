@@ -242,7 +242,7 @@ LN_EPS = 1e-5
 # (scripts/membound_ab.py)
 _LN_BWD_BLOCKS = 768
 # fp32 residual stream: ~174 VGPRs -> 2 resident 256-thread blocks per CU
-_LN_BWD_BLOCKS_X32 = 512
+_LN_BWD_BLOCKS_X32 = int(os.environ.get("NSA_LN_BWD_BLOCKS", "512"))
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -420,14 +420,15 @@ class LinearFn(torch.autograd.Function):
         x2, w, b = ctx.saved_tensors
         Nout = w.shape[0]
         d2 = dout.reshape(-1, Nout)
-        # weight gradient first: on the side stream it then waits only for dout, and
-        # the input-gradient GEMM below runs beside it (ops/streams.py)
-        gw = weight_grad(w, d2, x2)
+        # input gradient first, then the weight gradient: with the side stream on
+        # (ops/streams.py) the weight GEMM then starts after this input-gradient GEMM
+        # and runs beside the memory-bound kernels that follow it on the main stream
         dx = None
         if ctx.needs_input_grad[0]:
             wc = compute_weight(w, d2.dtype)
             dx = _tune.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
             dx = dx.view(*dout.shape[:-1], x2.shape[-1])
+        gw = weight_grad(w, d2, x2)
         gb = None
         if ctx.has_bias:
             gb = _accumulate(b, d2.sum(0, dtype=F32))
@@ -477,8 +478,16 @@ class MLPFn(torch.autograd.Function):
         x2, u, g, w_fc, w_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         wp = compute_weight(w_proj, dy.dtype)
-        # each weight gradient is issued before the input-gradient GEMM that runs
-        # beside it on the main stream (ops/streams.py)
+        if _streams.active(dy2) and not FUSE_GELU_EPILOGUE:
+            # side-stream order (ops/streams.py): each weight GEMM is forked right after
+            # an input-gradient GEMM, so it overlaps the memory-bound kernel that follows
+            # on the main stream (GELU backward here, the LayerNorm backward after dX)
+            out = {}
+            du = _tune.dgrad_dgelu(dy2, wp, u,
+                                   between=lambda: out.setdefault("gw", weight_grad(w_proj, dy2, g)))
+            dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
+            gw_fc = weight_grad(w_fc, du, x2)
+            return dx.view(ctx.xshape), gw_fc, out["gw"]
         gw_proj = weight_grad(w_proj, dy2, g)
         if FUSE_GELU_EPILOGUE:
             du = _gemm.dgrad(dy2, wp, u=u)
@@ -593,6 +602,7 @@ class AttentionFn(torch.autograd.Function):
             dqkv = torch.empty_like(qkv)
             # delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing (which also
             # zeroes dq_acc in the atomic mode; the split mode writes dQ once, in bf16)
+            _streams.before_compute(dy)
             dq_acc = None if FLASH_DQ_SPLIT else torch.empty(B, T, C, device=dy.device, dtype=F32)
             delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
             _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
@@ -667,9 +677,9 @@ class LMHeadLossFn(torch.autograd.Function):
             xs = torch.empty_like(x2)
             _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2.contiguous()), _lib.ptr(xs), _lib.ptr(g), xs.numel(),
                       _lib.stream())
-            gw = weight_grad(w, dlogits, xs)
             dx = _tune.dgrad(dlogits, wc)
             _lib.call("nsa_scale_rows_bf16", _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())
+            gw = weight_grad(w, dlogits, xs)  # after dX: see LinearFn.backward
             return dx.view(ctx.xshape), gw, None, None
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)

@@ -135,13 +135,27 @@ def _splits(name):
     return int(name.split("/s")[1]) if "/s" in name else None
 
 
+def _library_ok(M, N, K):
+    """Whether a library GEMM may run on the main stream.
+
+    With the weight-gradient side stream on (ops/streams.py), shapes for which
+    hipBLASLt's gfx950 pick is a persistent Stream-K kernel (``_SK3``: its
+    workgroups wait on each other's partial tiles) must not share the GPU with a
+    concurrent stream — measured on the 768 x 768 projection (attn.c_proj fwd and
+    input grad at n_embd = 768, M = 122880); those go to our kernel instead."""
+    from . import streams
+
+    return not (streams.ENABLED and streams.CONCURRENT_COMPUTE and N <= 1024 and K <= 1024
+                and M * N * K >= 2 ** 34)
+
+
 def fwd(x2, w):
     """y = x2 @ w^T (bf16)."""
     M, K = x2.shape
     N = w.shape[0]
     if not (_nsa_ok(x2, w) and _gemm.supported(M, N, K)):
         return x2 @ w.t()
-    cands = {"hipblaslt": lambda: x2 @ w.t()}
+    cands = {"hipblaslt": lambda: x2 @ w.t()} if _library_ok(M, N, K) else {}
     cands.update({f"nsa{v}": (lambda v=v: _gemm.fwd(x2, w, variant=v)) for v in NSA_VARIANTS})
     name = choose(("fwd", M, N, K), cands)
     return x2 @ w.t() if name == "hipblaslt" else _gemm.fwd(x2, w, variant=_variant(name))
@@ -182,11 +196,14 @@ def _wt(w):
 
 def dgrad(dy2, w):
     """dx = dy2 @ w (bf16)."""
+    from . import streams
+
+    streams.before_compute(dy2)  # the side stream's weight GEMMs never share the GPU with this one
     M, N = dy2.shape
     K = w.shape[1]
     if not (_nsa_ok(dy2, w) and _gemm.supported(M, K, N)):
         return dy2 @ w
-    cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()}
+    cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
     cands.update({f"nsa{v}": (lambda v=v: _gemm.dgrad(dy2, w, variant=v)) for v in NSA_VARIANTS})
     name = choose(("dgrad", M, N, K), cands)
     if name == "hipblaslt":
@@ -230,20 +247,35 @@ def fwd_gelu(x2, w):
     return split() if name == "split" else _gemm.fwd_gelu(x2, w, variant=_variant(name))
 
 
-def dgrad_dgelu(dy2, w, u):
-    """(dy2 @ w) * gelu'(u): fused GEMM epilogue or GEMM + GELU-backward kernel."""
+def dgrad_dgelu(dy2, w, u, between=None):
+    """(dy2 @ w) * gelu'(u): fused GEMM epilogue or GEMM + GELU-backward kernel.
+
+    ``between`` (optional callable) runs after the GEMM is issued and before the
+    GELU backward of the split form (after the fused kernel otherwise): the side
+    stream's weight-GEMM fork point (ops/streams.py)."""
     M, N = dy2.shape
     K = w.shape[1]
     if not (_nsa_ok(dy2, w, u) and _gemm.supported(M, K, N)):
-        return _gelu_bwd(dy2 @ w, u)
+        dg = dy2 @ w
+        if between is not None:
+            between()
+        return _gelu_bwd(dg, u)
 
-    def split():
-        return _gelu_bwd(dgrad(dy2, w), u)
+    def split(hook=None):
+        dg = dgrad(dy2, w)
+        if hook is not None:
+            hook()
+        return _gelu_bwd(dg, u)
 
     cands = {"split": split}
     cands.update({f"fused{v}": (lambda v=v: _gemm.dgrad(dy2, w, u=u, variant=v)) for v in NSA_VARIANTS})
     name = choose(("dgrad_dgelu", M, N, K), cands)
-    return split() if name == "split" else _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
+    if name == "split":
+        return split(between)
+    du = _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
+    if between is not None:
+        between()
+    return du
 
 
 def _hip_wgrad(dy2, x2, g32):

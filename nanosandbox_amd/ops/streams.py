@@ -35,15 +35,22 @@ Protocol (all calls are no-ops on CPU tensors and during HIP-graph capture):
   ``zero_grad``.  Bucket all-reduces are issued from the side stream itself
   (parallel/reducer.py), so they never stall the main stream.
 
+Scheduling: a weight GEMM is forked right after the input-gradient GEMM of the
+same layer, so it starts when that GEMM is done and runs beside the
+memory-bound kernel that follows on the main stream (GELU backward, LayerNorm
+backward); ``before_compute`` makes the main stream wait for the side stream
+before its next compute-bound launch (input-gradient GEMM, flash-attention
+backward).  Two compute kernels never share the GPU that way: measured on
+MI355X, a side weight GEMM left running beside the next input-gradient GEMM
+held the CUs it had (one 139 KB-LDS workgroup per CU, for the kernel's whole
+500 us) and stretched that GEMM from ~0.46 to ~8 ms, a zero-sum reshuffle;
+hipBLASLt's gfx950 picks for some shapes are also persistent Stream-K kernels
+(``_SK3``) whose workgroups wait on each other and stalled whole steps when a
+concurrent stream held CUs.  ``NSA_WGRAD_CONCURRENT=1`` drops the
+``before_compute`` waits (and keeps such library shapes off hipBLASLt) for A/B runs.
+
 Opt-in (``NSA_WGRAD_STREAM=1``); the default keeps every weight gradient on
-the main stream.  Measured on MI355X (GPT-2 124M, micro-batch 120): 497 vs
-501 ms/step (-0.8 %), but hipBLASLt's gfx950 solutions for these shapes are
-Stream-K kernels (``_SK3``: a persistent grid whose workgroups spin on each
-other's partial-tile flags), and side-stream workgroups occupying CUs they
-expect to be co-resident stretched individual steps to 3.6-4.2 s and once
-stalled a run for minutes.  Library Stream-K kernels and a concurrent compute
-stream do not mix safely, so the overlap stays off unless every main-stream
-GEMM is our own (non-persistent) kernel.
+the main stream.
 """
 
 from __future__ import annotations
@@ -54,6 +61,7 @@ import os
 import torch
 
 ENABLED = os.environ.get("NSA_WGRAD_STREAM", "0") == "1"
+CONCURRENT_COMPUTE = os.environ.get("NSA_WGRAD_CONCURRENT", "0") == "1"
 
 _side: dict = {}
 _pending: set = set()
@@ -107,6 +115,12 @@ def _on_side(s, tensors):
     with torch.cuda.stream(s):
         yield
     _held.append((s.record_event(), tensors))
+
+
+def before_compute(t: torch.Tensor) -> None:
+    """Main stream waits for the side stream before a compute-bound launch (see module doc)."""
+    if _pending and not CONCURRENT_COMPUTE and t.is_cuda:
+        join(t.device)
 
 
 def join(device=None) -> None:
