@@ -35,6 +35,8 @@
 // (b*H+h, q, k), so the backward regenerates the mask.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -752,7 +754,7 @@ template <int D, bool DROP>
 __global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
-    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, float delta_sign) {
   constexpr int BN = 64;
   constexpr int TILE_BYTES = BN * D * 2;
   constexpr int CPR = D / 8;
@@ -787,7 +789,7 @@ __global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
     gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
   }
   const float lse2 = lse[(int64_t)bh * T + qc] * kLog2e;
-  const float dlt = delta[(int64_t)bh * T + qc];
+  const float dlt = delta_sign * delta[(int64_t)bh * T + qc];  // v2 workspaces hold -delta
 
   f32x16 dq[NDT];
 #pragma unroll
@@ -864,6 +866,678 @@ __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict
   store8(dqkv + row * 3 * C + c, f);
 }
 
+// =============================================================================
+// Backward v2 (D = 64, the GPT-2 head size): dK/dV kernel, templated on
+//   NKB = 32-key blocks per wave (1 or 2) and NW = waves per workgroup (4 or 8).
+//
+// Wave w owns keys kw = k0 + 32*NKB*w as NKB 32-key blocks whose dK^T / dV^T
+// accumulators stay resident while the workgroup sweeps 32-query slices.  With
+// NKB = 2 each slice's Q / dO row fragments (ds_read_b128) and Q^T / dO^T transposed
+// fragments (ds_read_b64_tr_b16) feed both key blocks (24 LDS reads per 32 MFMAs).
+//
+// Query slices (Q and dO [32][64] tiles, XOR-swizzled as swz<64>, plus a per-wave
+// copy of the slice's row constants) arrive by LDS-DMA into a 2-slot ring, one
+// slice ahead: slice j+1 is issued right after the barrier that opens slice j, into
+// the slot slice j-1 used (every wave retired its reads of it -- lgkmcnt(0) -- before
+// that barrier).  Each wave waits only for its own pieces of slice j with vmcnt(0)
+// before the barrier (slice j+1 is not yet issued then); raw s_barrier (a
+// __syncthreads would add a fence).  The slice loop is unrolled by the ring parity,
+// so every LDS address is a per-lane base + an immediate offset.
+//
+// Row constants come in as the accumulators' initial values (cdna_hip_programming.md
+// App. B "row constants as the initial accumulator"): S' = Q·K^T - lse/scale and
+// dP' = dO·V^T - delta leave the MFMA chains ready, so P = exp2(c·S') and
+// dS = P·dP' cost one multiply each.  P and dS are packed to bf16 pairwise
+// (one v_cvt_pk_bf16_f32 per two elements).
+// =============================================================================
+constexpr int V2_QT = 32 * 64 * 2;  // one [32][64] bf16 tile
+
+template <int NW>
+struct V2Geo {
+  static constexpr int SLOT = 2 * V2_QT + NW * 256;  // Q, dO, NW x (32 -lse/scale + 32 -delta)
+  static constexpr int PIECES = NW == 4 ? 3 : 2;     // LDS-DMA instructions per wave per slice
+};
+
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// two f32 -> one dword of two bf16 (v_cvt_pk_bf16_f32, RNE)
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// 16 accumulator values -> the two bf16x8 operand fragments (k-steps 0 and 1)
+__device__ __forceinline__ void pack16(const float (&v)[16], bf16x8 (&f)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 u;
+    u.x = cvt2(v[8 * s + 0], v[8 * s + 1]);
+    u.y = cvt2(v[8 * s + 2], v[8 * s + 3]);
+    u.z = cvt2(v[8 * s + 4], v[8 * s + 5]);
+    u.w = cvt2(v[8 * s + 6], v[8 * s + 7]);
+    f[s] = __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+// f32x16 of a per-query row constant for this lane's accumulator rows acc_row(i, h)
+__device__ __forceinline__ f32x16 row_consts(const float* v, int h) {
+  f32x16 a;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 x = *reinterpret_cast<const float4*>(v + 8 * g + 4 * h);
+    a[4 * g + 0] = x.x;
+    a[4 * g + 1] = x.y;
+    a[4 * g + 2] = x.z;
+    a[4 * g + 3] = x.w;
+  }
+  return a;
+}
+
+// Ring-slot dispatch: calls f(std::integral_constant<int, k>) for k = j % NS, so the
+// slot's LDS offsets are compile-time (immediates) inside every branch-free body.
+template <int K, int NS, typename F>
+__device__ __forceinline__ void slot_dispatch(int k, F& f) {
+  if constexpr (K + 1 < NS) {
+    if (k == K)
+      f(std::integral_constant<int, K>{});
+    else
+      slot_dispatch<K + 1, NS>(k, f);
+  } else {
+    f(std::integral_constant<int, K>{});
+  }
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
+__device__ __forceinline__ void vm_wait(int n) {
+#define NSA_VMW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
+    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+#undef NSA_VMW
+}
+
+// one 32-query slice for one wave: S, dP for its NKB key blocks, P / dS, then dV^T, dK^T.
+// ld = this wave's copy of the slice's row constants: [0, 32) -lse/scale, [32, 64) -delta.
+template <int NKB, bool MASK, bool DROP>
+__device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, const float* ld,
+                                           const bf16x8 (&kf)[NKB][4], const bf16x8 (&vf)[NKB][4],
+                                           f32x16 (&dk)[NKB][2], f32x16 (&dv)[NKB][2], int q0, int kw, int h,
+                                           int r, int lane, float scale_log2, const DropArgs& dr) {
+  constexpr int D = 64;
+  bf16x8 qa[4], da[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qa[ks] = as_frag(lds_b128(qt, swz<D>(r, 2 * ks + h)));
+    da[ks] = as_frag(lds_b128(dot, swz<D>(r, 2 * ks + h)));
+  }
+  f32x16 sacc[NKB], pacc[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    sacc[kb] = row_consts(ld, h);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sacc[kb] = mfma(qa[ks], kf[kb][ks], sacc[kb]);
+  }
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    pacc[kb] = DROP ? f32x16{} : row_consts(ld + 32, h);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) pacc[kb] = mfma(da[ks], vf[kb][ks], pacc[kb]);
+  }
+  bf16x8 pfr[NKB][2], dsfr[NKB][2];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const int key = kw + 32 * kb + r;
+    f32x16 nd;
+    if constexpr (DROP) nd = row_consts(ld + 32, h);
+    float pv[16], dsv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(sacc[kb][i] * scale_log2);
+      if constexpr (MASK) p = key > q0 + acc_row(i, h) ? 0.0f : p;
+      if constexpr (DROP) {
+        const int q = q0 + acc_row(i, h);
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)q) * (uint64_t)dr.T + (uint64_t)key;
+        const bool keep = nsa_keep(dr.seed, id, dr.thresh);
+        pv[i] = keep ? p * dr.scale : 0.0f;
+        dsv[i] = p * ((keep ? pacc[kb][i] * dr.scale : 0.0f) + nd[i]);
+      } else {
+        pv[i] = p;
+        dsv[i] = p * pacc[kb][i];
+      }
+    }
+    pack16(pv, pfr[kb]);
+    pack16(dsv, dsfr[kb]);
+  }
+  // dV^T += dO^T · P,  dK^T += Q^T · dS   (each transposed fragment feeds every key block)
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int r0 = 16 * s + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const bf16x8 doa = tr_frag<D>(dot, r0, r0 + 8, 32 * dt, lane);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) dv[kb][dt] = mfma(doa, pfr[kb][s], dv[kb][dt]);
+      const bf16x8 qta = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) dk[kb][dt] = mfma(qta, dsfr[kb][s], dk[kb][dt]);
+    }
+  }
+}
+
+// The two halves of a slice, for the software-pipelined loop (PIPE): the S / dP MFMA
+// chains of slice j+1 (dkdv_sdp) go into the same basic block as the softmax and the
+// dV / dK MFMAs of slice j (dkdv_finish), so each wave has two independent chains to
+// interleave instead of one dependent one.
+template <int NKB, bool DROP>
+__device__ __forceinline__ void dkdv_sdp(const char* qt, const char* dot, const float* ld,
+                                         const bf16x8 (&kf)[NKB][4], const bf16x8 (&vf)[NKB][4],
+                                         f32x16 (&sacc)[NKB], f32x16 (&pacc)[NKB], int h, int r) {
+  constexpr int D = 64;
+  bf16x8 qa[4], da[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qa[ks] = as_frag(lds_b128(qt, swz<D>(r, 2 * ks + h)));
+    da[ks] = as_frag(lds_b128(dot, swz<D>(r, 2 * ks + h)));
+  }
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    sacc[kb] = row_consts(ld, h);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sacc[kb] = mfma(qa[ks], kf[kb][ks], sacc[kb]);
+  }
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    pacc[kb] = DROP ? f32x16{} : row_consts(ld + 32, h);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) pacc[kb] = mfma(da[ks], vf[kb][ks], pacc[kb]);
+  }
+}
+
+template <int NKB, bool MASK, bool DROP>
+__device__ __forceinline__ void dkdv_finish(const char* qt, const char* dot, const float* ld,
+                                            const f32x16 (&sacc)[NKB], const f32x16 (&pacc)[NKB],
+                                            f32x16 (&dk)[NKB][2], f32x16 (&dv)[NKB][2], int q0, int kw, int h,
+                                            int r, int lane, float scale_log2, const DropArgs& dr) {
+  constexpr int D = 64;
+  bf16x8 pfr[NKB][2], dsfr[NKB][2];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const int key = kw + 32 * kb + r;
+    f32x16 nd;
+    if constexpr (DROP) nd = row_consts(ld + 32, h);
+    float pv[16], dsv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(sacc[kb][i] * scale_log2);
+      if constexpr (MASK) p = key > q0 + acc_row(i, h) ? 0.0f : p;
+      if constexpr (DROP) {
+        const int q = q0 + acc_row(i, h);
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)q) * (uint64_t)dr.T + (uint64_t)key;
+        const bool keep = nsa_keep(dr.seed, id, dr.thresh);
+        pv[i] = keep ? p * dr.scale : 0.0f;
+        dsv[i] = p * ((keep ? pacc[kb][i] * dr.scale : 0.0f) + nd[i]);
+      } else {
+        pv[i] = p;
+        dsv[i] = p * pacc[kb][i];
+      }
+    }
+    pack16(pv, pfr[kb]);
+    pack16(dsv, dsfr[kb]);
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int r0 = 16 * s + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const bf16x8 doa = tr_frag<D>(dot, r0, r0 + 8, 32 * dt, lane);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) dv[kb][dt] = mfma(doa, pfr[kb][s], dv[kb][dt]);
+      const bf16x8 qta = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) dk[kb][dt] = mfma(qta, dsfr[kb][s], dk[kb][dt]);
+    }
+  }
+}
+
+#ifndef NSA_DKDV_NS
+#define NSA_DKDV_NS 4  // LDS ring slots of the v2 dK/dV kernel (NS - 1 slices in flight)
+#endif
+
+template <int NKB, int NW, bool DROP, bool PIPE = false>
+__global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void flash_bwd_dkdv2_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
+    const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+  constexpr int D = 64;
+  constexpr int KPW = 32 * NKB;       // keys per wave
+  constexpr int KWG = KPW * NW;       // keys per workgroup
+  constexpr int SLOT = V2Geo<NW>::SLOT;
+  // PIPE keeps slice j's tiles in use after slice j+1's barrier: one slot less in flight
+  constexpr int NS = NSA_DKDV_NS, LA = PIPE ? NS - 2 : NS - 1;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int kbw = blockIdx.x / BH;  // key blocks near 0 see the most queries: launched first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int k0 = kbw * KWG;
+  const int kw = k0 + KPW * w;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+  const bf16_t* vbase = base + 2 * C + hh * D;
+  const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
+  const float* nls_bh = nls + (int64_t)bh * T;
+  const float* nd_bh = nd + (int64_t)bh * T;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  const int s_first = k0 / 32;
+  const int n_mine = T / 32 - s_first;  // query slices this workgroup visits
+
+  // slice s -> ring slot: the [32][64] Q and dO tiles are 4 + 4 pieces of 8 rows x 128 B
+  // (with 4 waves each wave copies one of each, with 8 waves one of the two); the
+  // swz<64> image is lane-linear, so the XOR goes on the per-lane source chunk.  Each
+  // wave also copies the slice's row constants for itself: lanes 0-31 -lse/scale,
+  // 32-63 -delta.
+  const int piece = NW == 4 ? w : (w & 3);
+  const int prow = 8 * piece + (lane >> 3);
+  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const bf16_t* qsrc = qbase + (int64_t)prow * row_stride + pch * 8;  // + slice * 32 rows
+  const bf16_t* dosrc = dobase + (int64_t)prow * C + pch * 8;
+  const float* csrc = (h == 0 ? nls_bh : nd_bh) + r;
+  auto issue = [&](int s, int slot) {
+    const uint32_t sb = lds0 + (uint32_t)(slot * SLOT);
+    if (NW == 4 || w < 4) glds16(qsrc + (int64_t)s * 32 * row_stride, sb + (uint32_t)(8 * piece * 128));
+    if (NW == 4 || w >= 4) glds16(dosrc + (int64_t)s * 32 * C, sb + (uint32_t)(V2_QT + 8 * piece * 128));
+    glds4(csrc + s * 32, sb + (uint32_t)(2 * V2_QT + w * 256));
+  };
+
+  for (int j = 0; j < LA && j < n_mine; ++j) issue(s_first + j, j);
+
+  // K^T / V^T fragments (B operands of S = Q·K^T, dP = dO·V^T): K[key][16ks + 8h ..]
+  bf16x8 kf[NKB][4], vf[NKB][4];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    int kc = kw + 32 * kb + r;
+    kc = kc < T ? kc : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[kb][ks] = as_frag(*reinterpret_cast<const uint4*>(kbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+      vf[kb][ks] = as_frag(*reinterpret_cast<const uint4*>(vbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+    }
+  }
+  // Retire the fragment loads HERE, in hipcc's own bookkeeping: an asm use of every
+  // fragment makes it wait for them now.  Otherwise its wait for a fragment's first
+  // use lands inside the slice loop and (blind to the asm LDS-DMA) drains the ring's
+  // in-flight slice with vmcnt(0) every iteration.
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+    asm volatile("" ::"v"(kf[kb][0]), "v"(kf[kb][1]), "v"(kf[kb][2]), "v"(kf[kb][3]), "v"(vf[kb][0]),
+                 "v"(vf[kb][1]), "v"(vf[kb][2]), "v"(vf[kb][3]));
+  f32x16 dk[NKB][2], dv[NKB][2];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      dk[kb][dt] = f32x16{};
+      dv[kb][dt] = f32x16{};
+    }
+
+  // Open slice j (ring slot j % NS): this wave's pieces of it have landed (slices
+  // j+1 .. j+LA-1 may stay in flight) and its LDS reads of slice j-1 are retired; the
+  // barrier makes every wave's pieces visible and frees slice j-1's slot for slice j+LA.
+  auto open_slice = [&](int j) {
+    vm_wait(V2Geo<NW>::PIECES * min(LA - 1, n_mine - 1 - j));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + LA < n_mine) issue(s_first + j + LA, (j + LA) % NS);
+  };
+  auto slice_full = [&](int j) {
+    auto f = [&](auto slot) {
+      const char* qt = smem + decltype(slot)::value * SLOT;
+      dkdv_slice<NKB, false, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, kf,
+                                   vf, dk, dv, (s_first + j) * 32, kw, h, r, lane, scale_log2, dr);
+    };
+    slot_dispatch<0, NS>(j % NS, f);
+  };
+  auto slice_diag = [&](int j) {
+    auto f = [&](auto slot) {
+      const char* qt = smem + decltype(slot)::value * SLOT;
+      dkdv_slice<NKB, true, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, kf,
+                                  vf, dk, dv, (s_first + j) * 32, kw, h, r, lane, scale_log2, dr);
+    };
+    slot_dispatch<0, NS>(j % NS, f);
+  };
+
+  // Three loops with branch-free bodies: slices wholly before this wave's keys (no
+  // work), the slices on its diagonal (masked), the rest.  Every wave runs n_mine
+  // iterations in all: same barrier count.
+  const int j_diag = min(NKB * w, n_mine);
+  const int j_full = min(NKB * w + NKB, n_mine);
+  int j = 0;
+  for (; j < j_diag; ++j) open_slice(j);
+  if constexpr (!PIPE) {
+    for (; j < j_full; ++j) {
+      open_slice(j);
+      slice_diag(j);
+    }
+    for (; j < n_mine; ++j) {
+      open_slice(j);
+      slice_full(j);
+    }
+  } else if (j < n_mine) {
+    // software pipeline: iteration j opens slice j+1 and issues its S / dP chains
+    // beside slice j's softmax and dV / dK MFMAs
+    f32x16 sacc[NKB], pacc[NKB];
+    open_slice(j);
+    {
+      auto f = [&](auto slot) {
+        const char* qt = smem + decltype(slot)::value * SLOT;
+        dkdv_sdp<NKB, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, kf, vf, sacc,
+                            pacc, h, r);
+      };
+      slot_dispatch<0, NS>(j % NS, f);
+    }
+    auto step = [&](int jj, auto mask) {
+      constexpr bool M = decltype(mask)::value;
+      const bool more = jj + 1 < n_mine;
+      if (more) open_slice(jj + 1);
+      auto f = [&](auto slot) {
+        constexpr int K = decltype(slot)::value;
+        constexpr int KN = (K + 1) % NS;
+        const char* qt = smem + K * SLOT;
+        const char* qn = smem + KN * SLOT;
+        f32x16 sn[NKB], pn[NKB];
+        if (more)
+          dkdv_sdp<NKB, DROP>(qn, qn + V2_QT, reinterpret_cast<const float*>(qn + 2 * V2_QT) + w * 64, kf, vf, sn,
+                              pn, h, r);
+        dkdv_finish<NKB, M, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, sacc,
+                                  pacc, dk, dv, (s_first + jj) * 32, kw, h, r, lane, scale_log2, dr);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          sacc[kb] = sn[kb];
+          pacc[kb] = pn[kb];
+        }
+      };
+      slot_dispatch<0, NS>(jj % NS, f);
+    };
+    for (; j < j_full; ++j) step(j, std::integral_constant<bool, true>{});
+    for (; j < n_mine; ++j) step(j, std::integral_constant<bool, false>{});
+  }
+
+  // epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T -> dqkv[:, :, C + ...] and [2C + ...]
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const int kpos = kw + 32 * kb + r;
+    if (kpos < T) {
+      bf16_t* krow = dqkv + ((int64_t)b * T + kpos) * row_stride + C + hh * D;
+      bf16_t* vrow = krow + C;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          uint2 uk, uv;
+          uk.x = cvt2(dk[kb][dt][4 * g + 0] * scale, dk[kb][dt][4 * g + 1] * scale);
+          uk.y = cvt2(dk[kb][dt][4 * g + 2] * scale, dk[kb][dt][4 * g + 3] * scale);
+          uv.x = cvt2(dv[kb][dt][4 * g + 0], dv[kb][dt][4 * g + 1]);
+          uv.y = cvt2(dv[kb][dt][4 * g + 2], dv[kb][dt][4 * g + 3]);
+          *reinterpret_cast<uint2*>(krow + d) = uk;
+          *reinterpret_cast<uint2*>(vrow + d) = uv;
+        }
+      }
+    }
+  }
+}
+
+// =============================================================================
+// dQ kernel v2 (D = 64): one workgroup = 4 waves x 32 queries of one (b, h), the
+// query on the lane (swapped products, as the forward):
+//   S^T  = K · Q^T,  dP^T = V · dO^T     A = K / V rows (ds_read_b128), B = Q^T / dO^T
+//                                        fragments held in registers for the whole loop
+//   dS^T = P^T · dP'^T,  P^T = exp2(c·S^T - lse·log2e),  dP'^T = dP^T - delta
+//   dQ^T += K^T · dS^T                   A = K^T (ds_read_b64_tr_b16), B = dS^T packed
+//                                        straight from the accumulator registers
+// lse·log2e and delta are per-lane scalars here; -delta enters as a constant
+// initial-accumulator tile (C operand), so dS costs one multiply per element and P
+// is never converted to bf16 (only dS feeds an MFMA).  64-key K / V tiles arrive by
+// LDS-DMA into a 2-slot ring one tile ahead (4 pieces per wave per tile); the tile
+// loop is unrolled by ring parity (immediate LDS offsets) and split into branch-free
+// loops: fully visible tiles, the wave's one diagonal tile, trailing tiles past it.
+// dQ is written once, in bf16: no atomics, no fp32 accumulator.
+// =============================================================================
+constexpr int DQ2_T = 64 * 64 * 2;  // one [64][64] bf16 tile
+
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void dq2_tile(const char* kt, const char* vt, const bf16x8 (&qf)[4],
+                                         const bf16x8 (&gf)[4], const f32x16& ndt, f32x16 (&dq)[2], float lse2,
+                                         int kv0, int qpos, int h, int r, int lane, float scale_log2,
+                                         const DropArgs& dr) {
+  constexpr int D = 64;
+  f32x16 st[2], pt[2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
+  }
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    pt[sb] = DROP ? f32x16{} : ndt;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) pt[sb] = mfma(as_frag(lds_b128(vt, swz<D>(32 * sb + r, 2 * ks + h))), gf[ks], pt[sb]);
+  }
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    float dsv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kpos = kv0 + 32 * sb + acc_row(i, h);
+      float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
+      if constexpr (MASK) p = kpos > qpos ? 0.0f : p;
+      if constexpr (DROP) {
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
+        dsv[i] = p * ((nsa_keep(dr.seed, id, dr.thresh) ? pt[sb][i] * dr.scale : 0.0f) + ndt[i]);
+      } else {
+        dsv[i] = p * pt[sb][i];
+      }
+    }
+    bf16x8 dsf[2];
+    pack16(dsv, dsf);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane), dsf[s], dq[dt]);
+    }
+  }
+}
+
+#ifndef NSA_DQ2_NS
+#define NSA_DQ2_NS 4  // LDS ring slots of the v2 dQ kernel (NS - 1 tiles in flight)
+#endif
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
+    const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale, float scale_log2,
+    uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+  constexpr int D = 64;
+  constexpr int SLOT = 2 * DQ2_T;  // K, V
+  constexpr int NS = NSA_DQ2_NS, LA = NS - 1;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 127) / 128;
+  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int q0w = qt * 128 + 32 * w;
+  const int qpos = q0w + r;
+  const int qc = qpos < T ? qpos : T - 1;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // K / V tile j -> ring slot: 8 + 8 pieces of 8 rows x 128 B, wave w copies K rows and
+  // V rows 16w .. 16w+15 (two pieces each), XOR swizzle on the per-lane source chunk
+  const int prow = 16 * w + (lane >> 3);
+  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);        // piece 0: row prow
+  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);  // piece 1: row prow + 8
+  const bf16_t* krow = base + C + hh * D + (int64_t)prow * row_stride;
+  const int kv_end = min(T, qt * 128 + 128);
+  const int n_tiles = (kv_end + 63) / 64;
+  auto issue = [&](int j, int slot) {
+    const uint32_t sb = lds0 + (uint32_t)(slot * SLOT) + (uint32_t)(16 * w * 128);
+    const int64_t o = (int64_t)j * 64 * row_stride;
+    int64_t o0 = 0, o8 = 8 * row_stride;
+    if (j * 64 + 64 > T) {  // last, partial tile: rows past T re-read row T-1 (their keys are masked)
+      const int k = j * 64 + prow;
+      o0 = (int64_t)(min(k, T - 1) - k) * row_stride;
+      o8 = (int64_t)(min(k + 8, T - 1) - k) * row_stride;
+    }
+    const bf16_t* k0 = krow + o + o0 + pch0 * 8;
+    const bf16_t* k8 = krow + o + o8 + pch1 * 8;
+    glds16(k0, sb);
+    glds16(k8, sb + 1024);
+    glds16(k0 + C, sb + DQ2_T);
+    glds16(k8 + C, sb + DQ2_T + 1024);
+  };
+  for (int j = 0; j < LA && j < n_tiles; ++j) issue(j, j);
+
+  // Q^T and dO^T fragments (B operands): lane holds row qpos, d = 16ks + 8h .. +8
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
+    gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
+  }
+  // lse·log2e = -nls·c (nls = -lse/scale), and the -delta tile
+  const float lse2 = -nls[(int64_t)bh * T + qc] * scale_log2;
+  const float ndl = nd[(int64_t)bh * T + qc];
+  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(gf[0]), "v"(gf[1]), "v"(gf[2]),
+               "v"(gf[3]), "v"(lse2), "v"(ndl));  // retire these loads before the ring loop (see dK/dV)
+  f32x16 ndt;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ndt[i] = ndl;
+  f32x16 dq[2];
+  dq[0] = f32x16{};
+  dq[1] = f32x16{};
+
+  auto open_tile = [&](int j) {
+    vm_wait(4 * min(LA - 1, n_tiles - 1 - j));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + LA < n_tiles) issue(j + LA, (j + LA) % NS);
+  };
+  auto tile_full = [&](int j) {
+    auto f = [&](auto slot) {
+      const char* kt = smem + decltype(slot)::value * SLOT;
+      dq2_tile<false, DROP>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
+    };
+    slot_dispatch<0, NS>(j % NS, f);
+  };
+  auto tile_diag = [&](int j) {
+    auto f = [&](auto slot) {
+      const char* kt = smem + decltype(slot)::value * SLOT;
+      dq2_tile<true, DROP>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
+    };
+    slot_dispatch<0, NS>(j % NS, f);
+  };
+
+  // tiles [0, m) are visible to every query of the wave; tile m holds its diagonal;
+  // later tiles (at most one) are all masked
+  const int m = min(q0w / 64, n_tiles);
+  int j = 0;
+  for (; j < m; ++j) {
+    open_tile(j);
+    tile_full(j);
+  }
+  if (j < n_tiles) {
+    open_tile(j);
+    tile_diag(j);
+    ++j;
+  }
+  for (; j < n_tiles; ++j) open_tile(j);
+
+  // epilogue: dQ = scale · (dQ^T)^T -> dqkv[b, qpos, hh*D + d]; lane owns query qpos
+  if (qpos < T) {
+    bf16_t* qrow = dqkv + ((int64_t)b * T + qpos) * row_stride + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = cvt2(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
+        u.y = cvt2(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(qrow + d) = u;
+      }
+    }
+  }
+}
+
+// v2 backward's row constants, both [B, H, T]: nd = -rowsum(dO * O) (= -delta) and
+// nls = -lse / scale (the initial accumulators of dP' and S')
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_pre2_kernel(const bf16_t* __restrict__ o,
+                                                            const bf16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse, float* __restrict__ nd,
+                                                            float* __restrict__ nls, float inv_scale, int B, int T,
+                                                            int H) {
+  constexpr int LPR = D / 8;
+  const int C = H * D;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / LPR;  // (b*T + t)*H + h
+  const int sub = gid % LPR;
+  if (row >= (int64_t)B * T * H) return;
+  const int hh = row % H;
+  const int64_t bt = row / H;
+  const int t = bt % T, b = bt / T;
+  const int64_t off = bt * C + hh * D + sub * 8;
+  float a[8], g[8];
+  load8(o + off, a);
+  load8(dout + off, g);
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += a[j] * g[j];
+#pragma unroll
+  for (int k = LPR / 2; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
+  const int64_t idx = ((int64_t)b * H + hh) * T + t;
+  if (sub == 0) nd[idx] = -s;
+  if (sub == 1) nls[idx] = -lse[idx] * inv_scale;
+}
+
 template <int D>
 hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H, float scale, float p,
                       uint64_t seed, hipStream_t s) {
@@ -912,11 +1586,11 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
     if (th)
       flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
-          scale, scale * kLog2e, th, dscale, seed);
+          scale, scale * kLog2e, th, dscale, seed, 1.0f);
     else
       flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>(
           (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
-          scale, scale * kLog2e, th, dscale, seed);
+          scale, scale * kLog2e, th, dscale, seed, 1.0f);
     return hipGetLastError();
   }
   const int C = H * D;
@@ -926,7 +1600,92 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
   return hipGetLastError();
 }
 
+// v2 backward (D = 64, T % 32 == 0): pre2 (-delta, -lse/scale) -> dK/dV kernel (64 keys
+// per wave) -> the split-mode dQ kernel.  ws = 2 x [B, H, T] fp32.
+hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws, void* dqkv,
+                         int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
+  constexpr int D = 64;
+  float* nd = (float*)ws;
+  float* nls = nd + (int64_t)B * H * T;
+  const int64_t threads = (int64_t)B * T * H * (D / 8);
+  flash_bwd_pre2_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+      (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, nd, nls, 1.0f / scale, B, T, H);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  // geometry (NSA_FLASH_DKDV): k1w4 = 1 key block per wave, 4 waves (default: 216 VGPRs,
+  // two independent workgroups per CU), k1w8, k2w4 (2 key blocks per wave, 1 wave/SIMD).
+  // A/B at B120 T1024 H12 (whole backward incl. the dQ kernel): v1 1307, k2w4 1304,
+  // k1w8 1203, k1w4 1189 us.
+  const char* g = getenv("NSA_FLASH_DKDV");
+  const int geo = (g && g[0] == 'k' && g[1] == '2') ? 0 : (g && g[0] == 'k' && g[3] == '8') ? 1
+                  : (g && g[0] == 'k' && g[4] == 'p') ? 3 : 2;
+#define NSA_DKDV2(NKB, NW, PIPE)                                                                              \
+  do {                                                                                                        \
+    const int n_kb = (T + 32 * NKB * NW - 1) / (32 * NKB * NW);                                              \
+    if (th)                                                                                                   \
+      flash_bwd_dkdv2_kernel<NKB, NW, true, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                           \
+          (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
+          dscale, seed);                                                                                      \
+    else                                                                                                      \
+      flash_bwd_dkdv2_kernel<NKB, NW, false, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                          \
+          (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
+          dscale, seed);                                                                                      \
+  } while (0)
+  if (geo == 1) NSA_DKDV2(1, 8, false);
+  else if (geo == 2) NSA_DKDV2(1, 4, false);
+  else if (geo == 3) NSA_DKDV2(1, 4, true);
+  else NSA_DKDV2(2, 4, false);
+#undef NSA_DKDV2
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int n_qt = (T + 127) / 128;
+  const char* dq2 = getenv("NSA_FLASH_DQ2");
+  if (!(dq2 && dq2[0] == '0')) {
+    if (th)
+      flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
+                                                              (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
+                                                              dscale, seed);
+    else
+      flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
+                                                               (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
+                                                               dscale, seed);
+    return hipGetLastError();
+  }
+  if (th)
+    flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                              (const float*)lse, nd, (bf16_t*)dqkv, B, T, H, scale,
+                                                              scale * kLog2e, th, dscale, seed, -1.0f);
+  else
+    flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                               (const float*)lse, nd, (bf16_t*)dqkv, B, T, H, scale,
+                                                               scale * kLog2e, th, dscale, seed, -1.0f);
+  return hipGetLastError();
+}
+
+bool bwd2_enabled() {
+  const char* e = getenv("NSA_FLASH_BWD");
+  return !(e && e[0] == 'v' && e[1] == '1');
+}
+
 }  // namespace
+
+// Backward with a 2 x [B, H, T] fp32 workspace.  D = 64 with T % 32 == 0 runs the v2
+// dK/dV kernel (NSA_FLASH_BWD=v1 selects the 32-keys-per-wave kernel instead, for
+// A/B); every other shape runs the split-mode v1 backward with ws[0] as delta.
+NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
+                                  void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
+                                  hipStream_t s) {
+  if (D == 64 && T % 32 == 0 && bwd2_enabled())
+    return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
+  switch (D) {
+    case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
+    case 64: return bwd_launch<64>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
+    case 128: return bwd_launch<128>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {

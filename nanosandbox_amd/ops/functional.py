@@ -603,7 +603,14 @@ class AttentionFn(torch.autograd.Function):
             # delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing (which also
             # zeroes dq_acc in the atomic mode; the split mode writes dQ once, in bf16)
             _streams.before_compute(dy)
-            dq_acc = None if FLASH_DQ_SPLIT else torch.empty(B, T, C, device=dy.device, dtype=F32)
+            if FLASH_DQ_SPLIT:
+                # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
+                # D = 64 runs the 64-keys-per-wave dK/dV kernel (NSA_FLASH_BWD=v1: the older one)
+                ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
+                _lib.call("nsa_flash_bwd2", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(ws),
+                          _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
+                return dqkv, None, None
+            dq_acc = torch.empty(B, T, C, device=dy.device, dtype=F32)
             delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
             _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
                       _lib.ptr(dq_acc), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())

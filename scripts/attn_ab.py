@@ -2,11 +2,11 @@
 interleaved rounds, random data; cdna_hip_programming.md §5.4 rules 24-25).
 
 Variants are selected per launch through environment switches read by the kernel
-library (e.g. NSA_FLASH_DKDV=ref for the reference dK/dV body).  Also checks that
+library (e.g. NSA_FLASH_BWD=v1 for the 32-keys-per-wave dK/dV kernel).  Also checks that
 every variant's outputs match the first variant's.
 
     python scripts/attn_ab.py [--B 120] [--T 1024] [--H 12] [--D 64] [--rounds 7]
-        [--bwd "default:;ref:NSA_FLASH_DKDV=ref"] [--fwd "default:"]
+        [--bwd "v2:NSA_FLASH_BWD=v2;v1:NSA_FLASH_BWD=v1"] [--fwd "default:"]
 """
 
 import argparse
@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--p", type=float, default=0.0)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--bwd", default="default:;ref:NSA_FLASH_DKDV=ref")
+    ap.add_argument("--bwd", default="v2:NSA_FLASH_BWD=v2;v1:NSA_FLASH_BWD=v1")
     ap.add_argument("--fwd", default="default:")
     a = ap.parse_args()
     B, T, H, D = a.B, a.T, a.H, a.D
@@ -68,7 +68,7 @@ def main():
     y = torch.empty(B, T, C, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(B, H, T, device="cuda", dtype=F32)
     dy = torch.randn(B, T, C, device="cuda").to(torch.bfloat16)
-    delta = torch.empty(B, H, T, device="cuda", dtype=F32)
+    ws = torch.empty(2, B, H, T, device="cuda", dtype=F32)
     seed = 1234
     s = _lib.stream()
 
@@ -78,8 +78,8 @@ def main():
     outs = {}
 
     def bwd_into(dq):
-        _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
-                  None, _lib.ptr(dq), B, T, H, D, scale, a.p, seed, s)
+        _lib.call("nsa_flash_bwd2", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(ws),
+                  _lib.ptr(dq), B, T, H, D, scale, a.p, seed, s)
 
     fwd_v = parse(a.fwd)
     bwd_v = parse(a.bwd)

@@ -297,6 +297,33 @@ def test_flash_attention_deferred_rescale(kernels, pattern):
         assert e < 4e-2, f"{pattern}: d{name} rel err {e}"
 
 
+@pytest.mark.parametrize("T", [320, 1024, 96])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("geo", ["k1w4", "k1w8", "k2w4"])
+def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo):
+    """The v2 backward (D = 64: LDS-DMA-fed dK/dV kernel in each geometry + the v2 dQ
+    kernel) against the v1 kernels, with and without dropout; T = 320 and 96 leave the
+    last key / query workgroups partial."""
+    from nanosandbox_amd.ops import functional as fn
+
+    torch.manual_seed(0)
+    B, H, D = 2, 3, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
+    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
+    grads = {}
+    monkeypatch.setenv("NSA_FLASH_DKDV", geo)
+    for ver in ("v1", "v2"):
+        monkeypatch.setenv("NSA_FLASH_BWD", ver)
+        torch.manual_seed(5)
+        x = qkv.clone().requires_grad_(True)
+        fn.attention(x, H, p, True).backward(dy)
+        torch.cuda.synchronize()
+        grads[ver] = x.grad.float().view(B, T, 3, H * D)
+    for i, name in enumerate("qkv"):
+        e = rel_err(grads["v2"][:, :, i], grads["v1"][:, :, i])
+        assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
+
+
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_flash_bwd_split_matches_atomic(kernels, monkeypatch, p):
     """The two dQ strategies of the backward (split: separate dQ kernel, bf16 written
