@@ -1507,6 +1507,191 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
   }
 }
 
+// =============================================================================
+// Forward v2 (D = 64, opt-in: NSA_FLASH_FWD=v2s3): the v1 forward's math (swapped
+// S^T = K·Q^T with the query on the lane, deferred max-rescale, O^T += V^T·P^T from
+// the accumulator registers) on the v2 backward's plumbing: 64-key K / V tiles by
+// LDS-DMA into an NS-slot ring (NS - 1 tiles in flight; v1 stages one tile through
+// registers and parks ~54 % of wave cycles on its waits, PMC), slot-dispatched
+// branch-free bodies, the loop split into fully visible tiles / the wave's diagonal
+// tile / trailing masked tiles, and pairwise bf16 packing of P.  Measured slower than
+// v1 (see fwd_launch): the deeper ring costs the occupancy that hid those waits.
+// =============================================================================
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2],
+                                          float& m_i, float& l_i, int kv0, int qpos, int h, int r, int lane,
+                                          float scale_log2, const DropArgs& dr) {
+  constexpr int D = 64;
+  f32x16 st[2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
+  }
+  float mt = st[0][0];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int i = (sb == 0 ? 1 : 0); i < 16; ++i) mt = fmaxf(mt, st[sb][i]);
+  mt = half_swap_max(mt);
+  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
+  if (__builtin_amdgcn_ballot_w64(grow)) {  // wave-uniform: rescale only when some lane's max moved
+    const float m_new = grow ? mt : m_i;
+    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
+    l_i *= alpha;
+    m_i = m_new;
+    o[0] *= alpha;
+    o[1] *= alpha;
+  }
+  const float mc = m_i * scale_log2;
+  float rs = 0.0f;
+  bf16x8 pf[2][2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    float pv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(st[sb][i] * scale_log2 - mc);
+      rs += p;
+      if constexpr (DROP) {
+        const int kpos = kv0 + 32 * sb + acc_row(i, h);
+        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
+        p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
+      }
+      pv[i] = p;
+    }
+    pack16(pv, pf[sb]);
+  }
+  l_i += half_swap_sum(rs);
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r0 = 32 * sb + 16 * s2 + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s2], o[dt]);
+    }
+}
+
+template <int NS, bool DROP>
+__global__ __launch_bounds__(256, 2) void flash_fwd2_kernel(const bf16_t* __restrict__ qkv,
+                                                                         bf16_t* __restrict__ out,
+                                                                         float* __restrict__ lse_out, int B, int T,
+                                                                         int H, float scale_log2,
+                                                                         uint32_t drop_thresh, float drop_scale,
+                                                                         uint64_t seed) {
+  constexpr int D = 64;
+  constexpr int SLOT = 2 * DQ2_T;  // K, V [64][64]
+  constexpr int LA = NS - 1;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 127) / 128;
+  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const int q0w = qt * 128 + 32 * w;
+  const int qpos = q0w + r;
+  const int qc = qpos < T ? qpos : T - 1;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // K / V tile j -> ring slot (the dQ v2 kernel's piece layout)
+  const int prow = 16 * w + (lane >> 3);
+  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
+  const bf16_t* krow = base + C + hh * D + (int64_t)prow * row_stride;
+  const int kv_end = min(T, qt * 128 + 128);
+  const int n_tiles = (kv_end + 63) / 64;
+  auto issue = [&](int j, int slot) {
+    const uint32_t sb = lds0 + (uint32_t)(slot * SLOT) + (uint32_t)(16 * w * 128);
+    const int64_t o = (int64_t)j * 64 * row_stride;
+    int64_t o0 = 0, o8 = 8 * row_stride;
+    if (j * 64 + 64 > T) {
+      const int k = j * 64 + prow;
+      o0 = (int64_t)(min(k, T - 1) - k) * row_stride;
+      o8 = (int64_t)(min(k + 8, T - 1) - k) * row_stride;
+    }
+    const bf16_t* k0 = krow + o + o0 + pch0 * 8;
+    const bf16_t* k8 = krow + o + o8 + pch1 * 8;
+    glds16(k0, sb);
+    glds16(k8, sb + 1024);
+    glds16(k0 + C, sb + DQ2_T);
+    glds16(k8 + C, sb + DQ2_T + 1024);
+  };
+  for (int j = 0; j < LA && j < n_tiles; ++j) issue(j, j);
+
+  // Q^T fragments (B operand): lane holds Q[qpos][16ks + 8h .. +8]
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
+  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // retire before the ring loop
+  f32x16 o[2];
+  o[0] = f32x16{};
+  o[1] = f32x16{};
+  float m_i = -1e30f, l_i = 0.0f;
+
+  auto open_tile = [&](int j) {
+    vm_wait(4 * min(LA - 1, n_tiles - 1 - j));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + LA < n_tiles) issue(j + LA, (j + LA) % NS);
+  };
+  auto tile = [&](int j, auto mask) {
+    constexpr bool M = decltype(mask)::value;
+    auto f = [&](auto slot) {
+      const char* kt = smem + decltype(slot)::value * SLOT;
+      fwd2_tile<M, DROP>(kt, kt + DQ2_T, qf, o, m_i, l_i, 64 * j, qpos, h, r, lane, scale_log2, dr);
+    };
+    slot_dispatch<0, NS>(j % NS, f);
+  };
+  const int m = min(q0w / 64, n_tiles);
+  int j = 0;
+  for (; j < m; ++j) {
+    open_tile(j);
+    tile(j, std::integral_constant<bool, false>{});
+  }
+  if (j < n_tiles) {
+    open_tile(j);
+    tile(j, std::integral_constant<bool, true>{});
+    ++j;
+  }
+  for (; j < n_tiles; ++j) open_tile(j);
+
+  // epilogue: O = O^T / l ; lane owns query qpos, registers hold d
+  if (qpos < T) {
+    const float inv_l = 1.0f / l_i;
+    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = cvt2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
+        u.y = cvt2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
+        *reinterpret_cast<uint2*>(orow + d) = u;
+      }
+    }
+    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
+  }
+}
+
 // v2 backward's row constants, both [B, H, T]: nd = -rowsum(dO * O) (= -delta) and
 // nls = -lse / scale (the initial accumulators of dP' and S')
 template <int D>
@@ -1544,6 +1729,28 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
   const int n_qt = (T + 127) / 128;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  if constexpr (D == 64) {
+    // NSA_FLASH_FWD = v1 (default: the register-staged kernel below) | v2s2 / v2s3 / v2s4
+    // (LDS-DMA ring slots).  A/B at B120 T1024 H12: v1 382, v2s2 420, v2s3 395, v2s4
+    // 424 us: v1's 127 VGPRs keep 4 waves per SIMD, v2's 168 three at most, and the
+    // deeper ring does not buy that back (identical outputs).
+    const char* e = getenv("NSA_FLASH_FWD");
+    const int ns = (!e || e[1] == '1') ? 0 : (e[3] - '0');
+#define NSA_FWD2(NS)                                                                                            \
+  do {                                                                                                          \
+    if (th)                                                                                                     \
+      flash_fwd2_kernel<NS, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, \
+                                                               T, H, scale * kLog2e, th, dscale, seed);          \
+    else                                                                                                        \
+      flash_fwd2_kernel<NS, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,   \
+                                                                B, T, H, scale * kLog2e, th, dscale, seed);     \
+    return hipGetLastError();                                                                                   \
+  } while (0)
+    if (ns == 2) NSA_FWD2(2);
+    if (ns == 3) NSA_FWD2(3);
+    if (ns == 4) NSA_FWD2(4);
+#undef NSA_FWD2
+  }
   if (th)
     flash_fwd_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                            scale * kLog2e, th, dscale, seed);
