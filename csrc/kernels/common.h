@@ -100,6 +100,27 @@ __device__ __forceinline__ bool nsa_keep(uint64_t seed, uint64_t idx, uint32_t t
   return nsa_hash(seed, idx) >= thresh;
 }
 
+// Graph-safe dropout RNG.  The host passes each dropout call site a salt (drawn from
+// torch's CPU generator, so activation checkpointing replays it); kernels mix in a
+// device-side step counter that nsa_rng_advance() bumps once per micro-step from
+// inside the stream.  A captured HIP graph bakes the salts but replays the counter
+// increment, so every replayed micro-step draws fresh masks, and forward / backward
+// / recompute of one micro-step see the same counter.  Each translation unit has
+// its own copy of the counter (no relocatable device code); nsa_rng_advance bumps
+// all of them in lockstep.
+static __device__ uint64_t nsa_rng_step = 0;
+
+__device__ __forceinline__ uint64_t nsa_seed(uint64_t salt) {
+  return salt ^ (nsa_rng_step * 0xD1B54A32D192ED03ull);
+}
+
+#define NSA_DEFINE_RNG_ADVANCE(NAME)                                                       \
+  __global__ void NAME##_kernel() { nsa_rng_step += 1; }                                   \
+  NSA_API hipError_t NAME(hipStream_t s) {                                                 \
+    NAME##_kernel<<<1, 1, 0, s>>>();                                                        \
+    return hipGetLastError();                                                              \
+  }
+
 static inline uint32_t nsa_drop_thresh(float p) {
   double t = (double)p * 4294967296.0;
   if (t >= 4294967295.0) return 0xffffffffu;

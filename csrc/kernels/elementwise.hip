@@ -103,7 +103,8 @@ __global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const bf16_t* __restri
 }
 
 __global__ __launch_bounds__(kBlock) void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                        int64_t n, uint32_t thresh, float scale, uint64_t seed) {
+                                                        int64_t n, uint32_t thresh, float scale, uint64_t salt) {
+  const uint64_t seed = nsa_seed(salt);
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
     float f[8];
@@ -155,6 +156,18 @@ NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s
 NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
   gelu_bwd_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
   NSA_LAUNCH_CHECK();
+}
+
+NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_ew)
+NSA_API hipError_t nsa_rng_advance_emb(hipStream_t s);
+NSA_API hipError_t nsa_rng_advance_attn(hipStream_t s);
+
+// one micro-step's dropout counter bump in every translation unit (see common.h)
+NSA_API hipError_t nsa_rng_advance(hipStream_t s) {
+  hipError_t e = nsa_rng_advance_ew(s);
+  if (e == hipSuccess) e = nsa_rng_advance_emb(s);
+  if (e == hipSuccess) e = nsa_rng_advance_attn(s);
+  return e;
 }
 
 NSA_API hipError_t nsa_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t s) {

@@ -32,7 +32,8 @@ __device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
 template <typename XT>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx, const bf16_t* __restrict__ wte,
                                                      const bf16_t* __restrict__ wpe, XT* __restrict__ out, int N,
-                                                     int T, int C, uint32_t thresh, float scale, uint64_t seed) {
+                                                     int T, int C, uint32_t thresh, float scale, uint64_t salt) {
+  const uint64_t seed = nsa_seed(salt);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -58,7 +59,8 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
 template <typename XT>
 __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restrict__ idx,
                                                          const XT* __restrict__ dx, float* __restrict__ dwte, int N,
-                                                         int C, uint32_t thresh, float scale, uint64_t seed) {
+                                                         int C, uint32_t thresh, float scale, uint64_t salt) {
+  const uint64_t seed = nsa_seed(salt);
   extern __shared__ __attribute__((aligned(16))) float stage[];  // [4][C]
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -88,7 +90,8 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restr
 template <typename XT>
 __global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const XT* __restrict__ dx, float* __restrict__ dwpe,
                                                          int B, int T, int C, uint32_t thresh, float scale,
-                                                         uint64_t seed) {
+                                                         uint64_t salt) {
+  const uint64_t seed = nsa_seed(salt);
   const int octs = C / 8;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= T * octs) return;
@@ -152,6 +155,8 @@ hipError_t launch_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, i
 }  // namespace
 
 // idx: dense int64 [B*T] (callers pass a contiguous tensor); out / dx: bf16
+NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_emb)
+
 NSA_API hipError_t nsa_embedding_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
                                      int C, float p, uint64_t seed, hipStream_t s) {
   return launch_fwd<bf16_t>(idx, wte, wpe, out, N, T, C, p, seed, s);

@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_ker
   const bf16_t* qbase = base + hh * D;
   const bf16_t* kbase = base + C + hh * D;
   const bf16_t* vbase = base + 2 * C + hh * D;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
 
   // Q^T fragments (B operand): lane holds Q[qpos][16ks + 8h .. +8]
   bf16x8 qf[NKS];
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kern
   const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
   const float* lse_bh = lse + (int64_t)bh * T;
   const float* delta_bh = delta + (int64_t)bh * T;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
 
   // K^T / V^T fragments for S = Q·K^T and dP = dO·V^T (B operands): K[kpos][16ks+8h..]
   bf16x8 kf[NKS], vf[NKS];
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
   const bf16_t* base = qkv + (int64_t)b * T * row_stride;
   const bf16_t* kbase = base + C + hh * D;
   const bf16_t* vbase = base + 2 * C + hh * D;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
 
   // Q^T and dO^T fragments (B operands): lane holds row qpos, d = 16ks + 8h .. +8
   bf16x8 qf[NKS], gf[NKS];
@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
   const float* nls_bh = nls + (int64_t)bh * T;
   const float* nd_bh = nd + (int64_t)bh * T;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
   const uint32_t lds0 =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
@@ -1405,7 +1405,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
   const int qpos = q0w + r;
   const int qc = qpos < T ? qpos : T - 1;
   const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
   const uint32_t lds0 =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
@@ -1606,7 +1606,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd2_kernel(const bf16_t* __rest
   const int qpos = q0w + r;
   const int qc = qpos < T ? qpos : T - 1;
   const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const DropArgs dr{drop_thresh, drop_scale, seed, bh, T};
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
   const uint32_t lds0 =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
@@ -1893,6 +1893,8 @@ NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* do
     default: return hipErrorInvalidValue;
   }
 }
+
+NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_attn)
 
 NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {

@@ -1,6 +1,7 @@
 """Fused GPT ops: HIP kernels on gfx950, fp32 torch reference on CPU."""
 
 from .functional import (  # noqa: F401
+    rng_advance,
     add_layer_norm,
     attention,
     compute_weight,

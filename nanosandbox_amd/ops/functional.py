@@ -123,6 +123,18 @@ def new_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+def rng_advance(device) -> None:
+    """Bump the kernels' device-side dropout step counter (once per micro-step).
+
+    The per-call salts from ``new_seed`` are host values, baked into a captured
+    HIP graph; the counter is device state the kernels mix into every salt, and
+    this bump is itself a stream operation, so a replayed micro-step (forward,
+    backward and any recompute) draws masks no earlier replay used
+    (csrc/kernels/common.h ``nsa_seed``).  No-op on CPU."""
+    if torch.device(device).type == "cuda":
+        _lib.call("nsa_rng_advance", _lib.stream())
+
+
 # ----------------------------------------------------------------------------
 # dropout (hash-based on GPU: the mask is regenerated in backward, never stored)
 # ----------------------------------------------------------------------------

@@ -17,10 +17,14 @@ Why it is sound here:
   refreshes in place, and the learning rate lives in the (eager) optimizer step;
 * the GEMM autotuner is warmed up before capture, so no timing runs are captured.
 
+* dropout (the char config's p = 0.2): the per-call dropout salts are host values
+  and get baked into the graph, but every dropout kernel mixes them with a
+  device-side step counter that the captured micro-step bumps first
+  (``ops.rng_advance``), so each replay draws fresh masks, identical between its
+  forward and backward.
+
 When it is not used (eager fallback, decided by ``graph_capture_supported``):
-dropout > 0 (the counter-based dropout seeds are host values and would be baked
-into the graph), more than one rank (bucket-ready hooks are Python callbacks),
-CPU devices.
+more than one rank (bucket-ready hooks are Python callbacks), CPU devices.
 """
 
 from __future__ import annotations
@@ -31,8 +35,6 @@ import torch
 def graph_capture_supported(device: str, dropout: float, world_size: int) -> tuple[bool, str]:
     if not str(device).startswith("cuda") or not torch.cuda.is_available():
         return False, "graph capture needs a GPU device"
-    if dropout > 0.0:
-        return False, "dropout > 0: per-step dropout seeds cannot be baked into a graph"
     if world_size > 1:
         return False, "world_size > 1: gradient-bucket hooks run in Python during backward"
     return True, ""
@@ -41,7 +43,10 @@ def graph_capture_supported(device: str, dropout: float, world_size: int) -> tup
 class MicroStepGraph:
     """Captured ``loss = model(X, Y)[1] / gas; loss.backward()``, replayed per micro-step."""
 
-    def __init__(self, model, X: torch.Tensor, Y: torch.Tensor, gas: int, warmup: int = 2, zero_grad=None):
+    def __init__(self, model, X: torch.Tensor, Y: torch.Tensor, gas: int, warmup: int = 2, zero_grad=None,
+                 dropout: bool = False):
+        from ..ops import rng_advance
+
         self.model = model
         self.gas = gas
         self.X = X.detach().clone()
@@ -50,6 +55,8 @@ class MicroStepGraph:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):  # tuner timing runs, allocator warm-up, lazy init
+                if dropout:
+                    rng_advance(self.X.device)
                 _, loss = model(self.X, self.Y)
                 (loss / gas).backward()
         torch.cuda.current_stream().wait_stream(side)
@@ -58,6 +65,8 @@ class MicroStepGraph:
             zero_grad()  # the warm-up backwards accumulated into the gradient buffer
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
+            if dropout:
+                rng_advance(self.X.device)  # replayed: fresh dropout masks per micro-step
             _, loss = model(self.X, self.Y)
             self.loss = loss / gas
             self.loss.backward()

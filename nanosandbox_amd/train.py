@@ -29,6 +29,7 @@ import torch
 
 from .config import TRAIN_DEFAULTS, config_keys, parse_argv
 from .data import load_meta, make_batch_source, resolve_data_dir
+from .ops import rng_advance
 from .runtime import MicroStepGraph, graph_capture_supported
 from .models import GPT, GPTConfig
 from .optim import FlatParamStore
@@ -201,7 +202,8 @@ class Trainer:
         if self.use_graph:
             if self.graph is None:
                 self.graph = MicroStepGraph(self.model, X, Y, self.gas,
-                                            zero_grad=lambda: self.optimizer.zero_grad(set_to_none=True))
+                                            zero_grad=lambda: self.optimizer.zero_grad(set_to_none=True),
+                                            dropout=c["dropout"] > 0.0)
             for _ in range(self.gas):
                 loss = self.graph.run(X, Y)
                 X, Y = self.batches.get_batch("train")
@@ -215,6 +217,8 @@ class Trainer:
                 self.reducer.prepare(sync)
             elif self.ddp_impl == "torch":
                 self.model.require_backward_grad_sync = sync
+            if c["dropout"] > 0.0:
+                rng_advance(self.device)  # the dropout kernels' device step counter (graph-safe RNG)
             _, loss = self.model(X, Y)
             loss = loss / self.gas  # scale the loss to account for gradient accumulation
             # immediately async prefetch next batch while model is doing the forward pass on the GPU

@@ -221,6 +221,33 @@ def test_dropout_mask_consistency(kernels):
     assert torch.allclose(y[kept].float(), x[kept].float() / 0.8, rtol=1e-2)
 
 
+def test_dropout_device_step_counter(kernels):
+    """Graph-safe RNG: the same host salt gives the same mask until ``rng_advance``
+    bumps the kernels' device step counter, then a different one (dropout, embedding
+    and attention kernels alike)."""
+    from nanosandbox_amd import ops
+
+    x = torch.randn(4096, device=DEV).to(BF)
+    qkv = torch.randn(1, 128, 3 * 128, device=DEV).to(BF)
+    idx = torch.randint(0, 64, (2, 64), device=DEV)
+    wte = param(torch.randn(64, 64, device=DEV))
+    wpe = param(torch.randn(64, 64, device=DEV))
+
+    def draw():
+        torch.manual_seed(7)  # same salts every draw
+        return (ops.dropout(x, 0.3, True).float(), ops.attention(qkv, 2, 0.3, True).float(),
+                ops.embedding(idx, wte, wpe, 0.3, True, dtype=torch.float32).float())
+
+    a = draw()
+    b = draw()
+    ops.rng_advance(DEV)
+    c = draw()
+    torch.cuda.synchronize()
+    for u, v, w in zip(a, b, c):
+        assert torch.equal(u, v)
+        assert not torch.equal(u, w)
+
+
 # --------------------------------------------------------- flash attention
 def attn_ref(qkv, H):
     B, T, C3 = qkv.shape

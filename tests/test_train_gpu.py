@@ -78,6 +78,37 @@ def test_compile_hip_graph_matches_eager(kernels, tmp_path):
     assert lg[-1] < lg[0]
 
 
+def test_compile_hip_graph_with_dropout(kernels, tmp_path):
+    """compile=True with dropout (the char config's p = 0.2): the captured micro-step
+    bumps the device-side dropout counter, so replays on the same batch draw different
+    masks, and graph training tracks eager training."""
+    from nanosandbox_amd.train import Trainer
+
+    def run(compile_, steps=12):
+        torch.manual_seed(0)
+        tr = Trainer(_cfg(tmp_path, compile=compile_, dropout=0.2, bias=False, max_iters=steps,
+                          eval_interval=1000, out_dir=str(tmp_path / f"d{int(compile_)}"), seed=1234))
+        X, Y = tr.batches.get_batch("train")
+        losses = []
+        for _ in range(steps):
+            for g in tr.optimizer.param_groups:
+                g["lr"] = 2e-3
+            loss, _, X, Y = tr.train_step(X, Y)
+            losses.append(loss.item() * tr.gas)
+        return tr, losses
+
+    tg, lg = run(True)
+    assert tg.use_graph and tg.graph is not None
+    # two replays on one batch: fresh masks -> different losses
+    X, Y = tg.batches.get_batch("train")
+    l1 = tg.graph.run(X, Y).item()
+    l2 = tg.graph.run(X, Y).item()
+    assert l1 != l2
+    te, le = run(False)
+    assert lg[-1] < 0.9 * lg[0] and le[-1] < 0.9 * le[0]
+    assert abs(sum(lg[-4:]) - sum(le[-4:])) < 0.1 * abs(sum(le[-4:])), (lg, le)
+
+
 def test_sample_from_checkpoint_gpu(kernels, tmp_path):
     """sample.py on the GPU (bf16 compute, last-position logits, top-k multinomial) from a
     checkpoint the GPU trainer wrote; the char codec comes from the dataset's meta.pkl."""
