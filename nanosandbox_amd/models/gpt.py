@@ -200,7 +200,8 @@ class GPT(nn.Module):
         """Blocks + ln_f with every residual add fused into the following LayerNorm."""
         tr = self.transformer
         blocks = tr.h
-        h = blocks[0].ln_1(x)
+        ln = blocks[0].ln_1
+        x, h = ops.layer_norm_pass(x, ln.weight, ln.bias, out_dtype=ln.out_dtype)
         ckpt = self.grad_ckpt and self.training and torch.is_grad_enabled()
         for i, block in enumerate(blocks):
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else tr.ln_f

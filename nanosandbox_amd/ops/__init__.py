@@ -9,6 +9,7 @@ from .functional import (  # noqa: F401
     embedding,
     gelu,
     layer_norm,
+    layer_norm_pass,
     linear,
     lm_head_logits,
     lm_head_loss,

@@ -66,6 +66,7 @@ _SIGNATURES = {
     "nsa_flash_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_rng_advance": [c_void_p],
+    "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],
 }

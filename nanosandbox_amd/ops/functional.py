@@ -271,13 +271,14 @@ class LayerNormFn(torch.autograd.Function):
     the gradient of both x and y — no separate autograd add kernel."""
 
     @staticmethod
-    def forward(ctx, x, y, w, b, out_dtype):
+    def forward(ctx, x, y, w, b, out_dtype, passthrough=False):
         ctx.set_materialize_grads(False)
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         N = x2.shape[0]
         ctx.has_bias = b is not None
-        ctx.fused = y is not None
+        ctx.fused = y is not None or passthrough
+        ctx.passthrough = passthrough and y is None
         out_dtype = out_dtype or (y.dtype if y is not None else x.dtype)
         ctx.y_dtype = y.dtype if y is not None else None
         if x.is_cuda:
@@ -314,6 +315,8 @@ class LayerNormFn(torch.autograd.Function):
         hshape = (*x.shape[:-1], C)
         if y is not None:
             return inp.view(x.shape), h.view(hshape)
+        if ctx.passthrough:
+            return x.view_as(x), h.view(hshape)
         return h.view(hshape)
 
     @staticmethod
@@ -328,8 +331,8 @@ class LayerNormFn(torch.autograd.Function):
         N = x2.shape[0]
         shape = (*(dh if dh is not None else ds).shape[:-1], C)
         if dh is None:  # only the residual output was used
-            dyb = ds.to(ctx.y_dtype) if ctx.fused else None
-            return ds, dyb, None, None, None
+            dyb = ds.to(ctx.y_dtype) if (ctx.fused and not ctx.passthrough) else None
+            return ds, dyb, None, None, None, None
         dy2 = dh.reshape(-1, C)
         if dh.is_cuda:
             x32 = x2.dtype == F32
@@ -339,7 +342,8 @@ class LayerNormFn(torch.autograd.Function):
                 ds2 = ds2.to(x2.dtype)
             dx = torch.empty_like(x2)
             # the fused form also hands the branch (y) its gradient in y's dtype
-            dyb = torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype) if (ctx.fused and x32) else None
+            dyb = (torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype)
+                   if (ctx.fused and x32 and not ctx.passthrough) else None)
             nblk = min(_LN_BWD_BLOCKS_X32 if x32 else _LN_BWD_BLOCKS, max(1, (N + 7) // 8))
             dw_part = torch.empty(nblk, C, device=dh.device, dtype=F32)
             db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
@@ -355,9 +359,9 @@ class LayerNormFn(torch.autograd.Function):
             gw = _colsum_into(w, dw_part)
             gb = _colsum_into(b, db_part) if b is not None else None
             dx = dx.view(shape)
-            if not ctx.fused:
-                return dx, None, gw, gb, None
-            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None
+            if not ctx.fused or ctx.passthrough:
+                return dx, None, gw, gb, None, None
+            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None, None
         xf = x2.float()
         d = dy2.float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
@@ -369,9 +373,9 @@ class LayerNormFn(torch.autograd.Function):
         gw = _accumulate(w, (d * xhat).sum(0))
         gb = _accumulate(b, d.sum(0)) if b is not None else None
         dxs = dx.to(x2.dtype).view(shape)
-        if not ctx.fused:
-            return dxs, None, gw, gb, None
-        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None
+        if not ctx.fused or ctx.passthrough:
+            return dxs, None, gw, gb, None, None
+        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None, None
 
 
 def _colsum_into(p, partial):
@@ -390,6 +394,14 @@ def _colsum_into(p, partial):
 def layer_norm(x, w, b, out_dtype=None):
     """LN(x); ``out_dtype`` (default x's dtype) is the dtype of the normalised output."""
     return LayerNormFn.apply(x, None, w, b, out_dtype)
+
+
+def layer_norm_pass(x, w, b, out_dtype=None):
+    """(x, LN(x)) as one node: the returned x is the residual stream's continuation,
+    so its gradient enters the LayerNorm backward kernel as the residual input (one
+    pass computes dx = LN'(dh) + ds) instead of being summed with LN's own input
+    gradient by a separate add kernel."""
+    return LayerNormFn.apply(x, None, w, b, out_dtype, True)
 
 
 def add_layer_norm(x, y, w, b, out_dtype=None):

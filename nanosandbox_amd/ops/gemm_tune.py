@@ -30,6 +30,7 @@ import threading
 
 import torch
 
+from . import _lib
 from . import gemm as _gemm
 
 F32 = torch.float32
@@ -181,17 +182,29 @@ def _wt(w):
     amortised over every micro-step of an optimizer step.  Inside HIP-graph capture
     the transpose is recomputed (captured into the graph) instead of cached."""
     if w.is_cuda and torch.cuda.is_current_stream_capturing():
-        return w.t().contiguous()
+        return _transpose(w)
     key = (_weight_gen, w._version, w.data_ptr())
     hit = getattr(w, "_nsa_wt", None)
     if hit is not None and hit[0] == key:
         return hit[1]
-    t = w.t().contiguous()
+    t = _transpose(w, out=hit[1] if hit is not None else None)  # rebuilt in place each step
     try:
         w._nsa_wt = (key, t)
     except (AttributeError, RuntimeError):
         pass
     return t
+
+
+def _transpose(w, out=None):
+    """w^T, contiguous: our bf16 transpose kernel (LDS-free 8x8 register blocks) when the
+    shape allows, else torch's copy."""
+    R, C = w.shape
+    if w.is_cuda and w.dtype == torch.bfloat16 and R % 64 == 0 and C % 64 == 0 and w.is_contiguous():
+        if out is None or out.shape != (C, R) or out.dtype != w.dtype or out.device != w.device:
+            out = torch.empty(C, R, device=w.device, dtype=w.dtype)
+        _lib.call("nsa_transpose_bf16", _lib.ptr(w), _lib.ptr(out), R, C, _lib.stream())
+        return out
+    return w.t().contiguous()
 
 
 def dgrad(dy2, w):

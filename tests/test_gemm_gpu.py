@@ -99,3 +99,16 @@ def test_transposed_weight_dgrad_cache(kernels):
     assert not torch.equal(stale, dy @ w)  # ... so the cache is stale until announced
     gemm_tune.weights_changed()
     assert torch.equal(via_t(), dy @ w)
+
+
+@pytest.mark.parametrize("R,C", [(768, 3072), (50304, 768), (64, 128), (2304, 768)])
+def test_transpose_bf16(kernels, R, C):
+    """The weight-transpose kernel behind the cached K-contiguous dgrad weights."""
+    from nanosandbox_amd.ops import gemm_tune
+
+    w = torch.randn(R, C, device="cuda").to(torch.bfloat16)
+    t = gemm_tune._transpose(w)
+    assert t.shape == (C, R) and t.is_contiguous()
+    assert torch.equal(t, w.t())
+    t2 = gemm_tune._transpose(w * 2, out=t)  # rebuilt in place
+    assert t2.data_ptr() == t.data_ptr() and torch.equal(t2, (w * 2).t())
