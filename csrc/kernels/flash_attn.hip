@@ -1384,9 +1384,9 @@ __device__ __forceinline__ void dq2_tile(const char* kt, const char* vt, const b
 
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
-    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
-    const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale, float scale_log2,
-    uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
+    const float* __restrict__ lse, float* __restrict__ nls, float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B,
+    int T, int H, float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
   constexpr int D = 64;
   constexpr int SLOT = 2 * DQ2_T;  // K, V
   constexpr int NS = NSA_DQ2_NS, LA = NS - 1;
@@ -1443,8 +1443,26 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
     gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
   }
   // lse·log2e = -nls·c (nls = -lse/scale), and the -delta tile
-  const float lse2 = -nls[(int64_t)bh * T + qc] * scale_log2;
-  const float ndl = nd[(int64_t)bh * T + qc];
+  // this kernel runs first and forms the row constants itself: delta = rowsum(dO * O)
+  // from the dO fragments it holds anyway plus the matching O pieces (the two lane
+  // halves hold d = 8h + 16ks .. +8), written out for the dK/dV kernel as -delta and
+  // -lse/scale (no separate preprocessing pass over O and dO)
+  float dpart = 0.0f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    float fo[8], fg[8];
+    load8(o + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h, fo);
+    unpack8(__builtin_bit_cast(uint4, gf[ks]), fg);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dpart += fo[e] * fg[e];
+  }
+  const float ndl = -half_swap_sum(dpart);
+  const float lse_q = lse[(int64_t)bh * T + qc];
+  const float lse2 = lse_q * kLog2e;
+  if (h == 0 && qpos < T) {
+    nd[(int64_t)bh * T + qpos] = ndl;
+    nls[(int64_t)bh * T + qpos] = -lse_q / scale;
+  }
   asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(gf[0]), "v"(gf[1]), "v"(gf[2]),
                "v"(gf[3]), "v"(lse2), "v"(ndl));  // retire these loads before the ring loop (see dK/dV)
   f32x16 ndt;
@@ -1807,20 +1825,39 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
   return hipGetLastError();
 }
 
-// v2 backward (D = 64, T % 32 == 0): pre2 (-delta, -lse/scale) -> dK/dV kernel (64 keys
-// per wave) -> the split-mode dQ kernel.  ws = 2 x [B, H, T] fp32.
+// v2 backward (D = 64, T % 32 == 0): dQ v2 kernel (also forms the row constants -delta,
+// -lse/scale) -> dK/dV v2 kernel.  ws = 2 x [B, H, T] fp32.  NSA_FLASH_DQ2=0: pre2 ->
+// dK/dV v2 -> v1 dQ kernel.
 hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws, void* dqkv,
                          int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
   constexpr int D = 64;
   float* nd = (float*)ws;
   float* nls = nd + (int64_t)B * H * T;
-  const int64_t threads = (int64_t)B * T * H * (D / 8);
-  flash_bwd_pre2_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-      (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, nd, nls, 1.0f / scale, B, T, H);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int n_qt = (T + 127) / 128;
+  hipError_t e;
+  const char* dq2 = getenv("NSA_FLASH_DQ2");
+  const bool use_dq2 = !(dq2 && dq2[0] == '0');
+  if (use_dq2) {
+    // dQ first: it also writes the row constants (-delta, -lse/scale) the dK/dV kernel reads
+    if (th)
+      flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                              (const bf16_t*)o, (const float*)lse, nls, nd,
+                                                              (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
+                                                              dscale, seed);
+    else
+      flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                               (const bf16_t*)o, (const float*)lse, nls, nd,
+                                                               (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
+                                                               dscale, seed);
+  } else {
+    const int64_t threads = (int64_t)B * T * H * (D / 8);
+    flash_bwd_pre2_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
+        (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, nd, nls, 1.0f / scale, B, T, H);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
   // geometry (NSA_FLASH_DKDV): k1w4 = 1 key block per wave, 4 waves (default: 216 VGPRs,
   // two independent workgroups per CU), k1w8, k2w4 (2 key blocks per wave, 1 wave/SIMD).
   // A/B at B120 T1024 H12 (whole backward incl. the dQ kernel): v1 1307, k2w4 1304,
@@ -1846,20 +1883,8 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   else NSA_DKDV2(2, 4, false);
 #undef NSA_DKDV2
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int n_qt = (T + 127) / 128;
-  const char* dq2 = getenv("NSA_FLASH_DQ2");
-  if (!(dq2 && dq2[0] == '0')) {
-    if (th)
-      flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
-                                                              (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                              dscale, seed);
-    else
-      flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
-                                                               (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                               dscale, seed);
-    return hipGetLastError();
-  }
+  if (e != hipSuccess || use_dq2) return e;
+  // NSA_FLASH_DQ2=0: the v1 dQ kernel (reads -delta with delta_sign = -1)
   if (th)
     flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                               (const float*)lse, nd, (bf16_t*)dqkv, B, T, H, scale,

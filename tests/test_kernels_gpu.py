@@ -331,8 +331,8 @@ def test_flash_attention_deferred_rescale(kernels, monkeypatch, pattern, fwd):
 
 @pytest.mark.parametrize("T", [320, 1024, 96])
 @pytest.mark.parametrize("p", [0.0, 0.2])
-@pytest.mark.parametrize("geo", ["k1w4", "k1w8", "k2w4"])
-def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo):
+@pytest.mark.parametrize("geo,dq2", [("k1w4", "1"), ("k1w8", "1"), ("k2w4", "1"), ("k1w4", "0")])
+def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo, dq2):
     """The v2 backward (D = 64: LDS-DMA-fed dK/dV kernel in each geometry + the v2 dQ
     kernel) against the v1 kernels, with and without dropout; T = 320 and 96 leave the
     last key / query workgroups partial."""
@@ -344,6 +344,7 @@ def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo):
     dy = torch.randn(B, T, H * D, device=DEV).to(BF)
     grads = {}
     monkeypatch.setenv("NSA_FLASH_DKDV", geo)
+    monkeypatch.setenv("NSA_FLASH_DQ2", dq2)  # 0: pre-pass + v1 dQ kernel after the v2 dK/dV
     for ver in ("v1", "v2"):
         monkeypatch.setenv("NSA_FLASH_BWD", ver)
         torch.manual_seed(5)
