@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="bitwise-reproducible step: fixed-order split-K weight gradients, sorted embedding "
+                         "backward, ordered LayerNorm dW/db (no fp32 atomics)")
     ap.add_argument("--bf16-residual", action="store_true",
                     help="keep the residual stream and its gradient in bf16 (default fp32: nanoGPT's "
                          "autocast contract, fp32 embedding sum and fp32 + bf16 residual adds)")
@@ -100,7 +103,7 @@ def main():
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
                dropout=0.0, bias=False, compile=False, device="cuda", dtype="bfloat16", backend="nccl",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
-               fp32_residual=not args.bf16_residual,
+               fp32_residual=not args.bf16_residual, deterministic=args.deterministic,
                out_dir="/tmp/nsa_bench_out", metrics_jsonl=False, learning_rate=6e-4, warmup_iters=0,
                decay_lr=False)
 
@@ -174,7 +177,8 @@ def main():
                        "tokens_per_step": tokens_per_step, "micro_batch": args.micro_batch,
                        "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
                        "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
-                       "residual_dtype": "bf16" if args.bf16_residual else "fp32"},
+                       "residual_dtype": "bf16" if args.bf16_residual else "fp32",
+                       "deterministic": args.deterministic},
             "mfu_vs_2.5PF": round(mfu, 4),
             "loss": round(lossf, 4),
         }), flush=True)

@@ -114,10 +114,17 @@ __device__ __forceinline__ uint64_t nsa_seed(uint64_t salt) {
   return salt ^ (nsa_rng_step * 0xD1B54A32D192ED03ull);
 }
 
+// NAME(stream) bumps this TU's counter; NAME##_set(value, stream) sets it (a new run
+// restarts its dropout stream at 0, independent of earlier runs in the process)
 #define NSA_DEFINE_RNG_ADVANCE(NAME)                                                       \
   __global__ void NAME##_kernel() { nsa_rng_step += 1; }                                   \
+  __global__ void NAME##_set_kernel(uint64_t v) { nsa_rng_step = v; }                      \
   NSA_API hipError_t NAME(hipStream_t s) {                                                 \
     NAME##_kernel<<<1, 1, 0, s>>>();                                                        \
+    return hipGetLastError();                                                              \
+  }                                                                                        \
+  NSA_API hipError_t NAME##_set(uint64_t v, hipStream_t s) {                               \
+    NAME##_set_kernel<<<1, 1, 0, s>>>(v);                                                   \
     return hipGetLastError();                                                              \
   }
 

@@ -164,6 +164,34 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
   }
 }
 
+// out[i] += sum over s = 0 .. S-1 (in that order) of ws[s * n + i]: the fixed-order
+// reduction of split-K weight-gradient partials (deterministic mode)
+__global__ __launch_bounds__(kBlock) void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                              int64_t n, int splits) {
+  const int64_t nv = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    float4 acc = reinterpret_cast<const float4*>(ws)[i];
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (int64_t)sp * n)[i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    float4 o = reinterpret_cast<float4*>(out)[i];
+    o.x += acc.x;
+    o.y += acc.y;
+    o.z += acc.z;
+    o.w += acc.w;
+    reinterpret_cast<float4*>(out)[i] = o;
+  }
+  for (int64_t i = nv * 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    float acc = ws[i];
+    for (int sp = 1; sp < splits; ++sp) acc += ws[(int64_t)sp * n + i];
+    out[i] += acc;
+  }
+}
+
 // y[i] *= s[0]  (bf16 tensor scaled by a device scalar; no host sync)
 __global__ __launch_bounds__(kBlock) void scale_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                            const float* __restrict__ s, int64_t n) {
@@ -195,6 +223,16 @@ NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_ew)
 NSA_API hipError_t nsa_rng_advance_emb(hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_attn(hipStream_t s);
+NSA_API hipError_t nsa_rng_advance_emb_set(uint64_t v, hipStream_t s);
+NSA_API hipError_t nsa_rng_advance_attn_set(uint64_t v, hipStream_t s);
+
+// set every translation unit's dropout step counter (start of a run)
+NSA_API hipError_t nsa_rng_set(uint64_t v, hipStream_t s) {
+  hipError_t e = nsa_rng_advance_ew_set(v, s);
+  if (e == hipSuccess) e = nsa_rng_advance_emb_set(v, s);
+  if (e == hipSuccess) e = nsa_rng_advance_attn_set(v, s);
+  return e;
+}
 
 // one micro-step's dropout counter bump in every translation unit (see common.h)
 NSA_API hipError_t nsa_rng_advance(hipStream_t s) {
@@ -209,6 +247,11 @@ NSA_API hipError_t nsa_dropout(const void* x, void* y, int64_t n, float p, uint6
   dropout_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, nsa_drop_thresh(p), scale,
                                                     seed);
   NSA_LAUNCH_CHECK();
+}
+
+NSA_API hipError_t nsa_splitk_reduce(const void* ws, void* out, int64_t n, int splits, hipStream_t s) {
+  splitk_reduce_kernel<<<grid_for(n / 4 + 1), kBlock, 0, s>>>((const float*)ws, (float*)out, n, splits);
+  return hipGetLastError();
 }
 
 NSA_API hipError_t nsa_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t s) {

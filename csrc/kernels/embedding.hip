@@ -123,6 +123,52 @@ __global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const XT* __restrict__
   g[1] = g1;
 }
 
+// Deterministic dwte (deterministic mode; the default kernel above adds rows with fp32
+// atomics in arrival order).  The caller sorts the token positions by vocab id with a
+// stable sort (order) and passes the segment offsets (seg[v] .. seg[v+1]); one wave per
+// vocab row sums its tokens' gradient rows in token order and adds the sum into the
+// row once (a single writer: no atomics) -- cdna_hip_programming.md App. B, "scatter-add
+// without atomics".  Bitwise reproducible for any schedule.
+template <typename XT>
+__global__ __launch_bounds__(256) void emb_bwd_wte_det_kernel(const int64_t* __restrict__ order,
+                                                             const int64_t* __restrict__ seg,
+                                                             const XT* __restrict__ dx, float* __restrict__ dwte,
+                                                             int V, int C, uint32_t thresh, float scale,
+                                                             uint64_t salt) {
+  const uint64_t seed = nsa_seed(salt);
+  const int lane = threadIdx.x & 63;
+  const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const int64_t beg = seg[v], end = seg[v + 1];
+  if (beg == end) return;
+  for (int c = lane * 8; c < C; c += 512) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t k = beg; k < end; ++k) {
+      const int64_t row = order[k];
+      float f[8];
+      ld8(dx + row * C + c, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = f[j];
+        if (thresh) x = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? x * scale : 0.0f;
+        acc[j] += x;
+      }
+    }
+    float4* g = reinterpret_cast<float4*>(dwte + (int64_t)v * C + c);
+    float4 g0 = g[0], g1 = g[1];
+    g0.x += acc[0];
+    g0.y += acc[1];
+    g0.z += acc[2];
+    g0.w += acc[3];
+    g1.x += acc[4];
+    g1.y += acc[5];
+    g1.z += acc[6];
+    g1.w += acc[7];
+    g[0] = g0;
+    g[1] = g1;
+  }
+}
+
 template <typename XT>
 hipError_t launch_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T, int C, float p,
                       uint64_t seed, hipStream_t s) {
@@ -145,6 +191,21 @@ hipError_t launch_bwd(const void* idx, const void* dx, void* dwte, void* dwpe, i
   if (grid > 2048) grid = 2048;
   emb_bwd_wte_kernel<XT><<<grid, 256, 4 * C * sizeof(float), s>>>((const int64_t*)idx, (const XT*)dx,
                                                                    (float*)dwte, N, C, th, scale, seed);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int work = T * (C / 8);
+  emb_bwd_wpe_kernel<XT><<<(work + 255) / 256, 256, 0, s>>>((const XT*)dx, (float*)dwpe, B, T, C, th, scale, seed);
+  return hipGetLastError();
+}
+
+template <typename XT>
+hipError_t launch_bwd_det(const void* order, const void* seg, const void* dx, void* dwte, void* dwpe, int B, int T,
+                          int C, int V, float p, uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  emb_bwd_wte_det_kernel<XT><<<(V + 3) / 4, 256, 0, s>>>((const int64_t*)order, (const int64_t*)seg,
+                                                         (const XT*)dx, (float*)dwte, V, C, th, scale, seed);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int work = T * (C / 8);
@@ -176,4 +237,12 @@ NSA_API hipError_t nsa_embedding_fwd_x32(const void* idx, const void* wte, const
 NSA_API hipError_t nsa_embedding_bwd_x32(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T,
                                          int C, float p, uint64_t seed, hipStream_t s) {
   return launch_bwd<float>(idx, dx, dwte, dwpe, B, T, C, p, seed, s);
+}
+
+// deterministic backward (order: token positions stably sorted by id, seg: [V + 1] offsets)
+NSA_API hipError_t nsa_embedding_bwd_det(const void* order, const void* seg, const void* dx, void* dwte, void* dwpe,
+                                         int B, int T, int C, int V, int dx_fp32, float p, uint64_t seed,
+                                         hipStream_t s) {
+  if (dx_fp32) return launch_bwd_det<float>(order, seg, dx, dwte, dwpe, B, T, C, V, p, seed, s);
+  return launch_bwd_det<bf16_t>(order, seg, dx, dwte, dwpe, B, T, C, V, p, seed, s);
 }

@@ -43,7 +43,9 @@ constexpr int EP_LD = 68;                                 // epilogue row pitch 
 constexpr int EP_BYTES = (NTHREADS / 64) * 64 * EP_LD * 4;  // 136 KiB
 constexpr int SMEM_BYTES = LDS_BYTES > EP_BYTES ? LDS_BYTES : EP_BYTES;
 
-enum Epi : int { EPI_STORE_BF16 = 0, EPI_ATOMIC_F32 = 1, EPI_GELU = 2, EPI_DGELU = 3 };
+// EPI_STORE_F32: split z stores its fp32 partial tile to C + z * M * ldc (plain stores;
+// the deterministic weight-gradient path sums the splits in a fixed order afterwards)
+enum Epi : int { EPI_STORE_BF16 = 0, EPI_ATOMIC_F32 = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_STORE_F32 = 4 };
 
 // ---- swizzled LDS addressing -------------------------------------------------
 // K-contiguous image [rows][64]: 128-B rows, chunk' = chunk ^ ((row >> 1) & 7)
@@ -215,14 +217,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmArgs g) {
     __builtin_amdgcn_wave_barrier();
     const int row_base = m0 + wm * WTM + half * 64;
     const int col_base = n0 + wn * WTN;
-    if constexpr (EPI == EPI_ATOMIC_F32) {
+    if constexpr (EPI == EPI_ATOMIC_F32 || EPI == EPI_STORE_F32) {
       // one wave instruction = one 64-float (256 B) contiguous row segment
       float* C = reinterpret_cast<float*>(g.C);
+      if constexpr (EPI == EPI_STORE_F32) C += (int64_t)blockIdx.z * g.M * g.ldc;
       const int col = col_base + lane;
       if (col < g.N) {
         for (int rr = 0; rr < 64; ++rr) {
           const int row = row_base + rr;
-          if (row < g.M) atomicAdd(C + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+          if (row < g.M) {
+            if constexpr (EPI == EPI_STORE_F32)
+              C[(int64_t)row * g.ldc + col] = ep[rr * EP_LD + lane];
+            else
+              atomicAdd(C + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+          }
         }
       }
     } else {
@@ -319,7 +327,7 @@ template <int EPI, bool DIRECT>
 __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int wave) {
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
-  if constexpr (EPI == EPI_ATOMIC_F32 || !DIRECT) {
+  if constexpr (EPI == EPI_ATOMIC_F32 || EPI == EPI_STORE_F32 || !DIRECT) {
     // re-shape through LDS so each atomic wave-instruction covers one 256-B row
     __syncthreads();
     float* ep = reinterpret_cast<float*>(smem) + wave * 64 * EP_LD;
@@ -338,12 +346,19 @@ __device__ __forceinline__ void ring_epilogue(const GemmArgs& g, f32x4 (&acc)[FM
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int row_base = m0 + wm * WTM + half * 64;
-      if constexpr (EPI == EPI_ATOMIC_F32) {
+      if constexpr (EPI == EPI_ATOMIC_F32 || EPI == EPI_STORE_F32) {
+        float* Cz = C;
+        if constexpr (EPI == EPI_STORE_F32) Cz += (int64_t)blockIdx.z * g.M * g.ldc;
         const int col = n0 + wn * WTN + lane;
         if (col < g.N) {
           for (int rr = 0; rr < 64; ++rr) {
             const int row = row_base + rr;
-            if (row < g.M) atomicAdd(C + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+            if (row < g.M) {
+              if constexpr (EPI == EPI_STORE_F32)
+                Cz[(int64_t)row * g.ldc + col] = ep[rr * EP_LD + lane];
+              else
+                atomicAdd(Cz + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+            }
           }
         }
       } else {
@@ -954,7 +969,7 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.k_per_split = a.K / splits;
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  if constexpr (A_K && EPI != EPI_ATOMIC_F32) {
+  if constexpr (A_K && EPI != EPI_ATOMIC_F32 && EPI != EPI_STORE_F32) {
     if (variant == 9 || variant == 10) {
       if (splits != 1) return hipErrorInvalidValue;
       const int tiles = a.tiles_m * a.tiles_n;
@@ -990,7 +1005,7 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
 // layout: 0 = NT (A [M][K], B [N][K]: forward), 1 = NN (A [M][K], B [K][N]: input grad),
 //         2 = TN (A stored [K][M], B [K][N]: weight grad)
 // epi: 0 store bf16, 1 fp32 atomic add into C, 2 store pre-activation + gelu into C2,
-//      3 store acc * gelu'(U)
+//      3 store acc * gelu'(U), 4 fp32 store of split z's partial into C + z*M*ldc
 // bits 8..15 of `epi` select the pipeline: 0 = register-staged BK=64 double buffer,
 // 1..4 = LDS-DMA ring (BK=32 slices): 1 = 4 slots (2 in flight) + LDS epilogue,
 // 2 = 5 slots + LDS epilogue, 3 = 4 slots + direct stores, 4 = 5 slots + direct stores,
@@ -1004,7 +1019,7 @@ NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const v
   epi &= 0xff;
   if (K % BK != 0 || splits < 1 || splits > K / BK || M < 8 || N < 8 || M % 8 || N % 8) return hipErrorInvalidValue;
   if (layout == 2 && M % 8) return hipErrorInvalidValue;
-  if (epi != EPI_ATOMIC_F32 && splits != 1) return hipErrorInvalidValue;
+  if (epi != EPI_ATOMIC_F32 && epi != EPI_STORE_F32 && splits != 1) return hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A;
   a.B = (const bf16_t*)B;
@@ -1022,6 +1037,7 @@ NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const v
     switch (epi) {                                                                     \
       case EPI_STORE_BF16: return launch<AK, BKc, EPI_STORE_BF16>(a, splits, variant, s);       \
       case EPI_ATOMIC_F32: return launch<AK, BKc, EPI_ATOMIC_F32>(a, splits, variant, s);       \
+      case EPI_STORE_F32: return launch<AK, BKc, EPI_STORE_F32>(a, splits, variant, s);         \
       case EPI_GELU: return launch<AK, BKc, EPI_GELU>(a, splits, variant, s);                   \
       case EPI_DGELU: return launch<AK, BKc, EPI_DGELU>(a, splits, variant, s);                 \
       default: return hipErrorInvalidValue;                                            \

@@ -159,3 +159,11 @@ NSA_API hipError_t nsa_colsum_accum(const void* partial, void* out, int rows, in
   colsum_kernel<<<grid, kBlock, 0, s>>>((const float*)partial, (float*)out, rows, C, rps);
   NSA_LAUNCH_CHECK();
 }
+
+// deterministic mode: one row range per column block, so each column's single atomic
+// add lands on the flat gradient in a fixed order (bitwise reproducible)
+NSA_API hipError_t nsa_colsum_accum_ordered(const void* partial, void* out, int rows, int C, hipStream_t s) {
+  dim3 grid((C + 63) / 64, 1);
+  colsum_kernel<<<grid, kBlock, 0, s>>>((const float*)partial, (float*)out, rows, C, rows);
+  NSA_LAUNCH_CHECK();
+}

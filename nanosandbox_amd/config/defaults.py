@@ -59,6 +59,7 @@ TRAIN_DEFAULTS = dict(
     grad_reduce_dtype="float32",  # 'float32' | 'bfloat16' (compressed all-reduce)
     grad_ckpt=False,  # recompute each Block in backward (activation checkpointing)
     fp32_residual=True,  # residual stream + its gradient in fp32 (nanoGPT autocast contract); False: bf16
+    deterministic=False,  # bitwise-reproducible steps: no fp32 atomics (fixed-order split-K, sorted embedding bwd)
     metrics_jsonl=True,  # write <out_dir>/metrics.jsonl
     tensorboard_dir="",  # '' disables; else tfevents written to <tensorboard_dir>/<run>
     auto_resume=False,  # resume from <out_dir>/ckpt.pt if it exists (elastic restarts)

@@ -2,6 +2,8 @@
 
 from .functional import (  # noqa: F401
     rng_advance,
+    rng_set,
+    set_deterministic,
     add_layer_norm,
     attention,
     compute_weight,

@@ -50,6 +50,7 @@ _SIGNATURES = {
     "nsa_layernorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_void_p],
     "nsa_colsum_accum": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "nsa_colsum_accum_ordered": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gelu_fwd": [c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_gelu_bwd": [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_dropout": [c_void_p, c_void_p, c_int64, c_float, c_uint64, c_void_p],
@@ -66,6 +67,10 @@ _SIGNATURES = {
     "nsa_flash_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_rng_advance": [c_void_p],
+    "nsa_rng_set": [c_uint64, c_void_p],
+    "nsa_splitk_reduce": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
+    "nsa_embedding_bwd_det": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                              c_float, c_uint64, c_void_p],
     "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],

@@ -123,6 +123,21 @@ def new_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+def set_deterministic(flag: bool) -> None:
+    """Bitwise-reproducible training (config key ``deterministic``): weight gradients
+    reduce split-K partials in a fixed order and the embedding backward sums each vocab
+    row's tokens in token order (no fp32 atomics anywhere on the step).  Every other
+    kernel of the step is already order-deterministic."""
+    _tune.DETERMINISTIC = bool(flag)
+
+
+def rng_set(device, value: int = 0) -> None:
+    """Set the kernels' device-side dropout step counter (a run starts at 0, so two
+    runs with the same seed in one process draw the same masks)."""
+    if torch.device(device).type == "cuda":
+        _lib.call("nsa_rng_set", int(value), _lib.stream())
+
+
 def rng_advance(device) -> None:
     """Bump the kernels' device-side dropout step counter (once per micro-step).
 
@@ -220,8 +235,17 @@ class EmbeddingFn(torch.autograd.Function):
             if ret_wpe:
                 gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
             assert dx.dtype in (F32, BF16)
-            _lib.call("nsa_embedding_bwd_x32" if dx.dtype == F32 else "nsa_embedding_bwd", _lib.ptr(idx),
-                      _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe), B, T, C, ctx.p, ctx.seed, _lib.stream())
+            if _tune.DETERMINISTIC:
+                # atomic-free: token positions stably sorted by id, one writer per vocab row
+                flat = idx.view(-1)
+                order = torch.argsort(flat, stable=True)
+                seg = torch.zeros(V + 1, device=dx.device, dtype=torch.int64)
+                torch.cumsum(torch.bincount(flat, minlength=V), 0, out=seg[1:])
+                _lib.call("nsa_embedding_bwd_det", _lib.ptr(order), _lib.ptr(seg), _lib.ptr(dx), _lib.ptr(gwte),
+                          _lib.ptr(gwpe), B, T, C, V, 1 if dx.dtype == F32 else 0, ctx.p, ctx.seed, _lib.stream())
+            else:
+                _lib.call("nsa_embedding_bwd_x32" if dx.dtype == F32 else "nsa_embedding_bwd", _lib.ptr(idx),
+                          _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe), B, T, C, ctx.p, ctx.seed, _lib.stream())
             out_wte = gwte.to(wte.dtype) if ret_wte else None
             out_wpe = gwpe.to(wpe.dtype) if ret_wpe else None
             if not ret_wte:
@@ -382,12 +406,13 @@ def _colsum_into(p, partial):
     """Reduce per-block partial column sums into p.main_grad (fused) or a fresh fp32 grad."""
     mg = getattr(p, "main_grad", None)
     rows, C = partial.shape
+    fn = "nsa_colsum_accum_ordered" if _tune.DETERMINISTIC else "nsa_colsum_accum"
     if mg is not None:
-        _lib.call("nsa_colsum_accum", _lib.ptr(partial), _lib.ptr(mg), rows, C, _lib.stream())
+        _lib.call(fn, _lib.ptr(partial), _lib.ptr(mg), rows, C, _lib.stream())
         notify_grad_ready(p)
         return None
     out = torch.zeros(C, device=partial.device, dtype=F32)
-    _lib.call("nsa_colsum_accum", _lib.ptr(partial), _lib.ptr(out), rows, C, _lib.stream())
+    _lib.call(fn, _lib.ptr(partial), _lib.ptr(out), rows, C, _lib.stream())
     return out.to(p.dtype)
 
 

@@ -21,7 +21,7 @@ from . import _lib
 
 BF16 = torch.bfloat16
 LAYOUT_NT, LAYOUT_NN, LAYOUT_TN = 0, 1, 2
-EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
+EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU, EPI_STORE_F32 = 0, 1, 2, 3, 4
 BK = 64
 TILE = 256
 # pipeline variant (csrc/kernels/gemm.hip nsa_gemm): 0 = register-staged, 1-4 = 32-deep LDS-DMA ring,
@@ -118,8 +118,14 @@ def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=None):
     return best
 
 
-def wgrad_acc(dy2, x2, g32, splits=None, variant=None):
-    """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel."""
+def wgrad_acc(dy2, x2, g32, splits=None, variant=None, deterministic=False):
+    """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel.
+
+    Default: every K split adds its partial tile into g32 with fp32 atomics (arrival
+    order, so the last bits vary run to run).  ``deterministic``: each split stores
+    its partial to a workspace and one pass adds the splits to g32 in split order
+    (bitwise reproducible; with one split the single atomic add per element is
+    already order-free)."""
     T, N_out = dy2.shape
     K_in = x2.shape[1]
     _check(dy2, "dy")
@@ -127,6 +133,12 @@ def wgrad_acc(dy2, x2, g32, splits=None, variant=None):
     _check(g32, "grad")
     if splits is None:
         splits = wgrad_splits(N_out, K_in, T)
+    if deterministic and splits > 1:
+        ws = torch.empty(splits, N_out, K_in, device=g32.device, dtype=torch.float32)
+        _call(LAYOUT_TN, EPI_STORE_F32, dy2, N_out, x2, K_in, ws, K_in, N_out, K_in, T, splits=splits,
+              variant=variant)
+        _lib.call("nsa_splitk_reduce", _lib.ptr(ws), _lib.ptr(g32), g32.numel(), splits, _lib.stream())
+        return g32
     _call(LAYOUT_TN, EPI_ATOMIC, dy2, N_out, x2, K_in, g32, K_in, N_out, K_in, T, splits=splits,
           variant=variant)
     return g32

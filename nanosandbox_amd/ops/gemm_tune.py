@@ -70,6 +70,11 @@ def _save():
 
 
 WGRAD_ALLOW_BF16 = os.environ.get("NSA_WGRAD_ALLOW_BF16", "0") == "1"
+# Deterministic mode (config key ``deterministic``, ops.set_deterministic): weight
+# gradients reduce their K splits in a fixed order (no fp32 atomics) and the library
+# GEMM is left out of the weight-gradient race (its split-K reduction order is not ours
+# to pin); the embedding backward switches to its sorted, atomic-free kernel.
+DETERMINISTIC = False
 NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
 WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
 
@@ -307,7 +312,10 @@ def wgrad_acc(dy2, x2, g32):
     K = x2.shape[1]
     ok = _nsa_ok(dy2, x2, g32) and T % 64 == 0 and N % 8 == 0 and K % 8 == 0
     if not ok:
-        _hip_wgrad(dy2, x2, g32)
+        if DETERMINISTIC:
+            g32.add_(dy2.t().float() @ x2.float())  # plain fp32 GEMM, then one add
+        else:
+            _hip_wgrad(dy2, x2, g32)
         return
     scratch = None
 
@@ -319,6 +327,18 @@ def wgrad_acc(dy2, x2, g32):
             fn(dy2, x2, scratch)
         return run
 
+    if DETERMINISTIC:
+        # same kernels and split counts, partials reduced in split order
+        sdef = _gemm.wgrad_splits(N, K, T)
+        tiles = -(-N // _gemm.TILE) * -(-K // _gemm.TILE)
+        splits = {sdef, _gemm.wgrad_splits_balanced(N, K, T)}
+        splits.update(r * 256 // tiles for r in (1, 2, 3))
+        dc = {f"det{v}/s{sb}": cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v,
+                                                                                deterministic=True))
+              for v in WGRAD_VARIANTS for sb in sorted(x for x in splits if 1 <= x <= max(1, T // _gemm.BK))}
+        name = choose(("wgrad_det", T, N, K), dc)
+        _gemm.wgrad_acc(dy2, x2, g32, splits=_splits(name), variant=_variant(name), deterministic=True)
+        return
     # every default candidate keeps dW in fp32 until it is added into the fp32
     # accumulator; the bf16-rounding library path changes gradient precision, so a
     # speed race never picks it unless asked for (NSA_WGRAD_ALLOW_BF16=1)

@@ -119,6 +119,9 @@ class Trainer:
         model.set_compute_dtype(self.compute_dtype,
                                 torch.float32 if c["fp32_residual"] else self.compute_dtype)
         model.grad_ckpt = c["grad_ckpt"]
+        from . import ops as _ops
+        _ops.set_deterministic(c["deterministic"])
+        _ops.rng_set(self.device, 0)  # this run's dropout stream starts at step 0
         print(f"number of parameters: {model.get_num_params() / 1e6:.2f}M")
 
         # ------------------------------------------- flat store + fused AdamW

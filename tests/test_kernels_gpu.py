@@ -545,3 +545,44 @@ def test_fused_mlp(kernels, fuse, monkeypatch):
     assert rel_err(x.grad, xr.grad) < 3e-2
     assert rel_err(wf.main_grad, wfr.grad) < 3e-2
     assert rel_err(wp.main_grad, wpr.grad) < 3e-2
+
+
+def test_deterministic_kernels_match_default(kernels):
+    """The atomic-free weight-gradient (fixed-order split-K) and embedding backward
+    (sorted tokens, one writer per row) agree with the default atomic kernels, and are
+    bitwise repeatable."""
+    from nanosandbox_amd.ops import gemm
+
+    torch.manual_seed(0)
+    dy = torch.randn(8192, 768, device=DEV).to(BF)
+    x = torch.randn(8192, 2304, device=DEV).to(BF)
+    ref = torch.zeros(768, 2304, device=DEV)
+    gemm.wgrad_acc(dy, x, ref, splits=9)
+    outs = []
+    for _ in range(2):
+        g = torch.zeros(768, 2304, device=DEV)
+        gemm.wgrad_acc(dy, x, g, splits=9, deterministic=True)
+        outs.append(g)
+    assert torch.equal(outs[0], outs[1])
+    assert rel_err(outs[0], ref) < 1e-5
+    assert rel_err(outs[0], dy.float().t() @ x.float()) < 1e-3
+
+    from nanosandbox_amd import ops
+
+    V, C, B, T = 97, 64, 3, 40
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    idx[:, ::3] = 5  # a heavily repeated row
+    grads = []
+    for det in (False, True, True):
+        ops.set_deterministic(det)
+        try:
+            wte = param(torch.randn(V, C, device=DEV), fused=True)
+            wpe = param(torch.randn(T, C, device=DEV), fused=True)
+            torch.manual_seed(3)
+            y = ops.embedding(idx, wte, wpe, 0.1, True, dtype=torch.float32)
+            y.backward(torch.randn_like(y))
+            grads.append((wte.main_grad.clone(), wpe.main_grad.clone()))
+        finally:
+            ops.set_deterministic(False)
+    assert torch.equal(grads[1][0], grads[2][0]) and torch.equal(grads[1][1], grads[2][1])
+    assert rel_err(grads[1][0], grads[0][0]) < 1e-5 and rel_err(grads[1][1], grads[0][1]) < 1e-6
