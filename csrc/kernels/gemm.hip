@@ -701,6 +701,225 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_ring64_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
+// Variant 11 ("w4"): the ring64 pipeline with 4 waves (one per SIMD) that each own
+// a 128x128 quarter of the 256x256 tile (8x8 accumulators = 256 registers, which
+// the compiler keeps in AGPRs: nothing but the MFMAs touches them in the loop).
+// Per 64-deep K-tile the 8-wave layout (128x64 per wave) reads
+// 8 x (128 + 64) x 128 B = 192 KiB of fragments from LDS; 4 x (128 + 128) x 128 B
+// = 128 KiB here, for the same 64 KiB of DMA writes and the same MFMA count, which
+// is what bounds the transposed-read weight-gradient layout (every fragment a pair
+// of ds_read_b64_tr_b16).  Slot protocol, swizzles and DMA geometry as ring64,
+// with 8 DMA pieces per thread and operand per slot instead of 4.
+// ---------------------------------------------------------------------------
+constexpr int W4_THREADS = 256;
+constexpr int W4_WT = 128;            // wave tile (both dims)
+constexpr int W4_F = W4_WT / 16;      // 8 fragments per dim
+
+// MFMA with its accumulator tied to one AGPR tuple (in/out operand).  With all 256
+// AGPRs holding loop-carried accumulators, the builtin's untied form lets the
+// register allocator pick a different destination and rotate the tuples back with
+// ~256 v_accvgpr moves per iteration.  The hazards the compiler does not see through
+// the asm are covered by the caller: chains start with mfma_first (no VALU
+// initialisation to wait for) and wait states precede the epilogue's reads; operand VGPRs come straight
+// from LDS reads (lgkmcnt waits are inserted for asm operands as for any use).
+__device__ __forceinline__ void mfma_tied(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// first product of a chain: accumulator operand = inline constant 0 (no VALU init)
+__device__ __forceinline__ void mfma_first(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+
+template <int EPI>
+__device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[W4_F][W4_F], char* smem, int m0, int n0,
+                                            int wm, int wn, int lane, int wave) {
+  const int lrow = lane & 15, lcol = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_ATOMIC_F32 || EPI == EPI_STORE_F32) {
+    // re-shape each 64x64 quarter of the wave tile through LDS: one 256-B row per
+    // atomic / store wave-instruction
+    __syncthreads();
+    float* ep = reinterpret_cast<float*>(smem) + wave * 64 * EP_LD;
+    float* Cz = reinterpret_cast<float*>(g.C);
+    if constexpr (EPI == EPI_STORE_F32) Cz += (int64_t)blockIdx.z * g.M * g.ldc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int hm = q >> 1, hn = q & 1;
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const f32x4 v = acc[hm * 4 + ii][hn * 4 + jj];
+          *reinterpret_cast<float4*>(ep + (16 * ii + lrow) * EP_LD + 16 * jj + lcol) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int row_base = m0 + wm * W4_WT + hm * 64;
+      const int col = n0 + wn * W4_WT + hn * 64 + lane;
+      if (col < g.N) {
+        for (int rr = 0; rr < 64; ++rr) {
+          const int row = row_base + rr;
+          if (row < g.M) {
+            if constexpr (EPI == EPI_STORE_F32)
+              Cz[(int64_t)row * g.ldc + col] = ep[rr * EP_LD + lane];
+            else
+              atomicAdd(Cz + (int64_t)row * g.ldc + col, ep[rr * EP_LD + lane]);
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else {
+    bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+#pragma unroll
+    for (int i = 0; i < W4_F; ++i) {
+      const int row = m0 + wm * W4_WT + 16 * i + lrow;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < W4_F; ++j) {
+        const int col = n0 + wn * W4_WT + 16 * j + lcol;
+        if (col >= g.N) continue;
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        const int64_t off = (int64_t)row * g.ldc + col;
+        if constexpr (EPI == EPI_DGELU) {
+          const uint2 u = *reinterpret_cast<const uint2*>(g.U + off);
+          o[0] *= gelu_grad(__uint_as_float(u.x << 16));
+          o[1] *= gelu_grad(__uint_as_float(u.x & 0xffff0000u));
+          o[2] *= gelu_grad(__uint_as_float(u.y << 16));
+          o[3] *= gelu_grad(__uint_as_float(u.y & 0xffff0000u));
+        }
+        uint2 w;
+        w.x = pack2(o[0], o[1]);
+        w.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(C + off) = w;
+        if constexpr (EPI == EPI_GELU) {
+          uint2 gv;
+          gv.x = pack2(gelu_f(__uint_as_float(w.x << 16)), gelu_f(__uint_as_float(w.x & 0xffff0000u)));
+          gv.y = pack2(gelu_f(__uint_as_float(w.y << 16)), gelu_f(__uint_as_float(w.y & 0xffff0000u)));
+          *reinterpret_cast<uint2*>(g.C2 + off) = gv;
+        }
+      }
+    }
+  }
+}
+
+template <bool A_K, bool B_K, int EPI>
+__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * R64_SLOT];  // 128 KiB (epilogue: 4 x 17 KiB)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
+  const int k_begin = kb0 * 64;
+  const int nk = ((int)blockIdx.z + 1) * nkb / (int)gridDim.z - kb0;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // per thread and slot: 8 DMA pieces of A and 8 of B (32 KiB each / 256 lanes / 16 B)
+  auto issue = [&](int s) {
+    const int k0 = k_begin + s * 64;
+    const uint32_t slot = lds0 + (uint32_t)((s & 1) * R64_SLOT);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = j * W4_THREADS + tid;
+      const uint32_t wbase = (uint32_t)((j * W4_THREADS + wave * 64) * 16);
+      const bf16_t* srcA;
+      const bf16_t* srcB;
+      if constexpr (A_K) {
+        const int row = e >> 3, c = (e & 7) ^ ((row >> 1) & 7);
+        srcA = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + c * 8;
+      } else {
+        const int row = e >> 5;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = (e & 31) ^ (2 * gg);
+        srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
+      }
+      if constexpr (B_K) {
+        const int row = e >> 3, c = (e & 7) ^ ((row >> 1) & 7);
+        srcB = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + k0 + c * 8;
+      } else {
+        const int row = e >> 5;
+        const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+        const int c = (e & 31) ^ (2 * gg);
+        srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
+      }
+      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + R64_SLOT_A + wbase));
+    }
+  };
+
+  f32x4 acc[W4_F][W4_F];  // first written by the zero-accumulator MFMAs of K-tile 0
+
+  issue(0);
+  if (nk > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  bf16x8 af[W4_F], b0[W4_F], b1[W4_F];
+#pragma unroll
+  for (int j = 0; j < W4_F; ++j) b0[j] = load_frag<B_K, BN>(smem + R64_SLOT_A, wn * W4_WT + 16 * j, 0, lane);
+#pragma unroll
+  for (int i = 0; i < W4_F; ++i) af[i] = load_frag<A_K, BM>(smem, wm * W4_WT + 16 * i, 0, lane);
+
+#define NSA_W4_PHASE(BC, BNX, TA, TB, KKN, FIRST)                                              \
+  __builtin_amdgcn_s_setprio(1);                                                             \
+  _Pragma("unroll") for (int i = 0; i < W4_F; ++i) {                                         \
+    _Pragma("unroll") for (int j = 0; j < W4_F; ++j) {                                       \
+      if (FIRST)                                                                             \
+        mfma_first(acc[i][j], BC[j], af[i]);                                                 \
+      else                                                                                   \
+        mfma_tied(acc[i][j], BC[j], af[i]);                                                  \
+    }                                                                                        \
+    if (i < W4_F / 2) { /* B early: the next phase's first row needs all of them */           \
+      BNX[2 * i] = load_frag<B_K, BN>((TB), wn * W4_WT + 32 * i, (KKN), lane);                 \
+      BNX[2 * i + 1] = load_frag<B_K, BN>((TB), wn * W4_WT + 32 * i + 16, (KKN), lane);        \
+    }                                                                                        \
+    af[i] = load_frag<A_K, BM>((TA), wm * W4_WT + 16 * i, (KKN), lane);                      \
+  }                                                                                          \
+  __builtin_amdgcn_s_setprio(0);
+
+  // the loop body is branch-free (its last two iterations are peeled): a branch
+  // between the MFMA phases makes the register allocator copy the 256 loop-carried
+  // AGPR accumulators at the loop header
+#define NSA_W4_STEP(K, WAIT, ISS, FIRST)                                                       \
+  {                                                                                          \
+    const char* ta = smem + ((K) & 1) * R64_SLOT;                                            \
+    const char* tn = smem + (((K) + 1) & 1) * R64_SLOT; /* past the end: discarded reads */  \
+    NSA_W4_PHASE(b0, b1, ta, ta + R64_SLOT_A, 1, FIRST)                                      \
+    if (WAIT) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");      \
+    if (ISS) issue((K) + 2);                                                                 \
+    NSA_W4_PHASE(b1, b0, tn, tn + R64_SLOT_A, 0, false)                                      \
+  }
+  if (nk == 1) {
+    NSA_W4_STEP(0, false, false, true)
+  } else if (nk == 2) {
+    NSA_W4_STEP(0, true, false, true)
+    NSA_W4_STEP(1, false, false, false)
+  } else {
+    NSA_W4_STEP(0, true, true, true)
+    int k = 1;
+    for (; k + 2 < nk; ++k) NSA_W4_STEP(k, true, true, false)
+    NSA_W4_STEP(k, true, false, false)
+    NSA_W4_STEP(k + 1, false, false, false)
+  }
+#undef NSA_W4_STEP
+#undef NSA_W4_PHASE
+  // last MFMA results -> VALU / LDS reads of the accumulators: 18 wait states cover the
+  // 8-pass MFMA's write latency
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  w4_epilogue<EPI>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+}
+
+// ---------------------------------------------------------------------------
 // Variants 9/10 ("p8": phase-paired, persistent).  cdna_hip_programming.md §5's
 // 256² 8-phase structure, re-derived for the GPT layouts (A K-contiguous:
 // forward NT and input-grad NN):
@@ -962,6 +1181,142 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Variants 12/13 ("w4 ring", weight-gradient layout only: A and B stored [K][rows]):
+// the w4 wave geometry fed by an NS-slot ring of 32-deep slices (NS = 4 / 5, 32 KiB
+// each), one slice per MFMA phase.  Top of phase j: wait for this wave's DMA of slice
+// j+1 (slices up to j+NS-2 may stay in flight), barrier, DMA slice j+NS-1 into the
+// slot of slice j-1 (read in phase j-2, consumed by phase j-1's MFMAs, so every wave
+// is done with it); then 64 MFMAs on slice j (registers) | fragment reads of slice j+1.
+// No lgkmcnt(0) at the barrier, and the DMA lead is NS-2 phases (2048 / 3072 MFMA
+// cycles) instead of the 2-slot ring's one 64-deep K step.
+// ---------------------------------------------------------------------------
+constexpr int W4R_SLICE = 32;
+constexpr int W4R_OPER = W4R_SLICE * BM * 2;  // 16 KiB per operand and slice
+constexpr int W4R_SLOT = 2 * W4R_OPER;
+
+template <int EPI, int NS>
+__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[NS * W4R_SLOT];
+  static_assert(NS * W4R_SLOT <= 163840 && NS * W4R_SLOT >= 4 * 64 * EP_LD * 4, "LDS budget");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = g.tiles_m * g.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  // splits own whole 64-deep blocks (as every other variant); slices are 32 deep
+  const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
+  const int k_begin = kb0 * 64;
+  const int ns = 2 * (((int)blockIdx.z + 1) * nkb / (int)gridDim.z - kb0);  // slices
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // slice s -> slot s % NS: 4 DMA pieces of A and 4 of B per thread ([32][256] rimg images)
+  auto issue = [&](int s, int slot_idx) {
+    const int k0 = k_begin + s * W4R_SLICE;
+    const uint32_t slot = lds0 + (uint32_t)(slot_idx * W4R_SLOT);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = j * W4_THREADS + tid;
+      const uint32_t wbase = (uint32_t)((j * W4_THREADS + wave * 64) * 16);
+      const int row = e >> 5;
+      const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+      const int c = (e & 31) ^ (2 * gg);
+      const bf16_t* srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
+      const bf16_t* srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
+      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + W4R_OPER + wbase));
+    }
+  };
+  // wait until at most `n` younger slices' DMA (8 pieces each) are in flight
+  auto wait_slices = [&](int n) {
+    if (n >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[W4_F][W4_F];  // first written by the zero-accumulator MFMAs of slice 0
+  const int pre = min(NS - 1, ns);
+  for (int s = 0; s < pre; ++s) issue(s, s);
+  wait_slices(pre - 1);
+  asm volatile("s_barrier" ::: "memory");
+  bf16x8 af[W4_F], b0[W4_F], b1[W4_F];
+#pragma unroll
+  for (int j = 0; j < W4_F; ++j) b0[j] = load_frag<false, BN>(smem + W4R_OPER, wn * W4_WT + 16 * j, 0, lane);
+#pragma unroll
+  for (int i = 0; i < W4_F; ++i) af[i] = load_frag<false, BM>(smem, wm * W4_WT + 16 * i, 0, lane);
+
+#define NSA_W4R_PHASE(BC, BNX, TA, FIRST)                                                       \
+  __builtin_amdgcn_s_setprio(1);                                                             \
+  _Pragma("unroll") for (int i = 0; i < W4_F; ++i) {                                         \
+    _Pragma("unroll") for (int j = 0; j < W4_F; ++j) {                                       \
+      if (FIRST)                                                                             \
+        mfma_first(acc[i][j], BC[j], af[i]);                                                 \
+      else                                                                                   \
+        mfma_tied(acc[i][j], BC[j], af[i]);                                                  \
+    }                                                                                        \
+    if (i < W4_F / 2) {                                                                      \
+      BNX[2 * i] = load_frag<false, BN>((TA) + W4R_OPER, wn * W4_WT + 32 * i, 0, lane);        \
+      BNX[2 * i + 1] = load_frag<false, BN>((TA) + W4R_OPER, wn * W4_WT + 32 * i + 16, 0, lane); \
+    }                                                                                        \
+    af[i] = load_frag<false, BM>((TA), wm * W4_WT + 16 * i, 0, lane);                        \
+  }                                                                                          \
+  __builtin_amdgcn_s_setprio(0);
+
+  // phase j: top-of-phase wait + barrier + refill, then MFMA(j) | read(j+1).  The slot
+  // of slice j+1 and the refill slot are tracked incrementally (no % NS per phase).
+  int rd = 1 % NS;   // slot of slice j+1
+  int wr = NS - 1;   // slot of slice j+NS-1 (= slot of slice j-1)
+#define NSA_W4R_TOP(J)                                                                         \
+  {                                                                                          \
+    wait_slices(max(0, min(ns - (J) - 2, NS - 3))); /* slice J+1 landed */                   \
+    asm volatile("s_barrier" ::: "memory");                                                  \
+    if ((J) + NS - 1 < ns) issue((J) + NS - 1, wr);                                          \
+  }
+#define NSA_W4R_ADV()                        \
+  {                                          \
+    rd = rd + 1 == NS ? 0 : rd + 1;          \
+    wr = wr + 1 == NS ? 0 : wr + 1;          \
+  }
+  {
+    NSA_W4R_TOP(0)
+    const char* ta = smem + rd * W4R_SLOT;
+    NSA_W4R_PHASE(b0, b1, ta, true)
+    NSA_W4R_ADV()
+  }
+  int j = 1;
+  for (; j + 1 < ns; j += 2) {
+    {
+      NSA_W4R_TOP(j)
+      const char* ta = smem + rd * W4R_SLOT;
+      NSA_W4R_PHASE(b1, b0, ta, false)
+      NSA_W4R_ADV()
+    }
+    {
+      NSA_W4R_TOP(j + 1)
+      const char* ta = smem + rd * W4R_SLOT;
+      NSA_W4R_PHASE(b0, b1, ta, false)
+      NSA_W4R_ADV()
+    }
+  }
+  if (j < ns) {
+    NSA_W4R_TOP(j)
+    const char* ta = smem + rd * W4R_SLOT;  // slice ns: garbage reads, discarded
+    NSA_W4R_PHASE(b1, b0, ta, false)
+  }
+#undef NSA_W4R_TOP
+#undef NSA_W4R_ADV
+#undef NSA_W4R_PHASE
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  w4_epilogue<EPI>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+}
+
 template <bool A_K, bool B_K, int EPI>
 hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   GemmArgs a = a0;
@@ -979,6 +1334,19 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
     }
   }
   if (variant == 9 || variant == 10) variant = 7;  // TN (weight grad): the ring64 kernel
+  if constexpr (!A_K && !B_K) {
+    if (variant == 12 || variant == 13) {
+      if (variant == 12)
+        gemm_w4r_kernel<EPI, 4><<<grid, W4_THREADS, 0, s>>>(a);
+      else
+        gemm_w4r_kernel<EPI, 5><<<grid, W4_THREADS, 0, s>>>(a);
+      return hipGetLastError();
+    }
+  }
+  if (variant == 11 || variant == 12 || variant == 13) {
+    gemm_w4_kernel<A_K, B_K, EPI><<<grid, W4_THREADS, 0, s>>>(a);
+    return hipGetLastError();
+  }
   if (variant == 1)
     gemm_ring_kernel<A_K, B_K, EPI, 4, false><<<grid, NTHREADS, 0, s>>>(a);
   else if (variant == 2)
