@@ -80,6 +80,23 @@ def dgrad(dy2, w, u=None, variant=None):
     return out
 
 
+def dgrad_t(dy2, wt, u=None, variant=None):
+    """dX = dY @ W from the cached K-contiguous transpose ``wt`` = W^T ([K_in, N_out]):
+    the forward's NT layout (ds_read_b128 fragments for both operands instead of the
+    NN layout's transposed reads); with ``u`` also multiplies by gelu'(u)."""
+    M, N = dy2.shape
+    K = wt.shape[0]
+    _check(dy2, "dy")
+    _check(wt, "wt")
+    out = torch.empty(M, K, device=dy2.device, dtype=BF16)
+    if u is not None:
+        _check(u, "u")
+        _call(LAYOUT_NT, EPI_DGELU, dy2, N, wt, N, out, K, M, K, N, U=u, variant=variant)
+    else:
+        _call(LAYOUT_NT, EPI_STORE, dy2, N, wt, N, out, K, M, K, N, variant=variant)
+    return out
+
+
 def wgrad_splits(n_out, n_in, tokens, cus=256):
     """Largest split count with at most two rounds of blocks (one 512-thread block per CU)."""
     tiles = -(-n_out // TILE) * -(-n_in // TILE)

@@ -17,7 +17,9 @@ so a fusion is used exactly where it measures faster.
 Candidate names: ``hipblaslt``, ``nsa<v>`` (our kernel, pipeline variant v of
 ``csrc/kernels/gemm.hip``: 1 = 32-deep LDS-DMA ring, 7/8 = 64-deep ring64 with
 LDS-staged / direct-store epilogue),
-``fused<v>`` (our kernel with the GELU epilogue).  Weight-gradient candidates are
+``fused<v>`` (our kernel with the GELU epilogue), ``nsat<v>`` / ``fusedt<v>`` (input
+grads on the forward's NT layout through the cached weight transpose, plain or with
+the GELU' epilogue).  Weight-gradient candidates are
 timed into a scratch buffer so the real accumulator is touched exactly once.
 ``NSA_GEMM_BACKEND=nsa|hipblaslt`` pins a backend family (tests, A/B runs).
 """
@@ -77,6 +79,10 @@ WGRAD_ALLOW_BF16 = os.environ.get("NSA_WGRAD_ALLOW_BF16", "0") == "1"
 DETERMINISTIC = False
 NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
 WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
+# input-grad candidates on the NT layout through the cached W^T (e.g. NSA_NT_VARIANTS=7,9:
+# ring64, persistent p8).  Off by default: on the GPT-2 shapes neither the plain nor the
+# GELU'-fused form ever beat hipBLASLt on the same transpose (+ the GELU kernel)
+NT_VARIANTS = tuple(int(v) for v in os.environ.get("NSA_NT_VARIANTS", "").split(",") if v)
 
 
 def _time_all(candidates: dict, rounds=3, reps=3):
@@ -223,11 +229,14 @@ def dgrad(dy2, w):
         return dy2 @ w
     cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
     cands.update({f"nsa{v}": (lambda v=v: _gemm.dgrad(dy2, w, variant=v)) for v in NSA_VARIANTS})
+    cands.update({f"nsat{v}": (lambda v=v: _gemm.dgrad_t(dy2, _wt(w), variant=v)) for v in NT_VARIANTS})
     name = choose(("dgrad", M, N, K), cands)
     if name == "hipblaslt":
         return dy2 @ w
     if name == "hipblaslt_t":
         return dy2 @ _wt(w).t()
+    if name.startswith("nsat"):
+        return _gemm.dgrad_t(dy2, _wt(w), variant=_variant(name))
     return _gemm.dgrad(dy2, w, variant=_variant(name))
 
 
@@ -287,10 +296,15 @@ def dgrad_dgelu(dy2, w, u, between=None):
 
     cands = {"split": split}
     cands.update({f"fused{v}": (lambda v=v: _gemm.dgrad(dy2, w, u=u, variant=v)) for v in NSA_VARIANTS})
+    # the same epilogue on the NT layout through the cached weight transpose
+    cands.update({f"fusedt{v}": (lambda v=v: _gemm.dgrad_t(dy2, _wt(w), u=u, variant=v)) for v in NT_VARIANTS})
     name = choose(("dgrad_dgelu", M, N, K), cands)
     if name == "split":
         return split(between)
-    du = _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
+    if name.startswith("fusedt"):
+        du = _gemm.dgrad_t(dy2, _wt(w), u=u, variant=_variant(name))
+    else:
+        du = _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
     if between is not None:
         between()
     return du
