@@ -40,6 +40,9 @@
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
+#ifndef ATTN_ORDER_DEFAULT
+#define ATTN_ORDER_DEFAULT 0
+#endif
 
 template <int D>
 struct Geo {
@@ -83,6 +86,36 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// Workgroup -> (b*H + h, tile) order; tile 0 is a kernel's heaviest (longest causal
+// range), launched first.
+//  order 0: tile-major with (b, h) fastest: every (b, h)'s heaviest tile before any
+//           lighter one, chip-wide.
+//  order 1 (XCD-grouped): the dispatcher places workgroup v on XCD v % 8, so XCD x is
+//           given a contiguous range of (b, h) and walks all tiles of one (b, h) back to
+//           back, heaviest first.  The K/V (forward, dQ) or Q/dO (dK/dV) rows those tiles
+//           all stream then come from that XCD's L2 while they are in flight together,
+//           instead of once per tile from HBM (with tile-major order the 8 tiles of a
+//           (b, h) are B*H workgroups apart and never co-resident).
+__device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& bh, int& t) {
+  const int v = blockIdx.x;
+  if (order == 0) {
+    t = v / BH;
+    bh = v % BH;
+    return;
+  }
+  const int total = n_tiles * BH;
+  const int xcd = v % 8, q = total / 8, r = total % 8;
+  const int u = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + v / 8;
+  bh = u / n_tiles;
+  t = u % n_tiles;
+}
+
+// NSA_ATTN_ORDER = 0 / 1 (see attn_order); read per launch so A/B runs can switch it
+int attn_order_env() {
+  const char* e = getenv("NSA_ATTN_ORDER");
+  return e ? (e[0] == '1') : ATTN_ORDER_DEFAULT;
+}
+
 // accumulator register i of a 32x32 tile holds row (i&3) + 8*(i>>2) + 4*h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
@@ -106,6 +139,26 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int r1, int 
 template <int W>
 __device__ __forceinline__ bf16x8 tr_frag_w(const char* tile, int r0, int r1, int col_base, int lane) {
   return tr_frag<W>(tile, r0, r1, col_base, lane);
+}
+
+// global -> LDS DMA of 16 bytes per lane (lane l writes lds_dst + 16 l); M0 saved and
+// restored around it.  Volatile asm: the compiler keeps it where it is written (it
+// neither sinks it towards a later use nor counts it in its own vmcnt bookkeeping).
+// glds16s: wave-uniform 64-bit base in SGPRs + a 32-bit per-lane byte offset (one VGPR
+// per address instead of two).
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
 }
 
 // =============================================================================
@@ -231,10 +284,15 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
 
 // workgroup = 4 waves x 32 queries; K/V tiles of 64 keys double-buffered in LDS
 // (32 KB at D = 64, so LDS admits 4 workgroups per CU; VGPRs set the occupancy).
-template <int D, bool DROP>
-__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_kernel(
+// DMA (D = 64): the next K/V tile is fetched by LDS-DMA into the idle buffer at the top
+// of the iteration.  The register-staged form (DMA = false, other head dims) is what the
+// T14 split intends, but hipcc sinks the staging loads out of the loop head into the
+// latch, right before their LDS writes (the tile compute sits in branches), so every
+// tile waited out a full global-memory round trip.
+template <int D, bool DROP, bool DMA = false>
+__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, float* __restrict__ lse_out, int B, int T, int H,
-    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
   constexpr int BN = 64;
   constexpr int TILE_BYTES = BN * D * 2;
   constexpr int CPR = D / 8;
@@ -247,8 +305,9 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_ker
   const int64_t row_stride = 3 * (int64_t)C;
   const int BH = B * H;
   const int n_qt = (T + 127) / 128;
-  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
-  const int bh = blockIdx.x % BH;
+  int bh, qt;
+  attn_order(n_qt, BH, order, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = lane >> 5, r = lane & 31;
@@ -278,25 +337,75 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? 3 : 2) void flash_fwd_ker
   const int kv_end = min(T, q0 + 128);
   const int n_tiles = (kv_end + BN - 1) / BN;
 
-  uint4 kst[CHUNKS_PER_THREAD], vst[CHUNKS_PER_THREAD];
-  NSA_FWD_STAGE_LOAD(0)
-  NSA_FWD_STAGE_WRITE(0)
-  __syncthreads();
-
-  for (int j = 0; j < n_tiles; ++j) {
-    const int cur = j & 1;
-    const int kv0 = j * BN;
-    // unconditional staging (the last iteration re-stages its own tile into the idle
-    // buffer): conditional register staging makes hipcc keep kst/vst in scratch
-    { NSA_FWD_STAGE_LOAD(min(j + 1, n_tiles - 1)) }
-    const char* kt = smem + cur * TILE_BYTES;
-    const char* vt = smem + (2 + cur) * TILE_BYTES;
-    if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
-      fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-    else if (kv0 <= q0w + 31)  // the wave's diagonal tile
-      fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-    { NSA_FWD_STAGE_WRITE(cur ^ 1) }
+  if constexpr (DMA) {
+    static_assert(D == 64, "DMA tile geometry is for D = 64");
+    // tile j -> buffer: wave w fills rows 16w .. 16w+15 of K and V (2 x 1 KiB pieces
+    // each); lane l lands at 16 l of its piece, i.e. row 16w + 8i + (l >> 3), physical
+    // chunk l & 7, so it fetches logical chunk (l & 7) ^ key(row)
+    const uint32_t lds0 =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+    const int prow = 16 * w + (lane >> 3);
+    const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+    const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
+    // per-lane byte offsets from the tile's first key row (a batch's qkv slice is
+    // T x 3C x 2 bytes, far below 4 GiB); the tile base lives in SGPRs
+    const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
+    const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
+    auto issue = [&](int jt, int buf) {
+      const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
+      uint32_t o0 = koff0, o8 = koff8;
+      if (jt * BN + BN > T) {  // ragged last tile: clamp rows to T - 1 (wave-uniform branch)
+        const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
+        o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
+        o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
+      }
+      const uint32_t kb = lds0 + (uint32_t)(buf * TILE_BYTES + 16 * w * 128);
+      const uint32_t vb = kb + 2 * TILE_BYTES;
+      glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
+      glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
+      glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
+      glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
+    };
+    asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // Q landed before the DMA
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int j = 0; j < n_tiles; ++j) {
+      const int cur = j & 1;
+      const int kv0 = j * BN;
+      // the idle buffer held tile j-1, which every wave finished at the last barrier
+      // (the final iteration re-fetches its own tile there: harmless, branch-free)
+      issue(min(j + 1, n_tiles - 1), cur ^ 1);
+      const char* kt = smem + cur * TILE_BYTES;
+      const char* vt = smem + (2 + cur) * TILE_BYTES;
+      if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+        fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+        fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    uint4 kst[CHUNKS_PER_THREAD], vst[CHUNKS_PER_THREAD];
+    NSA_FWD_STAGE_LOAD(0)
+    NSA_FWD_STAGE_WRITE(0)
+    __syncthreads();
+
+    for (int j = 0; j < n_tiles; ++j) {
+      const int cur = j & 1;
+      const int kv0 = j * BN;
+      // unconditional staging (the last iteration re-stages its own tile into the idle
+      // buffer): conditional register staging makes hipcc keep kst/vst in scratch
+      { NSA_FWD_STAGE_LOAD(min(j + 1, n_tiles - 1)) }
+      const char* kt = smem + cur * TILE_BYTES;
+      const char* vt = smem + (2 + cur) * TILE_BYTES;
+      if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+        fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+        fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      { NSA_FWD_STAGE_WRITE(cur ^ 1) }
+      __syncthreads();
+    }
   }
 
   // epilogue: O = O^T / l ; lane owns query qpos, registers hold d
@@ -898,14 +1007,6 @@ struct V2Geo {
   static constexpr int PIECES = NW == 4 ? 3 : 2;     // LDS-DMA instructions per wave per slice
 };
 
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
 __device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -1126,7 +1227,7 @@ template <int NKB, int NW, bool DROP, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
     const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
-    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
   constexpr int D = 64;
   constexpr int KPW = 32 * NKB;       // keys per wave
   constexpr int KWG = KPW * NW;       // keys per workgroup
@@ -1137,8 +1238,8 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
   const int BH = B * H;
-  const int kbw = blockIdx.x / BH;  // key blocks near 0 see the most queries: launched first
-  const int bh = blockIdx.x % BH;
+  int bh, kbw;  // key blocks near 0 see the most queries: launched first
+  attn_order((T + KWG - 1) / KWG, BH, order, bh, kbw);
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1386,7 +1487,7 @@ template <bool DROP>
 __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
     const float* __restrict__ lse, float* __restrict__ nls, float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B,
-    int T, int H, float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    int T, int H, float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
   constexpr int D = 64;
   constexpr int SLOT = 2 * DQ2_T;  // K, V
   constexpr int NS = NSA_DQ2_NS, LA = NS - 1;
@@ -1395,8 +1496,9 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
   const int64_t row_stride = 3 * (int64_t)C;
   const int BH = B * H;
   const int n_qt = (T + 127) / 128;
-  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
-  const int bh = blockIdx.x % BH;
+  int bh, qt;
+  attn_order(n_qt, BH, order, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1600,7 +1702,10 @@ __device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const 
 }
 
 template <int NS, bool DROP>
-__global__ __launch_bounds__(256, 2) void flash_fwd2_kernel(const bf16_t* __restrict__ qkv,
+#ifndef NSA_FWD2_MINW
+#define NSA_FWD2_MINW 2
+#endif
+__global__ __launch_bounds__(256, NSA_FWD2_MINW) void flash_fwd2_kernel(const bf16_t* __restrict__ qkv,
                                                                          bf16_t* __restrict__ out,
                                                                          float* __restrict__ lse_out, int B, int T,
                                                                          int H, float scale_log2,
@@ -1769,12 +1874,27 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     if (ns == 4) NSA_FWD2(4);
 #undef NSA_FWD2
   }
+  if constexpr (D == 64) {
+    // v1 with LDS-DMA K/V staging (default) | NSA_FLASH_FWD=v1r: register staging
+    const char* e = getenv("NSA_FLASH_FWD");
+    if (!(e && e[0] == 'v' && e[1] == '1' && e[2] == 'r')) {
+      if (th)
+        flash_fwd_kernel<D, true, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
+                                                                     B, T, H, scale * kLog2e, th, dscale, seed,
+                                                                     attn_order_env());
+      else
+        flash_fwd_kernel<D, false, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out,
+                                                                      (float*)lse, B, T, H, scale * kLog2e, th,
+                                                                      dscale, seed, attn_order_env());
+      return hipGetLastError();
+    }
+  }
   if (th)
     flash_fwd_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                           scale * kLog2e, th, dscale, seed);
+                                                           scale * kLog2e, th, dscale, seed, attn_order_env());
   else
     flash_fwd_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
-                                                            H, scale * kLog2e, th, dscale, seed);
+                                                            H, scale * kLog2e, th, dscale, seed, attn_order_env());
   return hipGetLastError();
 }
 
@@ -1845,12 +1965,12 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
       flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                               (const bf16_t*)o, (const float*)lse, nls, nd,
                                                               (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                              dscale, seed);
+                                                              dscale, seed, attn_order_env());
     else
       flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                                (const bf16_t*)o, (const float*)lse, nls, nd,
                                                                (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                               dscale, seed);
+                                                               dscale, seed, attn_order_env());
   } else {
     const int64_t threads = (int64_t)B * T * H * (D / 8);
     flash_bwd_pre2_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
@@ -1862,6 +1982,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   // two independent workgroups per CU), k1w8, k2w4 (2 key blocks per wave, 1 wave/SIMD).
   // A/B at B120 T1024 H12 (whole backward incl. the dQ kernel): v1 1307, k2w4 1304,
   // k1w8 1203, k1w4 1189 us.
+  const int order = attn_order_env();
   const char* g = getenv("NSA_FLASH_DKDV");
   const int geo = (g && g[0] == 'k' && g[1] == '2') ? 0 : (g && g[0] == 'k' && g[3] == '8') ? 1
                   : (g && g[0] == 'k' && g[4] == 'p') ? 3 : 2;
@@ -1871,11 +1992,11 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
     if (th)                                                                                                   \
       flash_bwd_dkdv2_kernel<NKB, NW, true, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                           \
           (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
-          dscale, seed);                                                                                      \
+          dscale, seed, order);                                                                               \
     else                                                                                                      \
       flash_bwd_dkdv2_kernel<NKB, NW, false, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                          \
           (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
-          dscale, seed);                                                                                      \
+          dscale, seed, order);                                                                               \
   } while (0)
   if (geo == 1) NSA_DKDV2(1, 8, false);
   else if (geo == 2) NSA_DKDV2(1, 4, false);
