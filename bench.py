@@ -90,6 +90,13 @@ def main():
 
     dims = {"gpt2": (12, 12, 768), "gpt2-medium": (24, 16, 1024), "gpt2-large": (36, 20, 1280),
             "gpt2-xl": (48, 25, 1600)}[args.model]
+    if args.micro_batch <= 0 and not args.grad_ckpt:
+        # HBM-sized micro-batch: the largest divisor of the per-rank batch whose activations
+        # stay resident next to the model state (utils/memory.py); 120 for GPT-2 124M / 350M
+        from nanosandbox_amd.utils.memory import choose_micro_batch
+        hbm = torch.cuda.get_device_properties(int(os.environ.get("LOCAL_RANK", "0"))).total_memory
+        args.micro_batch, _ = choose_micro_batch(dims[0], dims[2], dims[1], 50304, args.block_size,
+                                                 480 // world, hbm, fp32_residual=not args.bf16_residual)
     args.micro_batch, total_micro = batch_plan(world, args.micro_batch)
     tokens_per_micro = args.micro_batch * args.block_size
     cfg = dict(TRAIN_DEFAULTS)
@@ -178,7 +185,8 @@ def main():
                        "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
                        "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
                        "residual_dtype": "bf16" if args.bf16_residual else "fp32",
-                       "deterministic": args.deterministic},
+                       "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt)},
+            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1),
             "mfu_vs_2.5PF": round(mfu, 4),
             "loss": round(lossf, 4),
         }), flush=True)

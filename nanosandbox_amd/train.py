@@ -135,6 +135,18 @@ class Trainer:
         if init_from == "resume" and checkpoint is not None:
             self.optimizer.load_state_dict(checkpoint["optimizer"])
         checkpoint = None  # free up memory
+        # HBM plan (utils/memory.py): with parameters, gradients and optimizer state now
+        # allocated, keep every block's activations resident unless they do not fit
+        self.activation_plan = None
+        if self.device_type == "cuda" and (c["grad_ckpt"] or c["hbm_plan"]):
+            from .utils.memory import plan_grad_ckpt
+            free, _ = torch.cuda.mem_get_info(torch.device(self.device))
+            self.activation_plan = plan_grad_ckpt(
+                model.config.n_layer, model.config.n_embd, model.config.n_head, model.config.vocab_size,
+                c["batch_size"] * c["block_size"], free, fp32_residual=c["fp32_residual"], requested=c["grad_ckpt"])
+            model.grad_ckpt = self.activation_plan.grad_ckpt
+            if self.master:
+                print(self.activation_plan.describe())
         # compile=True: no Triton/Inductor on this stack; the micro-step (forward +
         # backward) is captured once as a HIP graph and replayed (runtime/hipgraph.py)
         self.graph = None
