@@ -105,6 +105,10 @@ def model_state_bytes(n_layer: int, n_embd: int, vocab_size: int, block_size: in
     return 20 * n_params
 
 
+RUNTIME_RESERVE = 8 * GiB  # HIP context, library workspaces, allocator slack: the trainer's
+# free-memory reading after model setup sits ~4 GiB below total - model state
+
+
 def choose_micro_batch(n_layer: int, n_embd: int, n_head: int, vocab_size: int, block_size: int,
                        per_rank_seqs: int, hbm_bytes: int, fp32_residual: bool = True, cap: int = 120,
                        headroom: float = 0.9) -> tuple[int, bool]:
@@ -113,8 +117,8 @@ def choose_micro_batch(n_layer: int, n_embd: int, n_head: int, vocab_size: int, 
     resident in ``hbm_bytes`` next to the model state; if even a one-sequence micro-step
     would not fit, the largest divisor whose checkpointed activations fit, with grad_ckpt.
     Larger micro-steps amortise the per-launch costs; resident beats checkpointed at any
-    micro-batch (GPT-2 1.5B: 60 resident 5124 ms/step, 120 checkpointed 6779)."""
-    budget = headroom * (hbm_bytes - model_state_bytes(n_layer, n_embd, vocab_size, block_size))
+    micro-batch (GPT-2 1.5B: 60 resident 5025-5124 ms/step, 120 checkpointed 6779)."""
+    budget = headroom * (hbm_bytes - model_state_bytes(n_layer, n_embd, vocab_size, block_size) - RUNTIME_RESERVE)
     divisors = [d for d in range(min(cap, per_rank_seqs), 0, -1) if per_rank_seqs % d == 0]
     kw = dict(n_layer=n_layer, n_embd=n_embd, n_head=n_head, vocab_size=vocab_size, fp32_residual=fp32_residual)
     for d in divisors:

@@ -48,7 +48,7 @@ def test_trainer_reports_no_plan_on_cpu(tmp_path):
 def test_choose_micro_batch_prefers_resident_over_checkpointing():
     from nanosandbox_amd.utils.memory import choose_micro_batch
 
-    hbm = 288 * 10 ** 9
+    hbm = 288 * GiB  # what the MI355X reports as total memory (309e9 bytes)
     # GPT-2 124M / 350M: the whole 120-sequence micro-step stays resident
     assert choose_micro_batch(12, 768, 12, 50304, 1024, 480, hbm) == (120, False)
     assert choose_micro_batch(24, 1024, 16, 50304, 1024, 480, hbm) == (120, False)
@@ -57,7 +57,7 @@ def test_choose_micro_batch_prefers_resident_over_checkpointing():
     # eight ranks: 60 sequences per rank, one resident micro-step
     assert choose_micro_batch(48, 1600, 25, 50304, 1024, 60, hbm) == (60, False)
     # a small device shrinks the micro-step first ...
-    assert choose_micro_batch(48, 1600, 25, 50304, 1024, 480, 48 * 10 ** 9) == (4, False)
+    assert choose_micro_batch(48, 1600, 25, 50304, 1024, 480, 48 * 10 ** 9) == (2, False)
     # ... and checkpoints only when not even one resident sequence fits
     mb, ck = choose_micro_batch(48, 1600, 25, 50304, 1024, 480, 33 * 10 ** 9)
     assert ck and 480 % mb == 0
