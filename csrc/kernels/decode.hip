@@ -1,0 +1,326 @@
+// Incremental decoding (serving path): KV-cache append and single-query attention
+// over the cache for gfx950.  nanoGPT's generate() re-runs the whole context for
+// every new token (reference sample.py -> model.generate, SURVEY.md §2.3 U-M11 /
+// U-S1); runtime/decode.py keeps per-layer K/V caches instead and replays one
+// token's forward as a HIP graph, so the position of the token being decoded lives
+// in device memory (`pos`) and every kernel here reads it there: nothing in the
+// captured step depends on a host value that changes between tokens.
+//
+// Cache layout: K and V as [B, H, Tmax, D] bf16, one 128-byte row per key at D = 64
+// (a wave reads 64 consecutive rows = 8 KiB contiguous for the scores, and one
+// 128-byte row per key for the weighted V sum).
+//
+// Attention (flash-decoding): the cache is split into 256-key chunks; workgroup
+// (b*H + h, s) scores its chunk's keys (one key per thread, q in LDS), forms the
+// chunk-local softmax (max m, sum l) and the chunk's weighted V sum o, and writes
+// (m, l, o[64]) to a workspace; a combine kernel rescales the chunks to the global
+// max.  Chunks past `pos` write an empty partial (m = -inf) and exit, so the grid is
+// fixed by Tmax (graph-safe) while the work follows the live context length.
+#include "common.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr int DA_D = 64;        // head dim of the decode-attention kernel
+constexpr int DA_CHUNK = 256;   // keys per workgroup (one per thread)
+constexpr int DA_PART = 2 + DA_D;  // m, l, o[64]
+
+__global__ __launch_bounds__(256) void kv_append_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ kc,
+                                                        bf16_t* __restrict__ vc, const int64_t* __restrict__ pos_dev,
+                                                        int pos0, int B, int S, int H, int D, int Tmax) {
+  // one thread per 16-byte chunk of a K or V row: index = (((b*S + s)*2 + kv)*H + h)*cpr + c
+  const int cpr = D / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)B * S * 2 * H * cpr;
+  if (i >= total) return;
+  const int c = (int)(i % cpr);
+  int64_t r = i / cpr;
+  const int hh = (int)(r % H);
+  r /= H;
+  const int kv = (int)(r & 1);
+  r >>= 1;
+  const int s = (int)(r % S);
+  const int b = (int)(r / S);
+  const int p = (pos_dev ? (int)*pos_dev : pos0) + s;
+  if (p < 0 || p >= Tmax) return;
+  const int C = H * D;
+  const bf16_t* src = qkv + ((int64_t)b * S + s) * 3 * C + (1 + kv) * C + hh * D + c * 8;
+  bf16_t* dst = (kv ? vc : kc) + (((int64_t)b * H + hh) * Tmax + p) * D + c * 8;
+  *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// grid (B*H, n_split), 256 threads
+// append: also store the new token's K / V rows at position pos (kc_w / vc_w alias
+// kc / vc; separate non-restrict pointers for the one write)
+__global__ __launch_bounds__(256) void decode_attn_partial_kernel(const bf16_t* __restrict__ qkv,
+                                                                  const bf16_t* __restrict__ kc,
+                                                                  const bf16_t* __restrict__ vc, bf16_t* kc_w,
+                                                                  bf16_t* vc_w, const int64_t* __restrict__ pos_dev,
+                                                                  float* __restrict__ ws, int H, int Tmax,
+                                                                  float scale_log2, int append) {
+  __shared__ float qs[DA_D];
+  __shared__ float ps[DA_CHUNK];
+  __shared__ float red[2][4];
+  __shared__ float os[4][DA_D];
+  const int bh = blockIdx.x, s = blockIdx.y, n_split = gridDim.y;
+  const int b = bh / H, hh = bh % H;
+  const int C = H * DA_D;
+  const int pos = (int)*pos_dev;  // the query's own position = the newest key
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* part = ws + ((int64_t)bh * n_split + s) * DA_PART;
+  const int k0 = s * DA_CHUNK;
+  if (k0 > pos) {  // chunk beyond the live context: empty partial
+    if (tid < DA_PART) part[tid] = tid == 0 ? -INFINITY : 0.0f;
+    return;
+  }
+  const bf16_t* qrow = qkv + (int64_t)b * 3 * C + hh * DA_D;  // q | k | v of the new token
+  if (tid < DA_D) qs[tid] = bf2f(qrow[tid]);
+  if (append && pos < k0 + DA_CHUNK && tid < 2 * (DA_D / 8)) {
+    // this chunk holds position pos: store the new token's K / V rows for later steps
+    // (this kernel itself takes them straight from qkv, so no write->read ordering)
+    const int c = tid & 7, kv = tid >> 3;
+    *reinterpret_cast<uint4*>((kv ? vc_w : kc_w) + ((int64_t)bh * Tmax + pos) * DA_D + 8 * c) =
+        *reinterpret_cast<const uint4*>(qrow + (1 + kv) * C + 8 * c);
+  }
+  __syncthreads();
+  const int key = k0 + tid;
+  const bool live = key <= pos;
+  float sc = -INFINITY;
+  if (live) {
+    const bf16_t* krow = key == pos ? qrow + C : kc + ((int64_t)bh * Tmax + key) * DA_D;
+    float acc = 0.0f;
+#pragma unroll
+    for (int c = 0; c < DA_D / 8; ++c) {
+      float kf[8];
+      load8(krow + 8 * c, kf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf(qs[8 * c + j], kf[j], acc);
+    }
+    sc = acc * scale_log2;
+  }
+  float m = wave_max(sc);
+  if (lane == 0) red[0][w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  const float p = live ? exp2f(sc - m) : 0.0f;
+  const float lw = wave_sum(p);
+  if (lane == 0) red[1][w] = lw;
+  ps[tid] = p;
+  __syncthreads();
+  // weighted V sum: wave w covers keys k0 + 64w .. +63, lane = output dim
+  const int kw0 = k0 + 64 * w;
+  const int kend = min(64, pos - kw0 + 1);          // live keys of this wave (may be <= 0)
+  const bool new_here = append && pos < kw0 + 64 && kend > 0;  // the new token is its last live key
+  const bf16_t* vrow = vc + ((int64_t)bh * Tmax + kw0) * DA_D + lane;
+  float o = 0.0f;
+  for (int j = 0; j < kend - (new_here ? 1 : 0); ++j) o = fmaf(ps[64 * w + j], bf2f(vrow[(int64_t)j * DA_D]), o);
+  if (new_here) o = fmaf(ps[64 * w + kend - 1], bf2f(qrow[2 * C + lane]), o);  // its V row from qkv
+  os[w][lane] = o;
+  __syncthreads();
+  if (tid < DA_D) part[2 + tid] = os[0][tid] + os[1][tid] + os[2][tid] + os[3][tid];
+  if (tid == 0) {
+    part[0] = m;
+    part[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// grid B*H, 64 threads: out[b, h*64 + d] = sum_s 2^(m_s - M) o_s[d] / sum_s 2^(m_s - M) l_s
+__global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __restrict__ ws,
+                                                                 bf16_t* __restrict__ out, int H, int n_split) {
+  const int bh = blockIdx.x, d = threadIdx.x;
+  const int b = bh / H, hh = bh % H;
+  const float* part = ws + (int64_t)bh * n_split * DA_PART;
+  float M = -INFINITY;
+  for (int s = 0; s < n_split; ++s) M = fmaxf(M, part[s * DA_PART]);
+  float L = 0.0f, o = 0.0f;
+  for (int s = 0; s < n_split; ++s) {
+    const float f = exp2f(part[s * DA_PART] - M);  // empty chunks: 2^-inf = 0
+    L = fmaf(f, part[s * DA_PART + 1], L);
+    o = fmaf(f, part[s * DA_PART + 2 + d], o);
+  }
+  out[(int64_t)b * H * DA_D + hh * DA_D + d] = f2bf(o / L);
+}
+
+// ---------------------------------------------------------------------------
+// Sampling (nanoGPT sample.py: logits / temperature, keep the top_k, softmax,
+// multinomial) for one row per workgroup, fully on the device so the decode graph can
+// feed the sampled token back without a host round trip (torch's topk / multinomial
+// chain is ~20 launches and its segmented sort is not graph-replay safe here).
+//  1. row max M;
+//  2. top-k threshold by radix select on the order-preserving uint32 image of the
+//     logits (four 8-bit digit passes with LDS histograms): the k-th largest key K;
+//     ties with it are kept, as with torch's `logits < v[:, [-1]]` mask;
+//  3. w_i = exp2((l_i - M) * log2(e) / temperature) for kept i, S = sum w_i;
+//  4. u = uniform * S from the counter hash (salt, b, position), and the first index
+//     whose running sum of w exceeds u (per-thread contiguous chunks + an LDS scan).
+// The chosen id is written to tok[b] and gen[b, *pos].
+// ---------------------------------------------------------------------------
+constexpr int SMP_THREADS = 1024;
+
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename T>
+__device__ __forceinline__ T block_reduce(T v, T* red, bool is_max) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const T o = __shfl_xor(v, off, 64);
+    v = is_max ? (o > v ? o : v) : v + o;
+  }
+  __syncthreads();  // red[] may still be read from the previous reduction
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  T r = red[0];
+  for (int i = 1; i < SMP_THREADS / 64; ++i) r = is_max ? (red[i] > r ? red[i] : r) : r + red[i];
+  return r;
+}
+
+__global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* __restrict__ logits, int V, int ld,
+                                                                  float scale_log2, int top_k, uint64_t salt,
+                                                                  const int64_t* __restrict__ pos,
+                                                                  int64_t* __restrict__ tok, int64_t* __restrict__ gen,
+                                                                  int gen_ld) {
+  __shared__ float redf[SMP_THREADS / 64];
+  __shared__ float scan[SMP_THREADS];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t sel_digit[2];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* row = logits + (int64_t)b * ld;
+  const int chunk = (V + SMP_THREADS - 1) / SMP_THREADS;
+  const int i0 = min(V, t * chunk), i1 = min(V, i0 + chunk);
+  float m = -INFINITY;
+  for (int i = i0; i < i1; ++i) m = fmaxf(m, row[i]);
+  m = block_reduce<float>(m, redf, true);
+  uint32_t thr = 0;  // keep everything
+  if (top_k > 0 && top_k < V) {
+    // radix select, 8 bits per pass from the top: histogram (LDS atomics) of the next
+    // digit among keys that match the prefix so far, then the digit holding the k-th
+    // largest; 4 passes over the row
+    uint32_t prefix = 0, mask = 0;
+    int remaining = top_k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int d = t; d < 256; d += SMP_THREADS) hist[d] = 0;
+      __syncthreads();
+      for (int i = i0; i < i1; ++i) {
+        const uint32_t key = fkey(row[i]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (t == 0) {
+        int acc = 0, sel = 0;
+        for (int d = 255; d >= 0; --d) {
+          if (acc + (int)hist[d] >= remaining) {
+            sel = d;
+            break;
+          }
+          acc += (int)hist[d];
+        }
+        sel_digit[0] = (uint32_t)sel;
+        sel_digit[1] = (uint32_t)(remaining - acc);
+      }
+      __syncthreads();
+      prefix |= sel_digit[0] << shift;
+      mask |= 255u << shift;
+      remaining = (int)sel_digit[1];
+      __syncthreads();  // sel_digit / hist reused by the next pass
+    }
+    thr = prefix;  // the k-th largest key (ties with it are kept)
+  }
+  float part = 0.0f;
+  for (int i = i0; i < i1; ++i) {
+    const float l = row[i];
+    if (fkey(l) >= thr) part += exp2f((l - m) * scale_log2);
+  }
+  scan[t] = part;
+  __syncthreads();
+  // inclusive scan of the per-thread sums (Hillis-Steele over 1024 entries)
+  for (int off = 1; off < SMP_THREADS; off <<= 1) {
+    const float v = t >= off ? scan[t - off] : 0.0f;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  const float total = scan[SMP_THREADS - 1];
+  const int p = (int)*pos;
+  const uint32_t h = nsa_hash(nsa_seed(salt), (uint64_t)b * 0x9E3779B97F4A7C15ull + (uint64_t)p);
+  const float u = (float)(h >> 8) * (1.0f / 16777216.0f) * total;
+  const float before = t > 0 ? scan[t - 1] : 0.0f;
+  // exactly one thread owns the crossing (u in [before, scan[t])); u >= total (rounding)
+  // falls to the last thread with mass
+  const bool mine = (u >= before && u < scan[t]) || (t == SMP_THREADS - 1 && u >= total);
+  if (mine) {
+    int pick = -1;
+    float acc = before;
+    for (int i = i0; i < i1; ++i) {
+      const float l = row[i];
+      if (fkey(l) < thr) continue;
+      acc += exp2f((l - m) * scale_log2);
+      pick = i;
+      if (acc > u) break;
+    }
+    if (pick < 0) {  // no kept element in this chunk (u >= total on the last thread): last kept overall
+      for (int i = V - 1; i >= 0; --i)
+        if (fkey(row[i]) >= thr) {
+          pick = i;
+          break;
+        }
+    }
+    tok[b] = pick;
+    gen[(int64_t)b * gen_ld + p] = pick;
+  }
+}
+
+}  // namespace
+
+// K/V rows of qkv [B, S, 3C] -> caches [B, H, Tmax, D] at positions p0 .. p0+S-1 where
+// p0 = *pos (int64 device scalar) or, with pos == NULL, the host value pos0.
+NSA_API hipError_t nsa_kv_append(const void* qkv, void* kc, void* vc, const void* pos, int pos0, int B, int S, int H,
+                                 int D, int Tmax, hipStream_t s) {
+  if (D % 8 || B < 1 || S < 1) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * S * 2 * H * (D / 8);
+  kv_append_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
+      (const bf16_t*)qkv, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)pos, pos0, B, S, H, D, Tmax);
+  return hipGetLastError();
+}
+
+// Single-query causal attention of the newest token (position *pos) over the caches.
+// qkv: [B, 1, 3C] (q | k | v); out: [B, C] bf16; ws: B*H*ceil(Tmax/256)*66 fp32.
+// append != 0: the new token's K / V are taken from qkv and stored at *pos (fused
+// kv_append); otherwise the caches must already hold position *pos.
+NSA_API hipError_t nsa_decode_attn(const void* qkv, void* kc, void* vc, const void* pos, void* ws, void* out, int B,
+                                   int H, int D, int Tmax, float scale, int append, hipStream_t s) {
+  if (D != DA_D || B < 1 || H < 1 || Tmax < 1) return hipErrorInvalidValue;
+  const int n_split = (Tmax + DA_CHUNK - 1) / DA_CHUNK;
+  decode_attn_partial_kernel<<<dim3(B * H, n_split), 256, 0, s>>>(
+      (const bf16_t*)qkv, (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)pos,
+      (float*)ws, H, Tmax, scale * 1.4426950408889634f, append);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  decode_attn_combine_kernel<<<B * H, 64, 0, s>>>((const float*)ws, (bf16_t*)out, H, n_split);
+  return hipGetLastError();
+}
+
+// Top-k / temperature sampling of logits [B, V] (fp32, row stride ld) on the device:
+// writes tok[b] and gen[b * gen_ld + *pos].  top_k <= 0 keeps every logit.
+NSA_API hipError_t nsa_sample_topk(const void* logits, int B, int V, int ld, float temperature, int top_k,
+                                   uint64_t salt, const void* pos, void* tok, void* gen, int gen_ld, hipStream_t s) {
+  if (B < 1 || V < 1 || !(temperature > 0.0f)) return hipErrorInvalidValue;
+  sample_topk_kernel<<<B, SMP_THREADS, 0, s>>>((const float*)logits, V, ld, 1.4426950408889634f / temperature, top_k,
+                                               salt, (const int64_t*)pos, (int64_t*)tok, (int64_t*)gen, gen_ld);
+  return hipGetLastError();
+}

@@ -7,13 +7,16 @@ from .functional import (  # noqa: F401
     add_layer_norm,
     attention,
     compute_weight,
+    decode_attention,
     dropout,
     embedding,
     gelu,
+    kv_append,
     layer_norm,
     layer_norm_pass,
     linear,
     lm_head_logits,
     lm_head_loss,
     mlp,
+    sample_topk_,
 )

@@ -64,6 +64,11 @@ _SIGNATURES = {
     "nsa_flash_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_flash_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                       c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
+    "nsa_kv_append": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_decode_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                        c_float, c_int, c_void_p],
+    "nsa_sample_topk": [c_void_p, c_int, c_int, c_int, c_float, c_int, c_uint64, c_void_p, c_void_p, c_void_p, c_int,
+                        c_void_p],
     "nsa_flash_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_rng_advance": [c_void_p],

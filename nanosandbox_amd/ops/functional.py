@@ -166,7 +166,8 @@ class DropoutFn(torch.autograd.Function):
         ctx.p, ctx.seed = p, seed
         if x.is_cuda:
             y = torch.empty_like(x)
-            _lib.call("nsa_dropout", _lib.ptr(x.contiguous()), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
+            xc = x.contiguous()
+            _lib.call("nsa_dropout", _lib.ptr(xc), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
             return y
         mask = _cpu_keep_mask(x.shape, p, seed)
         return x * mask / (1.0 - p)
@@ -175,7 +176,8 @@ class DropoutFn(torch.autograd.Function):
     def backward(ctx, dy):
         if dy.is_cuda:
             dx = torch.empty_like(dy)
-            _lib.call("nsa_dropout", _lib.ptr(dy.contiguous()), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
+            dyc = dy.contiguous()
+            _lib.call("nsa_dropout", _lib.ptr(dyc), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
                       _lib.stream())
             return dx, None
         mask = _cpu_keep_mask(dy.shape, ctx.p, ctx.seed)
@@ -209,9 +211,12 @@ class EmbeddingFn(torch.autograd.Function):
             assert C % 8 == 0, "embedding kernel needs n_embd % 8 == 0"
             assert dtype in (F32, BF16)
             out = torch.empty(B, T, C, device=idx.device, dtype=dtype)
+            # keep the bf16 weight copies referenced until the launch: without an optimizer's
+            # persistent shadow they are temporaries, and the caching allocator would hand
+            # the first one's block to the second before the kernel is enqueued
+            wte_c, wpe_c = compute_weight(wte, BF16), compute_weight(wpe, BF16)
             _lib.call("nsa_embedding_fwd_x32" if dtype == F32 else "nsa_embedding_fwd", _lib.ptr(idx),
-                      _lib.ptr(compute_weight(wte, BF16)), _lib.ptr(compute_weight(wpe, BF16)), _lib.ptr(out),
-                      B * T, T, C, p, seed, _lib.stream())
+                      _lib.ptr(wte_c), _lib.ptr(wpe_c), _lib.ptr(out), B * T, T, C, p, seed, _lib.stream())
             return out
         x = wte.detach()[idx] + wpe.detach()[:T].unsqueeze(0)
         if p > 0:
@@ -678,6 +683,76 @@ def attention(qkv, n_head: int, p: float, training: bool):
 
 
 # ----------------------------------------------------------------------------
+# incremental decoding: KV cache append + single-query attention over the cache
+# (runtime/decode.py; csrc/kernels/decode.hip).  Inference only (no autograd).
+# ----------------------------------------------------------------------------
+
+def kv_append(qkv, kc, vc, pos=None, pos0: int = 0):
+    """Write the K / V rows of ``qkv`` [B, S, 3C] into the caches [B, H, Tmax, D] at
+    positions p0 .. p0+S-1, p0 = ``pos`` (int64 device tensor, graph-safe) or ``pos0``."""
+    B, S, C3 = qkv.shape
+    _, H, Tmax, D = kc.shape
+    if qkv.is_cuda and qkv.dtype == BF16 and D % 8 == 0:
+        qkv = qkv.contiguous()
+        _lib.call("nsa_kv_append", _lib.ptr(qkv), _lib.ptr(kc), _lib.ptr(vc), _lib.ptr(pos), int(pos0), B, S, H, D,
+                  Tmax, _lib.stream())
+        return
+    p0 = int(pos.item()) if pos is not None else int(pos0)
+    k, v = qkv.view(B, S, 3, H, D)[:, :, 1:].permute(2, 0, 3, 1, 4)
+    kc[:, :, p0:p0 + S] = k.to(kc.dtype)
+    vc[:, :, p0:p0 + S] = v.to(vc.dtype)
+
+
+def decode_attention(qkv, kc, vc, pos, n_head: int, append: bool = False):
+    """Causal attention of the newest token (position ``pos``) over the caches:
+    qkv [B, 1, 3C] -> [B, 1, C].  ``append``: also store the token's K / V at ``pos``
+    (the fused form of ``kv_append``).  GPU (head dim 64): split-K flash-decoding
+    kernels; otherwise fp32 torch (CPU reference)."""
+    B, S, C3 = qkv.shape
+    C = C3 // 3
+    _, H, Tmax, D = kc.shape
+    scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda and qkv.dtype == BF16 and D == 64:
+        qkv = qkv.contiguous()
+        n_split = -(-Tmax // 256)
+        ws = torch.empty(B * H * n_split * (2 + D), device=qkv.device, dtype=F32)
+        out = torch.empty(B, 1, C, device=qkv.device, dtype=qkv.dtype)
+        _lib.call("nsa_decode_attn", _lib.ptr(qkv), _lib.ptr(kc), _lib.ptr(vc), _lib.ptr(pos), _lib.ptr(ws),
+                  _lib.ptr(out), B, H, D, Tmax, scale, 1 if append else 0, _lib.stream())
+        return out
+    if append:
+        kv_append(qkv, kc, vc, pos)
+    p = int(pos.item())
+    q = qkv.view(B, 3, H, D)[:, 0].float()                      # [B, H, D]
+    k = kc[:, :, :p + 1].float()                                 # [B, H, p+1, D]
+    v = vc[:, :, :p + 1].float()
+    att = torch.softmax(torch.einsum("bhd,bhkd->bhk", q, k) * scale, dim=-1)
+    y = torch.einsum("bhk,bhkd->bhd", att, v)
+    return y.reshape(B, 1, C).to(qkv.dtype)
+
+
+def sample_topk_(logits, temperature: float, top_k, salt: int, pos, tok, gen):
+    """Device-side nanoGPT sampling (logits / temperature, top-k, softmax, multinomial)
+    of logits [B, V] fp32: the drawn ids go to ``tok`` [B, 1] and ``gen[:, pos]``
+    (``pos``: int64 device scalar).  One kernel, graph-capturable; the uniform draw is a
+    counter hash of (salt, row, position), so a run is reproducible from its salt."""
+    B, V = logits.shape
+    k = 0 if top_k is None else min(int(top_k), V)
+    if logits.is_cuda:
+        lg = logits if logits.dtype == F32 and logits.stride(1) == 1 else logits.float().contiguous()
+        _lib.call("nsa_sample_topk", _lib.ptr(lg), B, V, lg.stride(0), float(temperature), k, int(salt) & (2 ** 64 - 1),
+                  _lib.ptr(pos), _lib.ptr(tok), _lib.ptr(gen), gen.stride(0), _lib.stream())
+        return
+    lg = logits.float() / temperature
+    if k > 0:
+        v, _ = torch.topk(lg, k)
+        lg = lg.masked_fill(lg < v[:, -1:], -float("Inf"))
+    nxt = torch.multinomial(torch.softmax(lg, dim=-1), num_samples=1)
+    tok.copy_(nxt.view_as(tok))
+    gen.index_copy_(1, pos, nxt)
+
+
+# ----------------------------------------------------------------------------
 # tied lm_head + cross-entropy (ignore_index=-1, mean over valid targets)
 # ----------------------------------------------------------------------------
 
@@ -700,7 +775,8 @@ class LMHeadLossFn(torch.autograd.Function):
             V = wc.shape[0]
             logits = _tune.fwd(x2.contiguous(), wc)
             row_loss = torch.empty(N, device=x.device, dtype=F32)
-            _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t.contiguous()), _lib.ptr(row_loss), N, V,
+            t = t.contiguous()
+            _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t), _lib.ptr(row_loss), N, V,
                       1 if need_grad else 0, _lib.stream())
             n_valid = (t != -1).sum().to(F32)
             loss = row_loss.sum() / n_valid
@@ -731,7 +807,8 @@ class LMHeadLossFn(torch.autograd.Function):
             # kernel): only the scaled products are rounded to bf16, not g itself
             g = g.reshape(1).contiguous()
             xs = torch.empty_like(x2)
-            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2.contiguous()), _lib.ptr(xs), _lib.ptr(g), xs.numel(),
+            x2c = x2.contiguous()
+            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2c), _lib.ptr(xs), _lib.ptr(g), xs.numel(),
                       _lib.stream())
             dx = _tune.dgrad(dlogits, wc)
             _lib.call("nsa_scale_rows_bf16", _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())

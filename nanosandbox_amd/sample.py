@@ -6,7 +6,9 @@ Loads ``<out_dir>/ckpt.pt`` (``init_from='resume'``) or GPT-2 weights from a
 local HF snapshot (``init_from='gpt2*'``).  Text codec: the dataset's
 ``meta.json``/``meta.pkl`` for char models, else tiktoken / a local HF GPT-2
 tokenizer when available, else raw token ids (``--start="11,42,7"``).
-On MI355X the forward runs the same HIP kernels as training.
+On MI355X the forward runs the same HIP kernels as training; with ``kv_cache=True``
+(default) each new token runs one position through the model against per-layer
+KV caches, replayed as a HIP graph (``runtime/decode.py``).
 """
 
 from __future__ import annotations
@@ -34,6 +36,7 @@ SAMPLE_DEFAULTS = dict(
     dtype="bfloat16",
     compile=False,
     data_dir="",
+    kv_cache=True,  # per-layer KV caches + a replayed HIP-graph decode step (runtime/decode.py); False: nanoGPT's recompute loop
 )
 
 
@@ -88,7 +91,8 @@ def main(argv=None):
     outs = []
     with torch.no_grad():
         for _ in range(c["num_samples"]):
-            y = model.generate(x, c["max_new_tokens"], temperature=c["temperature"], top_k=c["top_k"])
+            gen = model.generate_cached if c["kv_cache"] else model.generate
+            y = gen(x, c["max_new_tokens"], temperature=c["temperature"], top_k=c["top_k"])
             text = decode(y[0].tolist())
             outs.append(text)
             print(text)
