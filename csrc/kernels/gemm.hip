@@ -730,9 +730,11 @@ __device__ __forceinline__ void mfma_first(f32x4& acc, const bf16x8& a, const bf
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
 
-template <int EPI>
-__device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[W4_F][W4_F], char* smem, int m0, int n0,
+// FM_ x FN_ accumulators of 16x16 per wave (wave tile 16 FM_ x 16 FN_), 2 x 2 waves
+template <int EPI, int FM_ = W4_F, int FN_ = W4_F>
+__device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[FM_][FN_], char* smem, int m0, int n0,
                                             int wm, int wn, int lane, int wave) {
+  constexpr int WM_ = 16 * FM_, WN_ = 16 * FN_;
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
   if constexpr (EPI == EPI_ATOMIC_F32 || EPI == EPI_STORE_F32) {
     // re-shape each 64x64 quarter of the wave tile through LDS: one 256-B row per
@@ -742,8 +744,8 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[W4_F
     float* Cz = reinterpret_cast<float*>(g.C);
     if constexpr (EPI == EPI_STORE_F32) Cz += (int64_t)blockIdx.z * g.M * g.ldc;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int hm = q >> 1, hn = q & 1;
+    for (int q = 0; q < (FM_ / 4) * (FN_ / 4); ++q) {
+      const int hm = q / (FN_ / 4), hn = q % (FN_ / 4);
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -753,8 +755,8 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[W4_F
         }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      const int row_base = m0 + wm * W4_WT + hm * 64;
-      const int col = n0 + wn * W4_WT + hn * 64 + lane;
+      const int row_base = m0 + wm * WM_ + hm * 64;
+      const int col = n0 + wn * WN_ + hn * 64 + lane;
       if (col < g.N) {
         for (int rr = 0; rr < 64; ++rr) {
           const int row = row_base + rr;
@@ -772,12 +774,12 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& g, f32x4 (&acc)[W4_F
   } else {
     bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
 #pragma unroll
-    for (int i = 0; i < W4_F; ++i) {
-      const int row = m0 + wm * W4_WT + 16 * i + lrow;
+    for (int i = 0; i < FM_; ++i) {
+      const int row = m0 + wm * WM_ + 16 * i + lrow;
       if (row >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < W4_F; ++j) {
-        const int col = n0 + wn * W4_WT + 16 * j + lcol;
+      for (int j = 0; j < FN_; ++j) {
+        const int col = n0 + wn * WN_ + 16 * j + lcol;
         if (col >= g.N) continue;
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         const int64_t off = (int64_t)row * g.ldc + col;
@@ -1192,13 +1194,29 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_p8_kernel(GemmArgs g) {
 // cycles) instead of the 2-slot ring's one 64-deep K step.
 // ---------------------------------------------------------------------------
 constexpr int W4R_SLICE = 32;
-constexpr int W4R_OPER = W4R_SLICE * BM * 2;  // 16 KiB per operand and slice
-constexpr int W4R_SLOT = 2 * W4R_OPER;
 
-template <int EPI, int NS>
-__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[NS * W4R_SLOT];
-  static_assert(NS * W4R_SLOT <= 163840 && NS * W4R_SLOT >= 4 * 64 * EP_LD * 4, "LDS budget");
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Generalised to a 2 x 2 wave grid of 16 FM_ x 16 FN_ wave tiles (block tile
+// 32 FM_ x 32 FN_): variants 12 / 13 are FM_ = FN_ = 8 (one 256x256 workgroup per CU,
+// one wave per SIMD); variants 14-16 use 64- or 128-row wave tiles and small enough
+// rings that 2-3 independent workgroups share a CU, so one workgroup's barrier and
+// DMA waits run beside another's MFMAs (the flash dK/dV kernel's k1w4 geometry).
+template <int EPI, int NS, int FM_, int FN_, int MINW>
+__global__ __launch_bounds__(W4_THREADS, MINW) void gemm_w4r_kernel(GemmArgs g) {
+  constexpr int BM_ = 32 * FM_, BN_ = 32 * FN_;
+  constexpr int OPER_A = W4R_SLICE * BM_ * 2, OPER_B = W4R_SLICE * BN_ * 2;
+  constexpr int SLOT = OPER_A + OPER_B;
+  constexpr int PA = OPER_A / 16 / W4_THREADS, PB = OPER_B / 16 / W4_THREADS;  // DMA pieces per thread
+  constexpr int PIECES = PA + PB;
+  constexpr int EPI_BYTES = 4 * 64 * EP_LD * 4;  // epilogue: one 64x64 fp32 staging tile per wave
+  constexpr int SMEM = NS * SLOT > EPI_BYTES ? NS * SLOT : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  static_assert(SMEM <= 163840, "LDS budget");
+  static_assert(PA >= 1 && PB >= 1 && FM_ % 4 == 0 && FN_ % 4 == 0, "geometry");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nwg = g.tiles_m * g.tiles_n;
@@ -1208,7 +1226,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
   }
   const int tm = bid / g.tiles_n, tn = bid % g.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BM_, n0 = tn * BN_;
   // splits own whole 64-deep blocks (as every other variant); slices are 32 deep
   const int nkb = g.K / 64, kb0 = (int)blockIdx.z * nkb / (int)gridDim.z;
   const int k_begin = kb0 * 64;
@@ -1216,56 +1234,66 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
-  // slice s -> slot s % NS: 4 DMA pieces of A and 4 of B per thread ([32][256] rimg images)
+  // slice s -> slot: [32][BM_] and [32][BN_] rimg images, PA + PB DMA pieces per thread
   auto issue = [&](int s, int slot_idx) {
     const int k0 = k_begin + s * W4R_SLICE;
-    const uint32_t slot = lds0 + (uint32_t)(slot_idx * W4R_SLOT);
+    const uint32_t slot = lds0 + (uint32_t)(slot_idx * SLOT);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PA; ++j) {
       const int e = j * W4_THREADS + tid;
       const uint32_t wbase = (uint32_t)((j * W4_THREADS + wave * 64) * 16);
-      const int row = e >> 5;
+      const int row = e / (BM_ / 8);
       const int gg = (row & 3) | (((row >> 3) & 1) << 2);
-      const int c = (e & 31) ^ (2 * gg);
-      const bf16_t* srcA = g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8);
-      const bf16_t* srcB = g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8);
-      glds16(srcA, __builtin_amdgcn_readfirstlane(slot + wbase));
-      glds16(srcB, __builtin_amdgcn_readfirstlane(slot + W4R_OPER + wbase));
+      const int c = (e % (BM_ / 8)) ^ (2 * gg);
+      glds16(g.A + (int64_t)(k0 + row) * g.lda + min(m0 + c * 8, g.M - 8),
+             __builtin_amdgcn_readfirstlane(slot + wbase));
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int e = j * W4_THREADS + tid;
+      const uint32_t wbase = (uint32_t)((j * W4_THREADS + wave * 64) * 16);
+      const int row = e / (BN_ / 8);
+      const int gg = (row & 3) | (((row >> 3) & 1) << 2);
+      const int c = (e % (BN_ / 8)) ^ (2 * gg);
+      glds16(g.B + (int64_t)(k0 + row) * g.ldb + min(n0 + c * 8, g.N - 8),
+             __builtin_amdgcn_readfirstlane(slot + OPER_A + wbase));
     }
   };
-  // wait until at most `n` younger slices' DMA (8 pieces each) are in flight
+  // wait until at most `n` younger slices' DMA are in flight
   auto wait_slices = [&](int n) {
-    if (n >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (n == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (n >= 3) vm_wait_n<3 * PIECES>();
+    else if (n == 2) vm_wait_n<2 * PIECES>();
+    else if (n == 1) vm_wait_n<PIECES>();
+    else vm_wait_n<0>();
   };
 
-  f32x4 acc[W4_F][W4_F];  // first written by the zero-accumulator MFMAs of slice 0
+  f32x4 acc[FM_][FN_];  // first written by the zero-accumulator MFMAs of slice 0
   const int pre = min(NS - 1, ns);
   for (int s = 0; s < pre; ++s) issue(s, s);
   wait_slices(pre - 1);
   asm volatile("s_barrier" ::: "memory");
-  bf16x8 af[W4_F], b0[W4_F], b1[W4_F];
+  bf16x8 af[FM_], b0[FN_], b1[FN_];
 #pragma unroll
-  for (int j = 0; j < W4_F; ++j) b0[j] = load_frag<false, BN>(smem + W4R_OPER, wn * W4_WT + 16 * j, 0, lane);
+  for (int j = 0; j < FN_; ++j) b0[j] = load_frag<false, BN_>(smem + OPER_A, wn * 16 * FN_ + 16 * j, 0, lane);
 #pragma unroll
-  for (int i = 0; i < W4_F; ++i) af[i] = load_frag<false, BM>(smem, wm * W4_WT + 16 * i, 0, lane);
+  for (int i = 0; i < FM_; ++i) af[i] = load_frag<false, BM_>(smem, wm * 16 * FM_ + 16 * i, 0, lane);
 
+  // B fragments of the next slice are read in the first FN_/2 rows (two per row), A
+  // fragments in place after their row's MFMAs
 #define NSA_W4R_PHASE(BC, BNX, TA, FIRST)                                                       \
   __builtin_amdgcn_s_setprio(1);                                                             \
-  _Pragma("unroll") for (int i = 0; i < W4_F; ++i) {                                         \
-    _Pragma("unroll") for (int j = 0; j < W4_F; ++j) {                                       \
+  _Pragma("unroll") for (int i = 0; i < FM_; ++i) {                                          \
+    _Pragma("unroll") for (int j = 0; j < FN_; ++j) {                                        \
       if (FIRST)                                                                             \
         mfma_first(acc[i][j], BC[j], af[i]);                                                 \
       else                                                                                   \
         mfma_tied(acc[i][j], BC[j], af[i]);                                                  \
     }                                                                                        \
-    if (i < W4_F / 2) {                                                                      \
-      BNX[2 * i] = load_frag<false, BN>((TA) + W4R_OPER, wn * W4_WT + 32 * i, 0, lane);        \
-      BNX[2 * i + 1] = load_frag<false, BN>((TA) + W4R_OPER, wn * W4_WT + 32 * i + 16, 0, lane); \
+    if (i < FN_ / 2) {                                                                       \
+      BNX[2 * i] = load_frag<false, BN_>((TA) + OPER_A, wn * 16 * FN_ + 32 * i, 0, lane);      \
+      BNX[2 * i + 1] = load_frag<false, BN_>((TA) + OPER_A, wn * 16 * FN_ + 32 * i + 16, 0, lane); \
     }                                                                                        \
-    af[i] = load_frag<false, BM>((TA), wm * W4_WT + 16 * i, 0, lane);                        \
+    af[i] = load_frag<false, BM_>((TA), wm * 16 * FM_ + 16 * i, 0, lane);                    \
   }                                                                                          \
   __builtin_amdgcn_s_setprio(0);
 
@@ -1286,7 +1314,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
   }
   {
     NSA_W4R_TOP(0)
-    const char* ta = smem + rd * W4R_SLOT;
+    const char* ta = smem + rd * SLOT;
     NSA_W4R_PHASE(b0, b1, ta, true)
     NSA_W4R_ADV()
   }
@@ -1294,27 +1322,27 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4r_kernel(GemmArgs g) {
   for (; j + 1 < ns; j += 2) {
     {
       NSA_W4R_TOP(j)
-      const char* ta = smem + rd * W4R_SLOT;
+      const char* ta = smem + rd * SLOT;
       NSA_W4R_PHASE(b1, b0, ta, false)
       NSA_W4R_ADV()
     }
     {
       NSA_W4R_TOP(j + 1)
-      const char* ta = smem + rd * W4R_SLOT;
+      const char* ta = smem + rd * SLOT;
       NSA_W4R_PHASE(b0, b1, ta, false)
       NSA_W4R_ADV()
     }
   }
   if (j < ns) {
     NSA_W4R_TOP(j)
-    const char* ta = smem + rd * W4R_SLOT;  // slice ns: garbage reads, discarded
+    const char* ta = smem + rd * SLOT;  // slice ns: garbage reads, discarded
     NSA_W4R_PHASE(b1, b0, ta, false)
   }
 #undef NSA_W4R_TOP
 #undef NSA_W4R_ADV
 #undef NSA_W4R_PHASE
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-  w4_epilogue<EPI>(g, acc, smem, m0, n0, wm, wn, lane, wave);
+  w4_epilogue<EPI, FM_, FN_>(g, acc, smem, m0, n0, wm, wn, lane, wave);
 }
 
 template <bool A_K, bool B_K, int EPI>
@@ -1335,15 +1363,22 @@ hipError_t launch(const GemmArgs& a0, int splits, int variant, hipStream_t s) {
   }
   if (variant == 9 || variant == 10) variant = 7;  // TN (weight grad): the ring64 kernel
   if constexpr (!A_K && !B_K) {
-    if (variant == 12 || variant == 13) {
-      if (variant == 12)
-        gemm_w4r_kernel<EPI, 4><<<grid, W4_THREADS, 0, s>>>(a);
-      else
-        gemm_w4r_kernel<EPI, 5><<<grid, W4_THREADS, 0, s>>>(a);
+    if (variant >= 12 && variant <= 16) {
+      // 12/13: 256x256 tiles, 4 / 5 slots; 14: 256x128, 3 slots (2 workgroups/CU);
+      // 15 / 16: 128x128, 4 / 3 slots (2/CU: the 70 KiB epilogue staging bounds it)
+      const int bm = variant <= 14 ? 256 : 128, bn = variant <= 13 ? 256 : 128;
+      a.tiles_m = (a.M + bm - 1) / bm;
+      a.tiles_n = (a.N + bn - 1) / bn;
+      const dim3 gr(a.tiles_m * a.tiles_n, 1, splits);
+      if (variant == 12) gemm_w4r_kernel<EPI, 4, 8, 8, 1><<<gr, W4_THREADS, 0, s>>>(a);
+      else if (variant == 13) gemm_w4r_kernel<EPI, 5, 8, 8, 1><<<gr, W4_THREADS, 0, s>>>(a);
+      else if (variant == 14) gemm_w4r_kernel<EPI, 3, 8, 4, 2><<<gr, W4_THREADS, 0, s>>>(a);
+      else if (variant == 15) gemm_w4r_kernel<EPI, 4, 4, 4, 2><<<gr, W4_THREADS, 0, s>>>(a);
+      else gemm_w4r_kernel<EPI, 3, 4, 4, 2><<<gr, W4_THREADS, 0, s>>>(a);
       return hipGetLastError();
     }
   }
-  if (variant == 11 || variant == 12 || variant == 13) {
+  if (variant >= 11 && variant <= 16) {  // other layouts: the 4-wave 256x256 kernel
     gemm_w4_kernel<A_K, B_K, EPI><<<grid, W4_THREADS, 0, s>>>(a);
     return hipGetLastError();
   }

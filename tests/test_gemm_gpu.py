@@ -15,7 +15,7 @@ def rel(a, b):
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
                                    (256, 256, 3072)])
-@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_fwd(kernels, M, N, K, variant):
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
@@ -29,7 +29,7 @@ def test_fwd(kernels, M, N, K, variant):
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 3072, 768), (264, 512, 200), (2048, 50304, 768)])
-@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_dgrad(kernels, M, N, K, variant):
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
@@ -49,7 +49,7 @@ def test_dgrad(kernels, M, N, K, variant):
                                           (2048, 768, 3072, 4), (1024, 50304, 768, 1),
                                           (1024, 768, 768, 3), (4096, 2304, 768, 28),  # uneven K splits
                                           (1024, 768, 768, 16)])  # one K-tile per split
-@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_wgrad_acc(kernels, T, N, K, splits, variant):
     from nanosandbox_amd.ops import gemm
     if K % 8:
@@ -63,7 +63,7 @@ def test_wgrad_acc(kernels, T, N, K, splits, variant):
     assert rel(g, ref) < 5e-3
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_asymmetric_identity(kernels, variant):
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from nanosandbox_amd.ops import gemm
