@@ -285,6 +285,95 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode linear: y[m, n] = act(sum_k x[m, k] W[n, k] + b[n]) for M <= 8 rows (the
+// decode batch), bf16 in / out, fp32 accumulation.  At these M every nn.Linear is a
+// weight stream: one kernel with the bias (and GELU) in its epilogue replaces the
+// library GEMM plus the bias-broadcast copy `addmm` issues, two launches per linear.
+// Workgroup = 8 output columns; its 4 waves split K (16-byte pieces: chunk
+// g = (it * 4 + wave) * 64 + lane covers k = 8g .. 8g+7), each lane keeps 8 x M partial
+// dot products, a butterfly (halve-and-exchange) shuffle reduction leaves each lane
+// with one (column, row) total over the wave, and the 4 waves meet in LDS.
+// ---------------------------------------------------------------------------
+template <int M, int V>
+__device__ __forceinline__ float wave_reduce_multi(float (&v)[V], int lane, int& index) {
+  // V values per lane -> lane holds the wave-wide sum of value `index`
+  int cnt = V;
+  index = 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    if (cnt > 1) {
+      const bool upper = (lane & off) != 0;
+      const int h = cnt / 2;
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        if (i < h) {
+          const float send = upper ? v[i] : v[i + h];
+          const float keep = upper ? v[i + h] : v[i];
+          v[i] = keep + __shfl_xor(send, off, 64);
+        }
+      }
+      if (upper) index += h;
+      cnt = h;
+    } else {
+      v[0] += __shfl_xor(v[0], off, 64);
+    }
+  }
+  return v[0];
+}
+
+template <int M, int ACT, bool OUTF>
+__global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ W,
+                                                   const bf16_t* __restrict__ bias, void* __restrict__ y, int rows,
+                                                   int N, int K) {
+  constexpr int NC = 8, V = NC * M;
+  __shared__ float red[4][V];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.x * NC;
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.0f;
+  const int nchunk = K / 8;
+  for (int g = w * 64 + lane; g < nchunk; g += 256) {
+    const int k = 8 * g;
+    float xf[M][8];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (m < rows) load8(x + (int64_t)m * K + k, xf[m]);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xf[m][j] = 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float wf[8];
+      load8(W + (int64_t)min(n0 + c, N - 1) * K + k, wf);
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[c * M + m] = fmaf(xf[m][j], wf[j], acc[c * M + m]);
+    }
+  }
+  int idx;
+  const float v = wave_reduce_multi<M, V>(acc, lane, idx);
+  // lanes below the last split's offset hold duplicates: the first of each group writes
+  constexpr int DUP = 64 / V;  // lanes per value
+  if ((lane & (DUP - 1)) == 0) red[w][idx] = v;
+  __syncthreads();
+  if (tid < V) {
+    const int c = tid / M, m = tid % M, n = n0 + c;
+    if (m < rows && n < N) {
+      float o = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      if (bias) o += bf2f(bias[n]);
+      if (ACT == 1) o = nsa_gelu(o);
+      if constexpr (OUTF)
+        reinterpret_cast<float*>(y)[(int64_t)m * N + n] = o;
+      else
+        reinterpret_cast<bf16_t*>(y)[(int64_t)m * N + n] = f2bf(o);
+    }
+  }
+}
+
 }  // namespace
 
 // K/V rows of qkv [B, S, 3C] -> caches [B, H, Tmax, D] at positions p0 .. p0+S-1 where
@@ -322,5 +411,32 @@ NSA_API hipError_t nsa_sample_topk(const void* logits, int B, int V, int ld, flo
   if (B < 1 || V < 1 || !(temperature > 0.0f)) return hipErrorInvalidValue;
   sample_topk_kernel<<<B, SMP_THREADS, 0, s>>>((const float*)logits, V, ld, 1.4426950408889634f / temperature, top_k,
                                                salt, (const int64_t*)pos, (int64_t*)tok, (int64_t*)gen, gen_ld);
+  return hipGetLastError();
+}
+
+// Decode-batch linear y[rows, N] = act(x[rows, K] W[N, K]^T + b), rows <= 8, K % 8 == 0;
+// act: 0 none, 1 exact-erf GELU; out_f32: y is fp32 (e.g. logits) instead of bf16.
+// bias may be NULL.
+NSA_API hipError_t nsa_gemv(const void* x, const void* W, const void* bias, void* y, int rows, int N, int K, int act,
+                            int out_f32, hipStream_t s) {
+  if (rows < 1 || rows > 8 || K % 8 || N < 1 || (act && out_f32)) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((N + 7) / 8);
+#define NSA_GEMV(MR)                                                                                        \
+  do {                                                                                                      \
+    if (act)                                                                                                \
+      gemv_kernel<MR, 1, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias, \
+                                                     y, rows, N, K);                                        \
+    else if (out_f32)                                                                                       \
+      gemv_kernel<MR, 0, true><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias,  \
+                                                    y, rows, N, K);                                         \
+    else                                                                                                    \
+      gemv_kernel<MR, 0, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias, \
+                                                     y, rows, N, K);                                        \
+  } while (0)
+  if (rows == 1) NSA_GEMV(1);
+  else if (rows == 2) NSA_GEMV(2);
+  else if (rows <= 4) NSA_GEMV(4);
+  else NSA_GEMV(8);
+#undef NSA_GEMV
   return hipGetLastError();
 }

@@ -8,6 +8,7 @@ from .functional import (  # noqa: F401
     attention,
     compute_weight,
     decode_attention,
+    decode_linear,
     dropout,
     embedding,
     gelu,

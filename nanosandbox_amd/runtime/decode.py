@@ -92,16 +92,24 @@ class Decoder:
         x, h = ops.layer_norm_pass(x, ln.weight, ln.bias, out_dtype=ln.out_dtype)
         for i, block in enumerate(blocks):
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else tr.ln_f
-            attn = block.attn
-            qkv = ops.linear(h, attn.c_attn.weight, attn.c_attn.bias)
-            if decode:  # K / V append fused into the attention kernel
+            attn, mlp = block.attn, block.mlp
+            if decode:
+                # weight-streaming linears with bias / GELU epilogues (ops.decode_linear),
+                # K / V append fused into the attention kernel
+                qkv = ops.decode_linear(h, attn.c_attn.weight, attn.c_attn.bias)
                 y = ops.decode_attention(qkv, self.kc[i], self.vc[i], self.pos, attn.n_head, append=True)
+                y = ops.decode_linear(y, attn.c_proj.weight, attn.c_proj.bias)
+                x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
+                u = ops.decode_linear(h2, mlp.c_fc.weight, mlp.c_fc.bias, gelu=True)
+                y = ops.decode_linear(u, mlp.c_proj.weight, mlp.c_proj.bias)
             else:
+                qkv = ops.linear(h, attn.c_attn.weight, attn.c_attn.bias)
                 ops.kv_append(qkv, self.kc[i], self.vc[i], None, 0)
                 y = ops.attention(qkv, attn.n_head, 0.0, False)
-            y = ops.linear(y, attn.c_proj.weight, attn.c_proj.bias)
-            x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
-            x, h = ops.add_layer_norm(x, block.mlp(h2), nxt.weight, nxt.bias)
+                y = ops.linear(y, attn.c_proj.weight, attn.c_proj.bias)
+                x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
+                y = mlp(h2)
+            x, h = ops.add_layer_norm(x, y, nxt.weight, nxt.bias)
         return h  # ln_f(x)
 
     @torch.no_grad()
@@ -124,7 +132,7 @@ class Decoder:
         x = wte.index_select(0, self.tok.view(-1)).float() + wpe.index_select(0, self.pos).float()
         x = x.to(self.rdtype).view(self.B, 1, -1)
         h = self._layers(x, decode=True)
-        logits = ops.lm_head_logits(h, self.model.lm_head.weight)[:, 0]
+        logits = ops.decode_linear(h, self.model.lm_head.weight, out_f32=True)[:, 0]
         self.pos.add_(1)
         return logits
 

@@ -148,3 +148,29 @@ def test_device_sampling_distribution(kernels, top_k, temperature):
         assert counts[p == 0].sum() == 0  # nothing outside the top-k
     tv = 0.5 * (freq - p).abs().sum().item()
     assert tv < 0.03, tv
+
+
+@pytest.mark.parametrize("rows", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("N,K,bias,gelu,f32", [(768, 768, True, False, False), (3072, 768, True, True, False),
+                                              (768, 3072, False, False, False), (50304, 768, False, False, True),
+                                              (4800, 1600, True, False, False), (100, 64, True, True, False)])
+def test_decode_linear_kernel(kernels, monkeypatch, rows, N, K, bias, gelu, f32):
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional
+    import torch.nn.functional as F
+
+    monkeypatch.setattr(functional, "GEMV_MAX_ROWS", 8)  # exercise the kernel at every row count
+
+    torch.manual_seed(rows * 7 + N)
+    x = torch.randn(rows, 1, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF) if bias else None
+    y = ops.decode_linear(x, w, b, gelu=gelu, out_f32=f32)
+    ref = x.float().view(rows, K) @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if gelu:
+        ref = F.gelu(ref)
+    assert y.shape == (rows, 1, N) and y.dtype == (torch.float32 if f32 else BF)
+    err = ((y.float().view(rows, N) - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
