@@ -159,9 +159,11 @@ __global__ __launch_bounds__(64) void decode_attn_combine_kernel(const float* __
 // feed the sampled token back without a host round trip (torch's topk / multinomial
 // chain is ~20 launches and its segmented sort is not graph-replay safe here).
 //  1. row max M;
-//  2. top-k threshold by radix select on the order-preserving uint32 image of the
-//     logits (four 8-bit digit passes with LDS histograms): the k-th largest key K;
-//     ties with it are kept, as with torch's `logits < v[:, [-1]]` mask;
+//  2. top-k threshold: bisection over the order-preserving uint32 image of the logits
+//     (held in registers: a 1024-thread workgroup keeps up to 52 per thread), the
+//     k-th largest key K; ties with it are kept, as with torch's `logits < v[:, [-1]]`
+//     mask (an LDS-atomic radix select measured 156 us at V = 50304: one hot bin per
+//     digit pass serialises the atomics);
 //  3. w_i = exp2((l_i - M) * log2(e) / temperature) for kept i, S = sum w_i;
 //  4. u = uniform * S from the counter hash (salt, b, position), and the first index
 //     whose running sum of w exceeds u (per-thread contiguous chunks + an LDS scan).
@@ -172,6 +174,9 @@ constexpr int SMP_THREADS = 1024;
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_val(uint32_t k) {  // inverse of fkey
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
 template <typename T>
@@ -190,62 +195,54 @@ __device__ __forceinline__ T block_reduce(T v, T* red, bool is_max) {
   return r;
 }
 
+constexpr int SMP_MAXC = 52;  // logits per thread kept in registers (V <= 53248: the GPT-2 vocab is 50304)
+
 __global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* __restrict__ logits, int V, int ld,
                                                                   float scale_log2, int top_k, uint64_t salt,
                                                                   const int64_t* __restrict__ pos,
                                                                   int64_t* __restrict__ tok, int64_t* __restrict__ gen,
                                                                   int gen_ld) {
-  __shared__ float redf[SMP_THREADS / 64];
+  __shared__ uint32_t redu[SMP_THREADS / 64];
   __shared__ float scan[SMP_THREADS];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t sel_digit[2];
   const int b = blockIdx.x, t = threadIdx.x;
   const float* row = logits + (int64_t)b * ld;
   const int chunk = (V + SMP_THREADS - 1) / SMP_THREADS;
-  const int i0 = min(V, t * chunk), i1 = min(V, i0 + chunk);
-  float m = -INFINITY;
-  for (int i = i0; i < i1; ++i) m = fmaxf(m, row[i]);
-  m = block_reduce<float>(m, redf, true);
-  uint32_t thr = 0;  // keep everything
-  if (top_k > 0 && top_k < V) {
-    // radix select, 8 bits per pass from the top: histogram (LDS atomics) of the next
-    // digit among keys that match the prefix so far, then the digit holding the k-th
-    // largest; 4 passes over the row
-    uint32_t prefix = 0, mask = 0;
-    int remaining = top_k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int d = t; d < 256; d += SMP_THREADS) hist[d] = 0;
-      __syncthreads();
-      for (int i = i0; i < i1; ++i) {
-        const uint32_t key = fkey(row[i]);
-        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      if (t == 0) {
-        int acc = 0, sel = 0;
-        for (int d = 255; d >= 0; --d) {
-          if (acc + (int)hist[d] >= remaining) {
-            sel = d;
-            break;
-          }
-          acc += (int)hist[d];
-        }
-        sel_digit[0] = (uint32_t)sel;
-        sel_digit[1] = (uint32_t)(remaining - acc);
-      }
-      __syncthreads();
-      prefix |= sel_digit[0] << shift;
-      mask |= 255u << shift;
-      remaining = (int)sel_digit[1];
-      __syncthreads();  // sel_digit / hist reused by the next pass
+  const int i0 = min(V, t * chunk), n = min(V, i0 + chunk) - i0;
+  // the thread's contiguous chunk stays in registers (as order-preserving keys; key 0 =
+  // padding, below every real key) for every pass below
+  uint32_t key[SMP_MAXC];
+  uint32_t kmax = 0, kmin = 0xffffffffu;
+#pragma unroll
+  for (int j = 0; j < SMP_MAXC; ++j) {
+    key[j] = j < n ? fkey(row[i0 + j]) : 0u;
+    if (j < n) {
+      kmax = max(kmax, key[j]);
+      kmin = min(kmin, key[j]);
     }
-    thr = prefix;  // the k-th largest key (ties with it are kept)
+  }
+  kmax = block_reduce<uint32_t>(kmax, redu, true);
+  const float m = key_val(kmax);
+  uint32_t thr = 1;  // keep every real key
+  if (top_k > 0 && top_k < V) {
+    // exact k-th largest key by bisection over [key(min), key(max)]: the largest K with
+    // count(key >= K) >= k; counts from registers, one block reduction per step
+    uint32_t lo = ~block_reduce<uint32_t>(~kmin, redu, true), hi = kmax;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < SMP_MAXC; ++j) c += key[j] >= mid ? 1u : 0u;
+      if (block_reduce<uint32_t>(c, redu, false) >= (uint32_t)top_k)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    thr = lo;  // the k-th largest key (ties with it are kept)
   }
   float part = 0.0f;
-  for (int i = i0; i < i1; ++i) {
-    const float l = row[i];
-    if (fkey(l) >= thr) part += exp2f((l - m) * scale_log2);
-  }
+#pragma unroll
+  for (int j = 0; j < SMP_MAXC; ++j)
+    if (key[j] >= thr) part += exp2f((key_val(key[j]) - m) * scale_log2);
   scan[t] = part;
   __syncthreads();
   // inclusive scan of the per-thread sums (Hillis-Steele over 1024 entries)
@@ -266,12 +263,14 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* _
   if (mine) {
     int pick = -1;
     float acc = before;
-    for (int i = i0; i < i1; ++i) {
-      const float l = row[i];
-      if (fkey(l) < thr) continue;
-      acc += exp2f((l - m) * scale_log2);
-      pick = i;
-      if (acc > u) break;
+    bool done = false;
+#pragma unroll
+    for (int j = 0; j < SMP_MAXC; ++j) {
+      if (!done && key[j] >= thr) {
+        acc += exp2f((key_val(key[j]) - m) * scale_log2);
+        pick = i0 + j;
+        done = acc > u;
+      }
     }
     if (pick < 0) {  // no kept element in this chunk (u >= total on the last thread): last kept overall
       for (int i = V - 1; i >= 0; --i)
@@ -408,7 +407,7 @@ NSA_API hipError_t nsa_decode_attn(const void* qkv, void* kc, void* vc, const vo
 // writes tok[b] and gen[b * gen_ld + *pos].  top_k <= 0 keeps every logit.
 NSA_API hipError_t nsa_sample_topk(const void* logits, int B, int V, int ld, float temperature, int top_k,
                                    uint64_t salt, const void* pos, void* tok, void* gen, int gen_ld, hipStream_t s) {
-  if (B < 1 || V < 1 || !(temperature > 0.0f)) return hipErrorInvalidValue;
+  if (B < 1 || V < 1 || V > SMP_THREADS * SMP_MAXC || !(temperature > 0.0f)) return hipErrorInvalidValue;
   sample_topk_kernel<<<B, SMP_THREADS, 0, s>>>((const float*)logits, V, ld, 1.4426950408889634f / temperature, top_k,
                                                salt, (const int64_t*)pos, (int64_t*)tok, (int64_t*)gen, gen_ld);
   return hipGetLastError();
