@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import math
 import os
+from typing import NamedTuple
 
 import torch
 import torch.nn.functional as F
@@ -703,11 +704,21 @@ def kv_append(qkv, kc, vc, pos=None, pos0: int = 0):
     vc[:, :, p0:p0 + S] = v.to(vc.dtype)
 
 
-def decode_attention(qkv, kc, vc, pos, n_head: int, append: bool = False):
+class AttnPartials(NamedTuple):
+    """Un-combined flash-decoding partials of one decode row (``decode_attention(...,
+    combine=False)``): (m, l, o[64]) per (head, 256-key chunk) in ``ws``.  Only
+    ``decode_linear`` consumes them: it combines the chunks in its own prologue."""
+    ws: torch.Tensor
+    n_split: int
+    C: int
+
+
+def decode_attention(qkv, kc, vc, pos, n_head: int, append: bool = False, combine: bool = True):
     """Causal attention of the newest token (position ``pos``) over the caches:
     qkv [B, 1, 3C] -> [B, 1, C].  ``append``: also store the token's K / V at ``pos``
     (the fused form of ``kv_append``).  GPU (head dim 64): split-K flash-decoding
-    kernels; otherwise fp32 torch (CPU reference)."""
+    kernels; otherwise fp32 torch (CPU reference).  ``combine=False`` with one row on the
+    GPU returns the partials (``AttnPartials``) for ``decode_linear`` to combine."""
     B, S, C3 = qkv.shape
     C = C3 // 3
     _, H, Tmax, D = kc.shape
@@ -715,11 +726,12 @@ def decode_attention(qkv, kc, vc, pos, n_head: int, append: bool = False):
     if qkv.is_cuda and qkv.dtype == BF16 and D == 64:
         qkv = qkv.contiguous()
         n_split = -(-Tmax // 256)
-        ws = torch.empty(B * H * n_split * (2 + D), device=qkv.device, dtype=F32)
-        out = torch.empty(B, 1, C, device=qkv.device, dtype=qkv.dtype)
+        ws = torch.empty(B * H * n_split * (4 + D), device=qkv.device, dtype=F32)  # (m, l, pad, o[D]) per chunk
+        partial = not combine and B == 1 and GEMV_MAX_ROWS >= 1 and C <= 8192
+        out = None if partial else torch.empty(B, 1, C, device=qkv.device, dtype=qkv.dtype)
         _lib.call("nsa_decode_attn", _lib.ptr(qkv), _lib.ptr(kc), _lib.ptr(vc), _lib.ptr(pos), _lib.ptr(ws),
                   _lib.ptr(out), B, H, D, Tmax, scale, 1 if append else 0, _lib.stream())
-        return out
+        return AttnPartials(ws, n_split, C) if partial else out
     if append:
         kv_append(qkv, kc, vc, pos)
     p = int(pos.item())
@@ -741,8 +753,14 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
     decode, HIP graph): batch 1 0.69 / 3.02 ms per token vs 0.90 / 4.70 with the library
     GEMM + bias copy; from 2 rows on the library GEMM is faster (batch 4: 1.52 vs
     < 0.9 ms at 124M), so the default cap is 1 row (``NSA_GEMV_MAX_ROWS``)."""
-    K = x.shape[-1]
     N = w.shape[0]
+    if isinstance(x, AttnPartials):  # one row; the attention combine runs in the GEMV prologue
+        y = torch.empty(N, device=x.ws.device, dtype=F32 if out_f32 else BF16)
+        _lib.call("nsa_gemv_attn", _lib.ptr(x.ws), x.n_split, _lib.ptr(compute_weight(w, BF16)),
+                  _lib.ptr(compute_weight(b, BF16) if b is not None else None), _lib.ptr(y), N, x.C,
+                  1 if gelu else 0, 1 if out_f32 else 0, _lib.stream())
+        return y.view(1, 1, N)
+    K = x.shape[-1]
     rows = x.numel() // K
     if x.is_cuda and x.dtype == BF16 and rows <= GEMV_MAX_ROWS and K % 8 == 0:
         x2 = x.reshape(rows, K).contiguous()
@@ -756,6 +774,61 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
     if gelu:
         y = GeluFn.apply(y)
     return y.float() if out_f32 else y
+
+
+def decode_linear_ln(res, branch, ln_w, ln_b, w, b=None, gelu: bool = False, out_f32: bool = False,
+                     out_dtype=None):
+    """One decode row through residual add + LayerNorm + linear:
+    s = res + branch, y = act(LN(s) @ W^T + b); returns (s, y) (s is res itself when
+    ``branch`` is None).  GPU (fp32 residual, bf16 weights, one row): one kernel that
+    recomputes the LayerNorm per workgroup (``nsa_gemv_ln``); otherwise add_layer_norm
+    + ``decode_linear`` (``out_dtype``: the LayerNorm output dtype there).  Inference only."""
+    C = res.shape[-1]
+    rows = res.numel() // C
+    if (res.is_cuda and res.dtype == F32 and rows == 1 and GEMV_MAX_ROWS >= 1 and C % 8 == 0 and C <= 8192
+            and (branch is None or branch.dtype == BF16)):
+        N = w.shape[0]
+        r2 = res.reshape(C).contiguous()
+        br = branch.reshape(C).contiguous() if branch is not None else None
+        s_out = torch.empty_like(r2) if branch is not None else None
+        lw, lb = compute_weight(ln_w, BF16), compute_weight(ln_b, BF16) if ln_b is not None else None
+        wc = compute_weight(w, BF16)
+        bc = compute_weight(b, BF16) if b is not None else None
+        y = torch.empty(N, device=res.device, dtype=F32 if out_f32 else BF16)
+        _lib.call("nsa_gemv_ln", _lib.ptr(r2), _lib.ptr(br), _lib.ptr(s_out), _lib.ptr(lw), _lib.ptr(lb), _lib.ptr(wc),
+                  _lib.ptr(bc), _lib.ptr(y), N, C, LN_EPS, 1 if gelu else 0, 1 if out_f32 else 0, _lib.stream())
+        s_new = s_out.view(res.shape) if branch is not None else res
+        return s_new, y.view(*res.shape[:-1], N)
+    if branch is None:
+        s_new, h = layer_norm_pass(res, ln_w, ln_b, out_dtype=out_dtype)
+    else:
+        s_new, h = add_layer_norm(res, branch, ln_w, ln_b, out_dtype=out_dtype)
+    return s_new, decode_linear(h, w, b, gelu=gelu, out_f32=out_f32)
+
+
+def decode_embed_linear_ln(tok, pos, wte, wpe, ln_w, ln_b, w, b=None, dtype=BF16, res_dtype=F32, out_dtype=None):
+    """First linear of a decode step with the embedding in front: x = wte[tok] + wpe[pos]
+    (rows of the ``dtype`` weight copies summed in fp32, stored as ``res_dtype``: the
+    residual stream), y = LN(x) @ W^T + b; returns (x [B, 1, C], y [B, 1, N]).  One GPU
+    kernel for a single bf16 row with an fp32 stream (``nsa_gemv_emb_ln``)."""
+    B = tok.numel()
+    C = wte.shape[1]
+    wte_c, wpe_c = compute_weight(wte, dtype), compute_weight(wpe, dtype)
+    if (tok.is_cuda and B == 1 and dtype == BF16 and res_dtype == F32 and GEMV_MAX_ROWS >= 1 and C % 8 == 0
+            and C <= 8192):
+        N = w.shape[0]
+        x = torch.empty(1, 1, C, device=tok.device, dtype=F32)
+        y = torch.empty(N, device=tok.device, dtype=BF16)
+        lw, lb = compute_weight(ln_w, BF16), compute_weight(ln_b, BF16) if ln_b is not None else None
+        wc = compute_weight(w, BF16)
+        bc = compute_weight(b, BF16) if b is not None else None
+        _lib.call("nsa_gemv_emb_ln", _lib.ptr(tok), _lib.ptr(pos), _lib.ptr(wte_c), _lib.ptr(wpe_c), _lib.ptr(x),
+                  _lib.ptr(lw), _lib.ptr(lb), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y), N, C, LN_EPS, 0, 0,
+                  _lib.stream())
+        return x, y.view(1, 1, N)
+    x = wte_c.index_select(0, tok.view(-1)).float() + wpe_c.index_select(0, pos.view(-1)).float()
+    x = x.to(res_dtype).view(B, 1, C)
+    return decode_linear_ln(x, None, ln_w, ln_b, w, b, out_dtype=out_dtype)
 
 
 def sample_topk_(logits, temperature: float, top_k, salt: int, pos, tok, gen):

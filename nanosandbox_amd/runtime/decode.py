@@ -12,9 +12,10 @@ sizes a few hundred tiny kernel launches per token whose host overhead dominates
   attention over the prompt), each layer's K/V rows are written to the caches, and
   the last position's logits are returned;
 * ``step(tok)``: embedding of the new token at position ``pos`` -> per layer
-  LN -> c_attn -> append K/V -> single-query attention over the cache
-  (``ops.decode_attention``: split-K flash-decoding kernels) -> c_proj -> fused
-  residual+LN -> MLP -> ... -> ln_f -> lm_head.  ``pos`` lives in a device tensor
+  residual-add+LN+c_attn -> append K/V + single-query attention over the cache
+  (``ops.decode_attention``: split-K flash-decoding kernels) -> combine+c_proj ->
+  residual-add+LN+c_fc+GELU -> c_proj -> ... -> residual-add+ln_f+lm_head (at batch
+  1 each arrow's producer runs in the prologue of the next weight-streaming kernel).  ``pos`` lives in a device tensor
   that the step itself increments, so on the GPU the whole step is captured once
   as a ``torch.cuda.CUDAGraph`` and replayed per token (one launch per token).
 
@@ -85,7 +86,7 @@ class Decoder:
         self.sgraphs = {}
 
     # ------------------------------------------------------------------ layers
-    def _layers(self, x, decode: bool):
+    def _prefill_layers(self, x):
         tr = self.model.transformer
         blocks = tr.h
         ln = blocks[0].ln_1
@@ -93,24 +94,46 @@ class Decoder:
         for i, block in enumerate(blocks):
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else tr.ln_f
             attn, mlp = block.attn, block.mlp
-            if decode:
-                # weight-streaming linears with bias / GELU epilogues (ops.decode_linear),
-                # K / V append fused into the attention kernel
-                qkv = ops.decode_linear(h, attn.c_attn.weight, attn.c_attn.bias)
-                y = ops.decode_attention(qkv, self.kc[i], self.vc[i], self.pos, attn.n_head, append=True)
-                y = ops.decode_linear(y, attn.c_proj.weight, attn.c_proj.bias)
-                x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
-                u = ops.decode_linear(h2, mlp.c_fc.weight, mlp.c_fc.bias, gelu=True)
-                y = ops.decode_linear(u, mlp.c_proj.weight, mlp.c_proj.bias)
-            else:
-                qkv = ops.linear(h, attn.c_attn.weight, attn.c_attn.bias)
-                ops.kv_append(qkv, self.kc[i], self.vc[i], None, 0)
-                y = ops.attention(qkv, attn.n_head, 0.0, False)
-                y = ops.linear(y, attn.c_proj.weight, attn.c_proj.bias)
-                x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
-                y = mlp(h2)
+            qkv = ops.linear(h, attn.c_attn.weight, attn.c_attn.bias)
+            ops.kv_append(qkv, self.kc[i], self.vc[i], None, 0)
+            y = ops.attention(qkv, attn.n_head, 0.0, False)
+            y = ops.linear(y, attn.c_proj.weight, attn.c_proj.bias)
+            x, h2 = ops.add_layer_norm(x, y, block.ln_2.weight, block.ln_2.bias)
+            y = mlp(h2)
             x, h = ops.add_layer_norm(x, y, nxt.weight, nxt.bias)
         return h  # ln_f(x)
+
+    def _decode_layers(self):
+        """The token ``tok`` at position ``pos`` through the embedding, every block and the
+        head -> fp32 logits [B, 1, V].
+
+        Each linear's producer rides in its prologue at batch 1: the embedding and ln_1 in
+        c_attn's (``ops.decode_embed_linear_ln``), the residual add + LayerNorm in c_attn /
+        c_fc / lm_head (``ops.decode_linear_ln``), the flash-decoding combine in c_proj's
+        (``decode_attention(combine=False)`` -> ``ops.decode_linear``); the K / V append
+        rides in the attention kernel and bias / GELU in the GEMV epilogues: 5 launches
+        per layer."""
+        tr = self.model.transformer
+        branch = None  # the previous sublayer's output, not yet added to the residual x
+        for i, block in enumerate(tr.h):
+            attn, mlp = block.attn, block.mlp
+            ln1, ln2 = block.ln_1, block.ln_2
+            if i == 0:
+                x, qkv = ops.decode_embed_linear_ln(self.tok, self.pos, tr.wte.weight, tr.wpe.weight, ln1.weight,
+                                                    ln1.bias, attn.c_attn.weight, attn.c_attn.bias, dtype=self.dtype,
+                                                    res_dtype=self.rdtype, out_dtype=ln1.out_dtype)
+            else:
+                x, qkv = ops.decode_linear_ln(x, branch, ln1.weight, ln1.bias, attn.c_attn.weight, attn.c_attn.bias,
+                                              out_dtype=ln1.out_dtype)
+            y = ops.decode_attention(qkv, self.kc[i], self.vc[i], self.pos, attn.n_head, append=True, combine=False)
+            y = ops.decode_linear(y, attn.c_proj.weight, attn.c_proj.bias)
+            x, u = ops.decode_linear_ln(x, y, ln2.weight, ln2.bias, mlp.c_fc.weight, mlp.c_fc.bias, gelu=True,
+                                        out_dtype=ln2.out_dtype)
+            branch = ops.decode_linear(u, mlp.c_proj.weight, mlp.c_proj.bias)
+        lnf = tr.ln_f
+        _, logits = ops.decode_linear_ln(x, branch, lnf.weight, lnf.bias, self.model.lm_head.weight, None,
+                                         out_f32=True, out_dtype=lnf.out_dtype)
+        return logits
 
     @torch.no_grad()
     def prefill(self, idx: torch.Tensor) -> torch.Tensor:
@@ -119,20 +142,12 @@ class Decoder:
         assert B == self.B and 1 <= T0 <= self.T
         tr = self.model.transformer
         x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.rdtype)
-        h = self._layers(x, decode=False)
+        h = self._prefill_layers(x)
         self.pos.fill_(T0)
         return ops.lm_head_logits(h[:, [-1], :], self.model.lm_head.weight)[:, 0]
 
     def _step_impl(self):
-        tr = self.model.transformer
-        # the embedding kernel of the prefill / training path reads the compute-dtype
-        # weight copies: gather the same rounded rows, sum in fp32
-        wte = ops.compute_weight(tr.wte.weight, self.dtype)
-        wpe = ops.compute_weight(tr.wpe.weight, self.dtype)
-        x = wte.index_select(0, self.tok.view(-1)).float() + wpe.index_select(0, self.pos).float()
-        x = x.to(self.rdtype).view(self.B, 1, -1)
-        h = self._layers(x, decode=True)
-        logits = ops.decode_linear(h, self.model.lm_head.weight, out_f32=True)[:, 0]
+        logits = self._decode_layers()[:, 0]
         self.pos.add_(1)
         return logits
 

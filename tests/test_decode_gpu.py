@@ -174,3 +174,121 @@ def test_decode_linear_kernel(kernels, monkeypatch, rows, N, K, bias, gelu, f32)
     assert y.shape == (rows, 1, N) and y.dtype == (torch.float32 if f32 else BF)
     err = ((y.float().view(rows, N) - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("branch", [False, True])
+@pytest.mark.parametrize("N,K,bias,gelu,f32", [(2304, 768, True, False, False), (3072, 768, True, True, False),
+                                              (50304, 768, False, False, True), (6400, 1600, True, True, False),
+                                              (100, 64, False, False, False)])
+def test_decode_linear_ln_kernel(kernels, branch, N, K, bias, gelu, f32):
+    """Fused residual add + LayerNorm + GEMV (one decode row) against fp32 torch on the
+    same bf16-rounded LayerNorm output."""
+    from nanosandbox_amd import ops
+    import torch.nn.functional as F
+
+    torch.manual_seed(N + K)
+    res = torch.randn(1, 1, K, device=DEV) * 3 + 0.5
+    br = torch.randn(1, 1, K, device=DEV).to(BF) if branch else None
+    lw = (1 + 0.1 * torch.randn(K, device=DEV)).to(BF)
+    lb = (0.1 * torch.randn(K, device=DEV)).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF) if bias else None
+    s, y = ops.decode_linear_ln(res, br, lw, lb, w, b, gelu=gelu, out_f32=f32)
+    s_ref = res + br.float() if branch else res
+    assert torch.allclose(s, s_ref) and (branch or s is res)
+    h = F.layer_norm(s_ref.view(1, K), (K,), lw.float(), lb.float(), 1e-5).to(BF).float()
+    ref = h @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if gelu:
+        ref = F.gelu(ref)
+    assert y.shape == (1, 1, N) and y.dtype == (torch.float32 if f32 else BF)
+    err = ((y.float().view(1, N) - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("V,top_k", [(63, 5), (50304, 200), (50304, 1), (4096, 2000), (50304, 1024)])
+def test_device_sampling_topk_support(kernels, V, top_k):
+    """Top-k restriction on wide rows and on every kernel path (candidate compaction for
+    k <= 1024, the register bisection for larger k, the scalar-load path for V % 4 != 0):
+    every draw is one of the k largest logits; k = 1 is the argmax."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(V + top_k)
+    R = 64
+    logits = torch.randn(R, V, device=DEV) * 3.0
+    thr = torch.topk(logits, top_k, dim=1).values[:, -1:]
+    tok = torch.zeros(R, 1, dtype=torch.int64, device=DEV)
+    gen = torch.zeros(R, 4, dtype=torch.int64, device=DEV)
+    seen = set()
+    for step in range(4):
+        pos = torch.tensor([step], dtype=torch.int64, device=DEV)
+        ops.sample_topk_(logits, 0.9, top_k, 77, pos, tok, gen)
+        picked = logits.gather(1, tok)
+        assert bool((picked >= thr).all()), step
+        if top_k == 1:
+            assert torch.equal(tok[:, 0], logits.argmax(1))
+        seen.update(tok[:, 0].tolist())
+    if top_k >= 200:
+        assert len(seen) > 64  # draws spread over the kept set
+
+
+def test_device_sampling_all_ties(kernels):
+    """Equal logits: > 4096 candidates tie with the k-th largest, so the kernel takes the
+    full bisection path and (ties kept) samples uniformly over the whole row."""
+    from nanosandbox_amd import ops
+
+    V, R = 50304, 256
+    logits = torch.zeros(R, V, device=DEV)
+    tok = torch.zeros(R, 1, dtype=torch.int64, device=DEV)
+    gen = torch.zeros(R, 1, dtype=torch.int64, device=DEV)
+    ops.sample_topk_(logits, 1.0, 200, 5, torch.zeros(1, dtype=torch.int64, device=DEV), tok, gen)
+    assert int(tok.min()) >= 0 and int(tok.max()) < V
+    assert len(set(tok[:, 0].tolist())) > 200
+
+
+def test_decode_embed_linear_ln_kernel(kernels):
+    from nanosandbox_amd import ops
+    import torch.nn.functional as F
+
+    torch.manual_seed(1)
+    V, T, C, N = 512, 128, 768, 2304
+    wte = (torch.randn(V, C, device=DEV) * 0.5).to(BF)
+    wpe = (torch.randn(T, C, device=DEV) * 0.5).to(BF)
+    lw = (1 + 0.1 * torch.randn(C, device=DEV)).to(BF)
+    lb = (0.1 * torch.randn(C, device=DEV)).to(BF)
+    w = (torch.randn(N, C, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF)
+    tok = torch.tensor([[311]], device=DEV)
+    pos = torch.tensor([77], device=DEV)
+    x, y = ops.decode_embed_linear_ln(tok, pos, wte, wpe, lw, lb, w, b)
+    x_ref = wte[311].float() + wpe[77].float()
+    assert x.dtype == torch.float32 and torch.equal(x.view(C), x_ref)
+    h = F.layer_norm(x_ref.view(1, C), (C,), lw.float(), lb.float(), 1e-5).to(BF).float()
+    ref = h @ w.float().t() + b.float()
+    err = ((y.float().view(1, N) - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("pos", [0, 300, 1023])
+def test_attention_partials_into_linear(kernels, pos):
+    """decode_attention(combine=False) -> decode_linear (combine in the GEMV prologue)
+    equals the combine kernel's output through the plain GEMV."""
+    from nanosandbox_amd import ops
+
+    torch.manual_seed(pos)
+    H, D, T = 12, 64, 1024
+    C = H * D
+    kc = torch.randn(1, H, T, D, device=DEV).to(BF)
+    vc = torch.randn(1, H, T, D, device=DEV).to(BF)
+    qkv = torch.randn(1, 1, 3 * C, device=DEV).to(BF)
+    p = torch.tensor([pos], device=DEV, dtype=torch.int64)
+    w = (torch.randn(C, C, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(C, device=DEV) * 0.1).to(BF)
+    y_ref = ops.decode_linear(ops.decode_attention(qkv, kc.clone(), vc.clone(), p, H, append=True), w, b)
+    part = ops.decode_attention(qkv, kc, vc, p, H, append=True, combine=False)
+    assert isinstance(part, ops.AttnPartials)
+    y = ops.decode_linear(part, w, b)
+    assert y.shape == y_ref.shape
+    err = ((y.float() - y_ref.float()).norm() / y_ref.float().norm()).item()
+    assert err < 5e-3, err
