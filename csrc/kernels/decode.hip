@@ -599,11 +599,11 @@ __device__ __forceinline__ float wave_reduce_multi(float (&v)[V], int lane, int&
   return v[0];
 }
 
-template <int M, int ACT, bool OUTF>
+template <int M, int ACT, bool OUTF, int NC = 8>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ W,
                                                    const bf16_t* __restrict__ bias, void* __restrict__ y, int rows,
                                                    int N, int K) {
-  constexpr int NC = 8, V = NC * M;
+  constexpr int V = NC * M;
   __shared__ float red[4][V];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n0 = blockIdx.x * NC;
@@ -611,6 +611,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.0f;
   const int nchunk = K / 8;
+#pragma unroll 4
   for (int g = w * 64 + lane; g < nchunk; g += 256) {
     const int k = 8 * g;
     float xf[M][8];
@@ -677,6 +678,7 @@ struct RowPro {
   const int64_t* pos;
   const bf16_t* wte;
   const bf16_t* wpe;
+  int64_t* pos_inc;  // PRO_LN: incremented by one thread after the row (the decode step's position)
 };
 
 template <int PRO, int ACT, bool OUTF, int NC>
@@ -880,10 +882,12 @@ __global__ __launch_bounds__(256) void gemv_row_kernel(const RowPro a, const bf1
     }
     __syncthreads();  // red[] is rewritten by the next block
   }
+  if constexpr (PRO == PRO_LN)
+    if (a.pos_inc && blockIdx.x == 0 && tid == 0) *a.pos_inc += 1;
 }
 
 // NSA_GEMV_GRID: workgroup cap of the single-row GEMVs (default 1024: 4 per CU);
-// NSA_GEMV_NC: output columns per workgroup block (8 or 16)
+// NSA_GEMV_NC: output columns per workgroup block (2, 4, 8 or 16)
 int gemv_row_grid() {
   static const int g = [] {
     const char* e = getenv("NSA_GEMV_GRID");
@@ -891,12 +895,22 @@ int gemv_row_grid() {
   }();
   return g;
 }
-int gemv_row_nc() {
-  static const int n = [] {
-    const char* e = getenv("NSA_GEMV_NC");
-    return e && atoi(e) == 16 ? 16 : 8;
-  }();
-  return n;
+int env_nc(const char* name) {  // 0: unset
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v == 2 || v == 4 || v == 8 || v == 16 ? v : 0;
+}
+int gemv_row_nc() {  // default 4: measured per-token decode (graph) 124M 0.372 / 1.5B 2.065 ms at 8, 0.336 / 1.901 at 4
+  static const int n = env_nc("NSA_GEMV_NC");
+  return n ? n : 4;
+}
+
+// NSA_GEMV1_NC: columns per workgroup of the plain one-row GEMV (default 2: the narrow
+// MLP down-projection, N = C, gets C / 2 workgroups; 4 / 8 measured 1-3% slower per token)
+int gemv1_nc(int N) {
+  static const int n = env_nc("NSA_GEMV1_NC");
+  (void)N;
+  return n ? n : 2;
 }
 
 template <int PRO>
@@ -922,6 +936,10 @@ hipError_t launch_gemv_row(const RowPro& a, const void* W, const void* bias, voi
   } while (0)
   if (nc == 16)
     NSA_ROW(16);
+  else if (nc == 4)
+    NSA_ROW(4);
+  else if (nc == 2)
+    NSA_ROW(2);
   else
     NSA_ROW(8);
 #undef NSA_ROW
@@ -995,8 +1013,28 @@ NSA_API hipError_t nsa_gemv(const void* x, const void* W, const void* bias, void
       gemv_kernel<MR, 0, false><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias, \
                                                      y, rows, N, K);                                        \
   } while (0)
-  if (rows == 1) NSA_GEMV(1);
-  else if (rows == 2) NSA_GEMV(2);
+  if (rows == 1) {
+    // one row: NC columns per workgroup (narrow outputs need more, smaller workgroups to
+    // keep enough weight bytes in flight)
+    const int nc = gemv1_nc(N);
+    const unsigned g1 = (unsigned)((N + nc - 1) / nc);
+#define NSA_GEMV1(NC_)                                                                                       \
+  do {                                                                                                       \
+    if (act)                                                                                                 \
+      gemv_kernel<1, 1, false, NC_><<<g1, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias, \
+                                                       y, 1, N, K);                                          \
+    else if (out_f32)                                                                                        \
+      gemv_kernel<1, 0, true, NC_><<<g1, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias,  \
+                                                      y, 1, N, K);                                           \
+    else                                                                                                     \
+      gemv_kernel<1, 0, false, NC_><<<g1, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)bias, \
+                                                       y, 1, N, K);                                          \
+  } while (0)
+    if (nc == 2) NSA_GEMV1(2);
+    else if (nc == 4) NSA_GEMV1(4);
+    else NSA_GEMV1(8);
+#undef NSA_GEMV1
+  } else if (rows == 2) NSA_GEMV(2);
   else if (rows <= 4) NSA_GEMV(4);
   else NSA_GEMV(8);
 #undef NSA_GEMV
@@ -1005,10 +1043,11 @@ NSA_API hipError_t nsa_gemv(const void* x, const void* W, const void* bias, void
 
 // One decode row: res_out = res + branch (if branch), h = LN(res [+ branch]) with (lw, lb),
 // y = act(h W^T + bias) (fp32 y with out_f32).  K % 8 == 0, K <= 8192; res_out must not
-// alias res.
+// alias res.  pos_inc (may be NULL): an int64 the kernel increments once (the decode
+// position, advanced by the step's last kernel instead of a separate add launch).
 NSA_API hipError_t nsa_gemv_ln(const void* res, const void* branch, void* res_out, const void* lw, const void* lb,
                                const void* W, const void* bias, void* y, int N, int K, float eps, int act,
-                               int out_f32, hipStream_t s) {
+                               int out_f32, void* pos_inc, hipStream_t s) {
   if (K % 8 || K > 8192 || N < 1 || (act && out_f32) || (branch && (!res_out || res_out == res)))
     return hipErrorInvalidValue;
   RowPro a{};
@@ -1018,6 +1057,7 @@ NSA_API hipError_t nsa_gemv_ln(const void* res, const void* branch, void* res_ou
   a.lw = (const bf16_t*)lw;
   a.lb = (const bf16_t*)lb;
   a.eps = eps;
+  a.pos_inc = (int64_t*)pos_inc;
   return launch_gemv_row<PRO_LN>(a, W, bias, y, N, K, act, out_f32, s);
 }
 

@@ -74,7 +74,7 @@ _SIGNATURES = {
                         c_void_p, c_int, c_int, c_float, c_int, c_int, c_void_p],
     "nsa_gemv_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemv_ln": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                    c_float, c_int, c_int, c_void_p],
+                    c_float, c_int, c_int, c_void_p, c_void_p],
     "nsa_flash_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_rng_advance": [c_void_p],

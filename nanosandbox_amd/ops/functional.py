@@ -777,12 +777,14 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
 
 
 def decode_linear_ln(res, branch, ln_w, ln_b, w, b=None, gelu: bool = False, out_f32: bool = False,
-                     out_dtype=None):
+                     out_dtype=None, pos_inc=None):
     """One decode row through residual add + LayerNorm + linear:
     s = res + branch, y = act(LN(s) @ W^T + b); returns (s, y) (s is res itself when
     ``branch`` is None).  GPU (fp32 residual, bf16 weights, one row): one kernel that
     recomputes the LayerNorm per workgroup (``nsa_gemv_ln``); otherwise add_layer_norm
-    + ``decode_linear`` (``out_dtype``: the LayerNorm output dtype there).  Inference only."""
+    + ``decode_linear`` (``out_dtype``: the LayerNorm output dtype there).  ``pos_inc``: an
+    int64 device tensor incremented by one after the row (inside the kernel on the fused
+    path: the decode step's position update without its own launch).  Inference only."""
     C = res.shape[-1]
     rows = res.numel() // C
     if (res.is_cuda and res.dtype == F32 and rows == 1 and GEMV_MAX_ROWS >= 1 and C % 8 == 0 and C <= 8192
@@ -796,14 +798,18 @@ def decode_linear_ln(res, branch, ln_w, ln_b, w, b=None, gelu: bool = False, out
         bc = compute_weight(b, BF16) if b is not None else None
         y = torch.empty(N, device=res.device, dtype=F32 if out_f32 else BF16)
         _lib.call("nsa_gemv_ln", _lib.ptr(r2), _lib.ptr(br), _lib.ptr(s_out), _lib.ptr(lw), _lib.ptr(lb), _lib.ptr(wc),
-                  _lib.ptr(bc), _lib.ptr(y), N, C, LN_EPS, 1 if gelu else 0, 1 if out_f32 else 0, _lib.stream())
+                  _lib.ptr(bc), _lib.ptr(y), N, C, LN_EPS, 1 if gelu else 0, 1 if out_f32 else 0, _lib.ptr(pos_inc),
+                  _lib.stream())
         s_new = s_out.view(res.shape) if branch is not None else res
         return s_new, y.view(*res.shape[:-1], N)
     if branch is None:
         s_new, h = layer_norm_pass(res, ln_w, ln_b, out_dtype=out_dtype)
     else:
         s_new, h = add_layer_norm(res, branch, ln_w, ln_b, out_dtype=out_dtype)
-    return s_new, decode_linear(h, w, b, gelu=gelu, out_f32=out_f32)
+    y = decode_linear(h, w, b, gelu=gelu, out_f32=out_f32)
+    if pos_inc is not None:
+        pos_inc.add_(1)
+    return s_new, y
 
 
 def decode_embed_linear_ln(tok, pos, wte, wpe, ln_w, ln_b, w, b=None, dtype=BF16, res_dtype=F32, out_dtype=None):

@@ -132,8 +132,8 @@ class Decoder:
             branch = ops.decode_linear(u, mlp.c_proj.weight, mlp.c_proj.bias)
         lnf = tr.ln_f
         _, logits = ops.decode_linear_ln(x, branch, lnf.weight, lnf.bias, self.model.lm_head.weight, None,
-                                         out_f32=True, out_dtype=lnf.out_dtype)
-        return logits
+                                         out_f32=True, out_dtype=lnf.out_dtype, pos_inc=self.pos)
+        return logits  # pos has advanced (by the head kernel itself on the fused path)
 
     @torch.no_grad()
     def prefill(self, idx: torch.Tensor) -> torch.Tensor:
@@ -147,9 +147,7 @@ class Decoder:
         return ops.lm_head_logits(h[:, [-1], :], self.model.lm_head.weight)[:, 0]
 
     def _step_impl(self):
-        logits = self._decode_layers()[:, 0]
-        self.pos.add_(1)
-        return logits
+        return self._decode_layers()[:, 0]  # also advances pos
 
     @torch.no_grad()
     def step(self, tok: torch.Tensor) -> torch.Tensor:
