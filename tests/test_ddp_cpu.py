@@ -149,3 +149,20 @@ def test_bucket_layout_contiguous_reverse_order():
         assert e0 == s1
     names = [s.name for s in store.slots]
     assert names[0].startswith("transformer.ln_f") and names[-1] == "transformer.wte.weight"
+
+
+def test_rccl_env_presets(monkeypatch):
+    """RCCL presets fill only unset variables: xGMI (single node) sets the torch NCCL
+    knobs; the socket preset adds the reference's TCP-only transport (README.md:101)."""
+    from nanosandbox_amd.parallel import dist
+
+    for k in list(dist.XGMI_ENV) + list(dist.SOCKET_ENV):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "ens5")
+    applied = dist.rccl_env_defaults("socket")
+    assert applied["NCCL_IB_DISABLE"] == "1" and "NCCL_SOCKET_IFNAME" not in applied
+    import os
+    assert os.environ["NCCL_SOCKET_IFNAME"] == "ens5"  # an operator's setting wins
+    for k in dist.XGMI_ENV:
+        assert os.environ[k] == dist.XGMI_ENV[k]
+    assert dist.rccl_env_defaults("xgmi") == {}  # idempotent

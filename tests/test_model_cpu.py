@@ -174,3 +174,45 @@ def test_mfu_uses_mi355x_peak():
     assert fpt == pytest.approx(0.855e9, rel=0.01)
     mfu = m.estimate_mfu(12 * 40, 1.0)
     assert mfu == pytest.approx(fpt * 1024 * 480 / 2.5e15)
+
+
+def test_from_pretrained_local_snapshot(tmp_path, monkeypatch):
+    """GPT.from_pretrained reads a local HuggingFace-layout safetensors snapshot (no
+    network): Conv1D [in, out] weights are transposed into Linear layout, the rest copied,
+    lm_head stays tied to wte.  The snapshot here is synthetic (random tensors of the
+    gpt2 shapes under the HF key names)."""
+    from safetensors.torch import save_file
+
+    torch.manual_seed(0)
+    C, L, V, T = 768, 12, 50257, 1024
+    sd = {"wte.weight": torch.randn(V, C), "wpe.weight": torch.randn(T, C),
+          "ln_f.weight": torch.randn(C), "ln_f.bias": torch.randn(C)}
+    for i in range(L):
+        p = f"h.{i}."
+        sd.update({p + "ln_1.weight": torch.randn(C), p + "ln_1.bias": torch.randn(C),
+                   p + "ln_2.weight": torch.randn(C), p + "ln_2.bias": torch.randn(C),
+                   p + "attn.c_attn.weight": torch.randn(C, 3 * C), p + "attn.c_attn.bias": torch.randn(3 * C),
+                   p + "attn.c_proj.weight": torch.randn(C, C), p + "attn.c_proj.bias": torch.randn(C),
+                   p + "attn.bias": torch.ones(1, 1, T, T).tril()[:, :, :8, :8].contiguous(),
+                   p + "mlp.c_fc.weight": torch.randn(C, 4 * C), p + "mlp.c_fc.bias": torch.randn(4 * C),
+                   p + "mlp.c_proj.weight": torch.randn(4 * C, C), p + "mlp.c_proj.bias": torch.randn(C)})
+    snap = tmp_path / "gpt2"
+    snap.mkdir()
+    save_file(sd, str(snap / "model.safetensors"))
+    monkeypatch.setenv("NSA_HF_GPT2_DIR", str(tmp_path))
+    m = GPT.from_pretrained("gpt2", {"dropout": 0.1})
+    assert m.config.vocab_size == V and m.config.bias and m.config.dropout == 0.1
+    blk = m.transformer.h[3]
+    assert torch.equal(blk.attn.c_attn.weight, sd["h.3.attn.c_attn.weight"].t())
+    assert torch.equal(blk.mlp.c_proj.weight, sd["h.3.mlp.c_proj.weight"].t())
+    assert torch.equal(blk.ln_2.bias, sd["h.3.ln_2.bias"])
+    assert torch.equal(m.transformer.wpe.weight, sd["wpe.weight"])
+    assert m.lm_head.weight is m.transformer.wte.weight
+    assert torch.equal(m.lm_head.weight, sd["wte.weight"])
+
+
+def test_from_pretrained_without_snapshot_says_why(tmp_path, monkeypatch):
+    monkeypatch.setenv("NSA_HF_GPT2_DIR", str(tmp_path))
+    monkeypatch.setenv("HF_HOME", str(tmp_path))
+    with pytest.raises(FileNotFoundError, match="NSA_HF_GPT2_DIR"):
+        GPT.from_pretrained("gpt2-medium")
