@@ -430,6 +430,227 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
 #undef NSA_FWD_STAGE_WRITE
 
 // =============================================================================
+// forward v3 (D = 64): one wave = 64 queries as two independent 32-query blocks
+// against the same K/V tile.  v1 gives a wave one dependency chain per tile
+// (S MFMAs -> row max -> exp -> P·V MFMAs) and leaves the overlap to the other
+// waves of the SIMD; the PMC trace shows the waves parked on that chain (42 %
+// of wave cycles in s_waitcnt, ≈21 % MFMA busy).  Two blocks per wave give the
+// scheduler a second chain inside the wave (block A's softmax VALU beside block
+// B's S MFMAs, A's P·V beside B's exp) and halve the LDS reads per MFMA (each K
+// fragment and each transposed V fragment feeds two MFMAs).  Workgroup = 4 waves
+// = 256 queries; K/V tiles of 64 keys by LDS-DMA, double-buffered (32 KB).
+// =============================================================================
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
+                                          f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
+                                          int h, int r, int lane, float scale_log2, const DropArgs& dr) {
+  constexpr int D = 64;
+  f32x16 st[2][2];  // [block][key sub-block]
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[0][sb] = f32x16{};
+    st[1][sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
+      st[0][sb] = mfma(kf, qf[0][ks], st[0][sb]);
+      st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
+    }
+  }
+  float mt[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    mt[blk] = -INFINITY;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if constexpr (MASK) {
+          if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) st[blk][sb][i] = -INFINITY;
+        }
+        mt[blk] = fmaxf(mt[blk], st[blk][sb][i]);
+      }
+    }
+    mt[blk] = half_swap_max(mt[blk]);
+  }
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const bool grow = (mt[blk] - m_i[blk]) * scale_log2 > kDeferLog2;
+    if (__builtin_amdgcn_ballot_w64(grow)) {
+      const float m_new = grow ? mt[blk] : m_i[blk];
+      const float alpha = fast_exp2((m_i[blk] - m_new) * scale_log2);
+      l_i[blk] *= alpha;
+      m_i[blk] = m_new;
+      o[blk][0] *= alpha;
+      o[blk][1] *= alpha;
+    }
+  }
+  bf16x8 pf[2][2][2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const float mc = m_i[blk] * scale_log2;
+    float rs = 0.0f;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
+        rs += p;
+        if constexpr (DROP) {
+          const int kpos = kv0 + 32 * sb + acc_row(i, h);
+          const uint64_t id =
+              ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
+          p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
+        }
+        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
+      }
+    }
+    l_i[blk] += half_swap_sum(rs);
+  }
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
+        o[0][dt] = mfma(vf, pf[0][sb][s], o[0][dt]);
+        o[1][dt] = mfma(vf, pf[1][sb][s], o[1][dt]);
+      }
+    }
+  }
+}
+
+// NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
+// end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
+// not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
+template <bool DROP, int NS>
+__global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse_out, int B, int T, int H,
+                                                            float scale_log2, uint32_t drop_thresh, float drop_scale,
+                                                            uint64_t seed) {
+  static_assert(NS >= 2 && NS <= 4, "ring slots");
+  constexpr int D = 64;
+  constexpr int BN = 64;
+  constexpr int TILE_BYTES = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 255) / 256;
+  int bh, qt;
+  attn_order(n_qt, BH, 0, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int q0 = qt * 256;
+  const int q0w = q0 + 64 * w;  // block A = queries q0w .. q0w + 31, block B = the next 32
+  const int qposA = q0w + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
+
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int qp = qposA + 32 * blk;
+    const int qc = qp < T ? qp : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[blk][ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
+  }
+  f32x16 o[2][2];
+  float m_i[2], l_i[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    o[blk][0] = f32x16{};
+    o[blk][1] = f32x16{};
+    m_i[blk] = -1e30f;
+    l_i[blk] = 0.0f;
+  }
+
+  const int kv_end = min(T, q0 + 256);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+  // same DMA geometry as flash_fwd_kernel<64, *, true>: wave w fills rows 16w .. 16w+15
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int prow = 16 * w + (lane >> 3);
+  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
+  const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
+  const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
+  auto issue = [&](int jt, int buf) {
+    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
+    uint32_t o0 = koff0, o8 = koff8;
+    if (jt * BN + BN > T) {
+      const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
+      o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
+      o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
+    }
+    const uint32_t kb = lds0 + (uint32_t)(buf * TILE_BYTES + 16 * w * 128);
+    const uint32_t vb = kb + NS * TILE_BYTES;
+    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
+    glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
+    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
+    glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
+  };
+  // every wave issues 4 DMA pieces per tile; "tile j + 1 landed" = at most NS - 2 younger
+  // tiles' pieces outstanding (no other vector-memory op is in flight inside the loop)
+  auto wait_next = [&]() {
+    if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  };
+  asm volatile("" ::"v"(qf[0][0]), "v"(qf[0][1]), "v"(qf[0][2]), "v"(qf[0][3]), "v"(qf[1][0]), "v"(qf[1][1]),
+               "v"(qf[1][2]), "v"(qf[1][3]));  // Q landed before the DMA
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue(min(t, n_tiles - 1), t);
+  wait_next();  // tile 0 landed
+  __syncthreads();
+  for (int j = 0; j < n_tiles; ++j) {
+    const int cur = j % NS;
+    const int kv0 = j * BN;
+    // slot of tile j - 1 (finished by every wave at the last barrier); past the end the
+    // last tile is re-fetched into a slot that is never read again (branch-free count)
+    issue(min(j + NS - 1, n_tiles - 1), (j + NS - 1) % NS);
+    const char* kt = smem + cur * TILE_BYTES;
+    const char* vt = smem + (NS + cur) * TILE_BYTES;
+    if (kv0 + BN - 1 <= q0w)  // wave-uniform: every key of the tile visible to all 64 queries
+      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+    else if (kv0 <= q0w + 63)  // the wave's diagonal tile
+      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+    wait_next();
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int qp = qposA + 32 * blk;
+    if (qp < T) {
+      const float inv_l = 1.0f / l_i[blk];
+      bf16_t* orow = out + ((int64_t)b * T + qp) * C + hh * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          uint2 u;
+          u.x = pack2(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
+          u.y = pack2(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
+          *reinterpret_cast<uint2*>(orow + d) = u;
+        }
+      }
+      if (h == 0)
+        lse_out[(int64_t)bh * T + qp] = (m_i[blk] * scale_log2 + __log2f(l_i[blk])) * 0.6931471805599453f;
+    }
+  }
+}
+
+// =============================================================================
 // backward preprocessing, one pass over [B, T, C]:
 //   delta[b, h, t] = rowsum(dO * O)  (fp32)   and   dq_acc[b, t, :] = 0
 // The zeroing rides along with the delta reads (same rows, same threads), so the
@@ -1858,7 +2079,34 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // 424 us: v1's 127 VGPRs keep 4 waves per SIMD, v2's 168 three at most, and the
     // deeper ring does not buy that back (identical outputs).
     const char* e = getenv("NSA_FLASH_FWD");
-    const int ns = (!e || e[1] == '1') ? 0 : (e[3] - '0');
+    const int n_qt3 = (T + 255) / 256;
+    // default (no NSA_FLASH_FWD or "auto"): v3s4 without dropout once the grid has at least
+    // 8 rounds of 512 resident workgroups.  B120 T1024 H12 (5760 v3 workgroups): v1 377,
+    // v3s2 354, v3s3 383, v3s4 344 us (step 465.3 -> 463.9 ms); v3 halves the K/V re-reads,
+    // which pays once qkv (566 MB) no longer sits in the 256 MB Infinity Cache.  B60
+    // (2880): v1 159 vs v3 188 us; B32 T1000: v1 88 vs v3 99-108 us.  With dropout v1 (the
+    // per-element hash doubles v3's VALU chain: 109 vs 158 us at B16)
+    const bool v3_auto = (!e || e[0] == 'a') && !th && (int64_t)n_qt3 * B * H >= 4096;
+    if (v3_auto || (e && e[0] == 'v' && e[1] == '3')) {
+      // v3 = 64 queries per wave; v3s<NS> picks the K/V ring depth (default 4)
+      const int ns3 = (e && e[0] == 'v' && e[2] == 's' && e[3] >= '2' && e[3] <= '4') ? e[3] - '0' : 4;
+#define NSA_FWD3(NS)                                                                                          \
+  do {                                                                                                        \
+    if (th)                                                                                                   \
+      flash_fwd3_kernel<true, NS><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, \
+                                                                B, T, H, scale * kLog2e, th, dscale, seed);   \
+    else                                                                                                      \
+      flash_fwd3_kernel<false, NS><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out,             \
+                                                                 (float*)lse, B, T, H, scale * kLog2e, th,    \
+                                                                 dscale, seed);                               \
+    return hipGetLastError();                                                                                 \
+  } while (0)
+      if (ns3 == 2) NSA_FWD3(2);
+      if (ns3 == 3) NSA_FWD3(3);
+      NSA_FWD3(4);
+#undef NSA_FWD3
+    }
+    const int ns = (!e || e[0] != 'v' || e[1] == '1') ? 0 : (e[3] - '0');
 #define NSA_FWD2(NS)                                                                                            \
   do {                                                                                                          \
     if (th)                                                                                                     \

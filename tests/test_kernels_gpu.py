@@ -257,7 +257,7 @@ def attn_ref(qkv, H):
     return y.transpose(1, 2).reshape(B, T, C)
 
 
-@pytest.mark.parametrize("fwd", ["v2s3", "v2s2", "v2s4", "v1"])
+@pytest.mark.parametrize("fwd", ["v2s3", "v2s2", "v2s4", "v1", "v3s2", "v3s3", "v3s4", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, monkeypatch, B, T, H, D, fwd):
@@ -282,7 +282,7 @@ def test_flash_attention(kernels, monkeypatch, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v2s3", "v1"])
+@pytest.mark.parametrize("fwd", ["v2s3", "v1", "v3s4"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes"])
 def test_flash_attention_deferred_rescale(kernels, monkeypatch, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -382,7 +382,7 @@ def test_flash_bwd_split_matches_atomic(kernels, monkeypatch, p):
 
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_flash_fwd_v2_matches_v1(kernels, monkeypatch, p):
-    """Forward v2 (LDS-DMA ring, every ring depth) against v1, with and without dropout
+    """Forward v2 / v3 (LDS-DMA rings, every ring depth) against v1, with and without dropout
     (the same counter-hash mask): outputs and LSE-dependent gradients agree."""
     from nanosandbox_amd.ops import functional as fn
 
@@ -390,12 +390,12 @@ def test_flash_fwd_v2_matches_v1(kernels, monkeypatch, p):
     B, T, H, D = 2, 384, 3, 64
     qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
     outs = {}
-    for ver in ("v1", "v2s2", "v2s3", "v2s4"):
+    for ver in ("v1", "v2s2", "v2s3", "v2s4", "v3s2", "v3s3", "v3s4"):
         monkeypatch.setenv("NSA_FLASH_FWD", ver)
         torch.manual_seed(5)
         outs[ver] = fn.attention(qkv, H, p, True).float()
         torch.cuda.synchronize()
-    for ver in ("v2s2", "v2s3", "v2s4"):
+    for ver in ("v2s2", "v2s3", "v2s4", "v3s2", "v3s3", "v3s4"):
         e = rel_err(outs[ver], outs["v1"])
         assert e < 5e-3, f"{ver} vs v1 rel err {e}"
 
