@@ -744,6 +744,11 @@ def decode_attention(qkv, kc, vc, pos, n_head: int, append: bool = False, combin
 
 
 GEMV_MAX_ROWS = int(os.environ.get("NSA_GEMV_MAX_ROWS", "1"))
+# decode batches of 2..SKINNY_MAX_ROWS rows: the MFMA weight-streaming kernel (nsa_skinny_gemm).
+# HIP-graph decode, ms/token (GPT-2 124M / 1.5B): batch 8 0.685 / 4.24 with the library GEMM,
+# 0.549 / 3.24 with this kernel; batch 64 0.938 / 5.45 vs 0.946 / 6.62 (every 16-column
+# workgroup re-reads the whole 64-row X, 4x its weight bytes), so the library keeps M > 16.
+SKINNY_MAX_ROWS = int(os.environ.get("NSA_SKINNY_MAX_ROWS", "16"))
 
 
 def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
@@ -752,7 +757,9 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
     otherwise ``linear`` (+ ``gelu``).  Inference only.  Measured (GPT-2 124M / 1.5B
     decode, HIP graph): batch 1 0.69 / 3.02 ms per token vs 0.90 / 4.70 with the library
     GEMM + bias copy; from 2 rows on the library GEMM is faster (batch 4: 1.52 vs
-    < 0.9 ms at 124M), so the default cap is 1 row (``NSA_GEMV_MAX_ROWS``)."""
+    < 0.9 ms at 124M), so the default cap is 1 row (``NSA_GEMV_MAX_ROWS``).  Batches of
+    2 .. ``NSA_SKINNY_MAX_ROWS`` (16) rows run on ``nsa_skinny_gemm`` (MFMA weight stream,
+    bias / GELU epilogue) when N % 16 == 0 and K % 32 == 0."""
     N = w.shape[0]
     if isinstance(x, AttnPartials):  # one row; the attention combine runs in the GEMV prologue
         y = torch.empty(N, device=x.ws.device, dtype=F32 if out_f32 else BF16)
@@ -769,6 +776,15 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
         y = torch.empty(rows, N, device=x.device, dtype=F32 if out_f32 else BF16)
         _lib.call("nsa_gemv", _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y), rows, N, K, 1 if gelu else 0,
                   1 if out_f32 else 0, _lib.stream())
+        return y.view(*x.shape[:-1], N)
+    if (x.is_cuda and x.dtype == BF16 and 2 <= rows <= SKINNY_MAX_ROWS and K % 32 == 0 and N % 16 == 0
+            and not (gelu and out_f32)):
+        x2 = x.reshape(rows, K).contiguous()
+        wc = compute_weight(w, BF16)
+        bc = compute_weight(b, BF16) if b is not None else None
+        y = torch.empty(rows, N, device=x.device, dtype=F32 if out_f32 else BF16)
+        _lib.call("nsa_skinny_gemm", _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y), rows, N, K,
+                  1 if gelu else 0, 1 if out_f32 else 0, _lib.stream())
         return y.view(*x.shape[:-1], N)
     y = linear(x, w, b)
     if gelu:

@@ -181,6 +181,40 @@ def test_decode_linear_kernel(kernels, monkeypatch, rows, N, K, bias, gelu, f32)
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("rows", [2, 3, 8, 15, 16, 17, 31, 33, 64])
+@pytest.mark.parametrize("N,K,bias,gelu,f32", [(768, 768, True, False, False), (3072, 768, True, True, False),
+                                              (768, 3072, False, False, False), (50304, 768, False, False, True),
+                                              (4800, 1600, True, False, False), (6400, 1600, True, True, False),
+                                              (16, 32, True, False, False), (48, 448, False, True, False)])
+def test_decode_skinny_gemm(kernels, monkeypatch, rows, N, K, bias, gelu, f32):
+    """Decode batches of 2..64 rows: the MFMA weight-streaming kernel (nsa_skinny_gemm,
+    16 output columns per workgroup, K-units split over 4 waves, tail loop for K not a
+    multiple of 512) against the fp32 reference."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional
+    import torch.nn.functional as F
+
+    monkeypatch.setattr(functional, "GEMV_MAX_ROWS", 1)
+    monkeypatch.setattr(functional, "SKINNY_MAX_ROWS", 64)
+    calls = []
+    real_call = functional._lib.call
+    monkeypatch.setattr(functional._lib, "call", lambda name, *a: (calls.append(name), real_call(name, *a))[1])
+    torch.manual_seed(rows * 13 + N + K)
+    x = torch.randn(rows, 1, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF) if bias else None
+    y = ops.decode_linear(x, w, b, gelu=gelu, out_f32=f32)
+    assert "nsa_skinny_gemm" in calls
+    ref = x.float().view(rows, K) @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if gelu:
+        ref = F.gelu(ref)
+    assert y.shape == (rows, 1, N) and y.dtype == (torch.float32 if f32 else BF)
+    err = ((y.float().view(rows, N) - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
 @pytest.mark.parametrize("branch", [False, True])
 @pytest.mark.parametrize("N,K,bias,gelu,f32", [(2304, 768, True, False, False), (3072, 768, True, True, False),
                                               (50304, 768, False, False, True), (6400, 1600, True, True, False),
