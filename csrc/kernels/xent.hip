@@ -131,7 +131,13 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   return r;
 }
 
-template <int RB, int RC>
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// NT bit 0: nontemporal logit loads, bit 1: nontemporal gradient stores + packed
+// v_cvt_pk_bf16_f32 conversion (the logits are streamed exactly once each way)
+template <int RB, int RC, int NT = 0>
 __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logits,
                                                      const int64_t* __restrict__ targets,
                                                      float* __restrict__ row_loss, int V, int write_grad) {
@@ -148,7 +154,12 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
 #pragma unroll
   for (int c = 0; c < kRegChunks; ++c) {
     const int i = min((int)threadIdx.x + c * kBlock, nv - 1);
-    r[c] = *reinterpret_cast<const uint4*>(lr + (int64_t)i * 8);
+    if constexpr (NT & 1) {
+      const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(lr + (int64_t)i * 8));
+      r[c] = make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+      r[c] = *reinterpret_cast<const uint4*>(lr + (int64_t)i * 8);
+    }
   }
   const float tgt_logit = valid ? bf2f(lr[tgt]) : 0.0f;
   float m = -INFINITY;
@@ -188,7 +199,16 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
         f[2 * q + 1] = valid ? __expf(__uint_as_float(w4[q] & 0xffff0000u) - M) * invS : 0.0f;
       }
       if (valid && (tgt >> 3) == i) f[tgt & 7] -= 1.0f;
-      store8(lr + (int64_t)i * 8, f);
+      if constexpr (NT & 2) {
+        u32x4_t v;
+        v.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[0], f[1]}, bf16x2_t));
+        v.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[2], f[3]}, bf16x2_t));
+        v.z = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[4], f[5]}, bf16x2_t));
+        v.w = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[6], f[7]}, bf16x2_t));
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(lr + (int64_t)i * 8));
+      } else {
+        store8(lr + (int64_t)i * 8, f);
+      }
     }
   }
 }
@@ -197,7 +217,10 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
 
 // write_grad bits 8..15 select the register-resident geometry (A/B timing,
 // scripts/membound_ab.py at 122880 x 50304: 1024 x 7 4.55 ms = 5.4 TB/s,
-// 512 x 13 4.59 ms, 256 x 25 4.86 ms): 0 = default (1024 x 7), 1 = 256 x 25, 2 = 512 x 13
+// 512 x 13 4.59 ms, 256 x 25 4.86 ms): 0 = default (1024 x 7, nontemporal loads and
+// stores), 1 = 256 x 25, 2 = 512 x 13, 3 / 4 / 5 = 1024 x 7 with nontemporal loads + stores /
+// stores / loads, 6 = 1024 x 7 plain.  Nontemporal loads + stores: 4618 -> 4348 us
+// (5.35 -> 5.69 TB/s, bitwise-identical output); stores alone 4557, loads alone 4641.
 NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int write_grad,
                                 hipStream_t s) {
   const int variant = (write_grad >> 8) & 0xff;
@@ -205,12 +228,19 @@ NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_los
   bf16_t* lg = (bf16_t*)logits;
   const int64_t* tg = (const int64_t*)targets;
   float* rl = (float*)row_loss;
-  if (V % 8 == 0 && variant == 1 && V <= 256 * 8 * 25)
+  if (V % 8 == 0 && variant >= 3 && variant <= 5 && V <= 1024 * 8 * 7) {
+    // 3: nontemporal loads + stores, 4: nontemporal stores, 5: nontemporal loads
+    if (variant == 3) xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
+    else if (variant == 4) xent_reg_kernel<1024, 7, 2><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
+    else xent_reg_kernel<1024, 7, 1><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
+  } else if (V % 8 == 0 && variant == 1 && V <= 256 * 8 * 25)
     xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, write_grad);
   else if (V % 8 == 0 && variant == 2 && V <= 512 * 8 * 13)
     xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0 && V <= 1024 * 8 * 7)
-    xent_reg_kernel<1024, 7><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
+  else if (V % 8 == 0 && variant == 6 && V <= 1024 * 8 * 7)
+    xent_reg_kernel<1024, 7, 0><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
+  else if (V % 8 == 0 && V <= 1024 * 8 * 7)  // default: nontemporal loads + stores
+    xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
   else if (V % 8 == 0)
     xent_kernel<true><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
   else

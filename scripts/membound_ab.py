@@ -83,7 +83,8 @@ def main():
         loss = torch.empty(N, device=dev, dtype=F32)
         byts = 2 * N * V * 2
         cands = {}
-        for v, name in ((0, "1024x7"), (1, "256x25"), (2, "512x13")):
+        for v, name in ((6, "1024x7"), (1, "256x25"), (2, "512x13"), (3, "1024x7_nt_ld_st"), (4, "1024x7_nt_st"),
+                        (5, "1024x7_nt_ld"), (0, "default")):
             cands[f"xent/{name}"] = (
                 lambda v=v: _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(tgt), _lib.ptr(loss), N, V,
                                       1 | (v << 8), S()), byts)
@@ -99,6 +100,15 @@ def main():
             "gelu_bwd": (lambda: _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(g), n, S()), 3 * n * 2),
             "copy": (lambda: g.copy_(u), 2 * n * 2),
         }
+
+        def plain(fn):  # same kernel without nontemporal loads / stores (NSA_EW_NT=0, read per launch)
+            def run_plain():
+                os.environ["NSA_EW_NT"] = "0"
+                fn()
+                os.environ.pop("NSA_EW_NT")
+            return run_plain
+        cands["gelu_fwd_plain"] = (plain(cands["gelu_fwd"][0]), cands["gelu_fwd"][1])
+        cands["gelu_bwd_plain"] = (plain(cands["gelu_bwd"][0]), cands["gelu_bwd"][1])
         print(json.dumps({"kernel": "gelu", "res": run(cands, a.rounds)}), flush=True)
 
 
