@@ -59,11 +59,61 @@ __device__ __forceinline__ void store8x(float* p, const float (&f)[8]) {
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// nontemporal variants (NT): the residual stream, its gradient and the branch tensors are
+// streamed once per pass; the normalised output and the bf16 gradient copy (read by the
+// next GEMM) keep normal stores
+typedef unsigned ln_u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16n(const void* p) {
+  if constexpr (NT) {
+    const ln_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const ln_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st16n(void* p, uint4 u) {
+  if constexpr (NT) {
+    ln_u32x4 v;
+    v.x = u.x;
+    v.y = u.y;
+    v.z = u.z;
+    v.w = u.w;
+    __builtin_nontemporal_store(v, reinterpret_cast<ln_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ Raw8<T> ld_raw_n(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < Raw8<T>::W; ++i) r.u[i] = ld16n<NT>(reinterpret_cast<const uint4*>(p) + i);
+  return r;
+}
+template <bool NT>
+__device__ __forceinline__ void load8n(const bf16_t* p, float (&f)[8]) { unpack8(ld16n<NT>(p), f); }
+template <bool NT>
+__device__ __forceinline__ void load8xn(const bf16_t* p, float (&f)[8]) { load8n<NT>(p, f); }
+template <bool NT>
+__device__ __forceinline__ void load8xn(const float* p, float (&f)[8]) { unpack_raw(ld_raw_n<NT>(p), f); }
+template <bool NT>
+__device__ __forceinline__ void store8xn(bf16_t* p, const float (&f)[8]) {
+  st16n<NT>(p, make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])));
+}
+template <bool NT>
+__device__ __forceinline__ void store8xn(float* p, const float (&f)[8]) {
+  st16n<NT>(p, make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])));
+  st16n<NT>(p + 4,
+            make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7])));
+}
+
 // value as stored in the residual stream (bf16 rounding for a bf16 stream)
 __device__ __forceinline__ float as_stream(float v, bf16_t*) { return bf2f(f2bf(v)); }
 __device__ __forceinline__ float as_stream(float v, float*) { return v; }
 
-template <int NK, typename XT>
+template <int NK, typename XT, bool NT = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, const bf16_t* __restrict__ res,
                                                     XT* __restrict__ sum_out, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
@@ -79,13 +129,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
   for (int k = 0; k < NK; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (c < C) {
-      load8x(xr + c, v[k]);
+      load8xn<NT>(xr + c, v[k]);
       if (res) {  // fused residual add: s = x + res, written out (XT) and normalised
         float rv[8];
-        load8(res + (int64_t)row * C + c, rv);
+        load8n<NT>(res + (int64_t)row * C + c, rv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = as_stream(v[k][j] + rv[j], (XT*)nullptr);
-        store8x(sum_out + (int64_t)row * C + c, v[k]);
+        store8xn<NT>(sum_out + (int64_t)row * C + c, v[k]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[k][j];
@@ -139,7 +189,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
 // per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
 // xhat and dy*w are recomputed from the raw words in the second pass rather than
 // kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
-template <int NK, bool PIPE, typename XT>
+template <int NK, bool PIPE, typename XT, bool NT = false>
 __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const XT* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
                                                     const float* __restrict__ rstd_in, const XT* __restrict__ dres,
@@ -173,9 +223,9 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
   _Pragma("unroll") for (int k = 0; k < NK; ++k) {                                       \
     const int c = min((k * 64 + lane) * 8, C - 8);                                       \
     const int64_t off = (int64_t)min((R), N - 1) * C + c;                                \
-    nx[k] = ld_raw(x + off);                                                             \
-    nd[k] = *reinterpret_cast<const uint4*>(dy + off);                                   \
-    if (dres) nr[k] = ld_raw(dres + off);                                                \
+    nx[k] = ld_raw_n<NT>(x + off);                                                       \
+    nd[k] = ld16n<NT>(dy + off);                                                         \
+    if (dres) nr[k] = ld_raw_n<NT>(dres + off);                                          \
   }
   if (PIPE) NSA_LNB_LOAD(row)
   for (; row < N; row += row_step) {
@@ -239,7 +289,7 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
-        store8x(dx + (int64_t)row * C + c, o);
+        store8xn<NT>(dx + (int64_t)row * C + c, o);
         if (dx_branch) store8(dx_branch + (int64_t)row * C + c, o);  // bf16 copy for the branch GEMMs
       }
     }
@@ -255,12 +305,25 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
   }
 }
 
+// nontemporal streams in the LayerNorm passes (default; NSA_LN_NT=0 turns them off, read per
+// launch for A/B runs).  GPT-2 124M step, same box, interleaved: 462.7 / 463.3 ms without,
+// 461.6 / 461.7 ms with
+bool ln_nt() {
+  const char* e = getenv("NSA_LN_NT");
+  return !(e && e[0] == '0');
+}
+
 template <int NK, typename XT>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
                       void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
-  ln_fwd_kernel<NK, XT><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
-                                                    (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (float*)mean,
-                                                    (float*)rstd, N, C, eps);
+  if (ln_nt())
+    ln_fwd_kernel<NK, XT, true><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
+                                                            (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
+                                                            (float*)mean, (float*)rstd, N, C, eps);
+  else
+    ln_fwd_kernel<NK, XT, false><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
+                                                             (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
+                                                             (float*)mean, (float*)rstd, N, C, eps);
   return hipGetLastError();
 }
 
@@ -271,7 +334,11 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* 
   // bit 30 of nblk selects the non-pipelined body (A/B timing)
   const bool pipe = !(nblk & (1 << 30));
   nblk &= ~(1 << 30);
-  if (pipe)
+  if (pipe && ln_nt())
+    ln_bwd_kernel<NK, true, XT, true><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
+        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
+  else if (pipe)
     ln_bwd_kernel<NK, true, XT><<<nblk, 256, 8 * C * sizeof(float), s>>>(
         (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
         (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
