@@ -1098,6 +1098,162 @@ NSA_API hipError_t nsa_skinny_gemm(const void* x, const void* W, const void* bia
   return hipGetLastError();
 }
 
+// Skinny GEMM with the residual add + LayerNorm in the prologue (decode batches of
+// 2..16 rows, the batch counterpart of gemv_row_kernel<PRO_LN>): every workgroup forms
+// s = res + branch and x = LN(s) for all rows itself (wave w: rows w, w + 4, ...; a row of
+// K <= 2048 lives in 32 registers per lane, two-pass mean / variance as nanoGPT's fp32
+// LayerNorm), stores x as bf16 in LDS ([16][K + 8], padded rows) and reads the MFMA B
+// fragments from there; workgroup 0 writes s (fp32).  The first round of weight loads is
+// issued before the prologue and each round prefetches the next, so the weight stream
+// overlaps the LayerNorm.  Removes the separate add+LayerNorm launch per linear.
+__device__ __forceinline__ float sk_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int ACT, bool OUTF>
+__global__ __launch_bounds__(256) void skinny_ln_gemm_kernel(const float* __restrict__ res,
+                                                             const bf16_t* __restrict__ branch,
+                                                             float* __restrict__ s_out, const bf16_t* __restrict__ lw,
+                                                             const bf16_t* __restrict__ lb, float eps,
+                                                             const bf16_t* __restrict__ W,
+                                                             const bf16_t* __restrict__ bias, void* __restrict__ yv,
+                                                             int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [16][K + 8]
+  __shared__ float red[4][4][64];
+  const int KP = K + 8;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int g = lane >> 4, c = lane & 15;
+  const bf16_t* wrow = W + (int64_t)(n0 + c) * K + 8 * g;
+  const int U = K / 32;
+  constexpr int UN = 8;
+  uint4 a[UN];
+  auto load_a = [&](int u0, uint4 (&dst)[UN]) {
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+      const int uu = u0 + 4 * j;
+      dst[j] = *reinterpret_cast<const uint4*>(wrow + 32 * (uu < U ? uu : U - 1));
+      if (uu >= U) dst[j] = uint4{0u, 0u, 0u, 0u};
+    }
+  };
+  load_a(w, a);
+  // prologue: LayerNorm of the M batch rows into LDS (rows M..15 stay unwritten: they only
+  // feed output columns m >= M, which are never stored)
+  for (int m = w; m < M; m += 4) {
+    const int mm = m;
+    float v[4][8];
+    float sum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = (q * 64 + lane) * 8;
+      if (k < K) {
+        const float4 r0 = *reinterpret_cast<const float4*>(res + (int64_t)mm * K + k);
+        const float4 r1 = *reinterpret_cast<const float4*>(res + (int64_t)mm * K + k + 4);
+        v[q][0] = r0.x; v[q][1] = r0.y; v[q][2] = r0.z; v[q][3] = r0.w;
+        v[q][4] = r1.x; v[q][5] = r1.y; v[q][6] = r1.z; v[q][7] = r1.w;
+        if (branch) {
+          float bv[8];
+          load8(branch + (int64_t)mm * K + k, bv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[q][e] += bv[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum += v[q][e];
+      }
+    }
+    const float mean = sk_wave_sum(sum) / (float)K;
+    float sq = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if ((q * 64 + lane) * 8 < K)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sq = fmaf(v[q][e] - mean, v[q][e] - mean, sq);
+    const float rstd = rsqrtf(sk_wave_sum(sq) / (float)K + eps);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = (q * 64 + lane) * 8;
+      if (k < K) {
+        float wv[8], bv[8], o[8];
+        load8(lw + k, wv);
+        if (lb) {
+          load8(lb + k, bv);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bv[e] = 0.0f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (v[q][e] - mean) * rstd * wv[e] + bv[e];
+        store8(xs + m * KP + k, o);
+        if (blockIdx.x == 0 && s_out && m < M) {
+          float* sp = s_out + (int64_t)m * K + k;
+          *reinterpret_cast<float4*>(sp) = make_float4(v[q][0], v[q][1], v[q][2], v[q][3]);
+          *reinterpret_cast<float4*>(sp + 4) = make_float4(v[q][4], v[q][5], v[q][6], v[q][7]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 acc = f32x4{};
+  for (int u0 = w; u0 < U; u0 += 4 * UN) {
+    uint4 b[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+      const int uu = u0 + 4 * j;
+      b[j] = *reinterpret_cast<const uint4*>(xs + c * KP + 32 * (uu < U ? uu : U - 1) + 8 * g);
+    }
+    uint4 an[UN];
+    const bool more = u0 + 4 * UN < U;  // wave-uniform
+    if (more) load_a(u0 + 4 * UN, an);
+#pragma unroll
+    for (int j = 0; j < UN; ++j)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[j]), __builtin_bit_cast(bf16x8, b[j]),
+                                                    acc, 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < UN; ++j) a[j] = an[j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[w][i][lane] = acc[i];
+  __syncthreads();
+  {
+    const int e = tid, n = e & 15, m = e >> 4;
+    if (m < M) {
+      const int i = n & 3, ln = 16 * (n >> 2) + m;
+      float o = red[0][i][ln] + red[1][i][ln] + red[2][i][ln] + red[3][i][ln];
+      if (bias) o += bf2f(bias[n0 + n]);
+      if constexpr (ACT == 1) o = nsa_gelu(o);
+      if constexpr (OUTF)
+        reinterpret_cast<float*>(yv)[(int64_t)m * N + n0 + n] = o;
+      else
+        reinterpret_cast<bf16_t*>(yv)[(int64_t)m * N + n0 + n] = f2bf(o);
+    }
+  }
+}
+
+// (s, y) for 2..16 decode rows: s = res + branch (fp32, branch bf16 or NULL: s_out unused),
+// y = act(LN(s) W^T + b); N % 16 == 0, K % 32 == 0, K <= 1920 (LDS image [16][K + 8] bf16)
+NSA_API hipError_t nsa_skinny_ln_gemm(const void* res, const void* branch, void* s_out, const void* lw,
+                                      const void* lb, float eps, const void* W, const void* bias, void* y, int rows,
+                                      int N, int K, int act, int out_f32, hipStream_t s) {
+  if (rows < 1 || rows > 16 || N % 16 || K % 32 || N < 16 || K < 32 || K > 1920 || (act && out_f32) ||
+      (branch && !s_out))
+    return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)(N / 16);
+  const size_t lds = (size_t)16 * (K + 8) * sizeof(bf16_t);
+#define NSA_SKLN(A, F)                                                                                    \
+  skinny_ln_gemm_kernel<A, F><<<grid, 256, lds, s>>>((const float*)res, (const bf16_t*)branch, (float*)s_out, \
+                                                     (const bf16_t*)lw, (const bf16_t*)lb, eps, (const bf16_t*)W, \
+                                                     (const bf16_t*)bias, y, rows, N, K)
+  if (act) NSA_SKLN(1, false);
+  else if (out_f32) NSA_SKLN(0, true);
+  else NSA_SKLN(0, false);
+#undef NSA_SKLN
+  return hipGetLastError();
+}
+
 // Decode-batch linear y[rows, N] = act(x[rows, K] W[N, K]^T + b), rows <= 8, K % 8 == 0;
 // act: 0 none, 1 exact-erf GELU; out_f32: y is fp32 (e.g. logits) instead of bf16.
 // bias may be NULL.

@@ -71,6 +71,8 @@ _SIGNATURES = {
                         c_void_p],
     "nsa_gemv": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_skinny_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_skinny_ln_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p,
+                           c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemv_emb_ln": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_int, c_int, c_float, c_int, c_int, c_void_p],
     "nsa_gemv_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],

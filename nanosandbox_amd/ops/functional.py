@@ -749,6 +749,11 @@ GEMV_MAX_ROWS = int(os.environ.get("NSA_GEMV_MAX_ROWS", "1"))
 # 0.549 / 3.24 with this kernel; batch 64 0.938 / 5.45 vs 0.946 / 6.62 (every 16-column
 # workgroup re-reads the whole 64-row X, 4x its weight bytes), so the library keeps M > 16.
 SKINNY_MAX_ROWS = int(os.environ.get("NSA_SKINNY_MAX_ROWS", "16"))
+# residual add + LayerNorm recomputed in the skinny GEMM's prologue (nsa_skinny_ln_gemm) up to
+# this many rows; HIP-graph decode ms/token, 124M / 1.5B: batch 8 0.532 / 3.34 unfused vs
+# 0.532 / 3.18 fused; batch 16 0.597 / 3.78 unfused vs 0.667 / 4.10 fused (every workgroup
+# normalises all rows: the per-workgroup prologue outgrows the saved launch)
+SKINNY_LN_MAX_ROWS = int(os.environ.get("NSA_SKINNY_LN_MAX_ROWS", "8"))
 
 
 def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
@@ -816,6 +821,26 @@ def decode_linear_ln(res, branch, ln_w, ln_b, w, b=None, gelu: bool = False, out
         _lib.call("nsa_gemv_ln", _lib.ptr(r2), _lib.ptr(br), _lib.ptr(s_out), _lib.ptr(lw), _lib.ptr(lb), _lib.ptr(wc),
                   _lib.ptr(bc), _lib.ptr(y), N, C, LN_EPS, 1 if gelu else 0, 1 if out_f32 else 0, _lib.ptr(pos_inc),
                   _lib.stream())
+        s_new = s_out.view(res.shape) if branch is not None else res
+        return s_new, y.view(*res.shape[:-1], N)
+    N = w.shape[0]
+    if (res.is_cuda and res.dtype == F32 and 2 <= rows <= min(SKINNY_MAX_ROWS, SKINNY_LN_MAX_ROWS) and C % 32 == 0
+            and C <= 1920
+            and N % 16 == 0 and not (gelu and out_f32) and (branch is None or branch.dtype == BF16)
+            and out_dtype in (None, BF16)):
+        # 2..16 rows: residual add + LayerNorm recomputed per workgroup in the skinny GEMM's prologue
+        r2 = res.reshape(rows, C).contiguous()
+        br = branch.reshape(rows, C).contiguous() if branch is not None else None
+        s_out = torch.empty_like(r2) if branch is not None else None
+        lw, lb = compute_weight(ln_w, BF16), compute_weight(ln_b, BF16) if ln_b is not None else None
+        wc = compute_weight(w, BF16)
+        bc = compute_weight(b, BF16) if b is not None else None
+        y = torch.empty(rows, N, device=res.device, dtype=F32 if out_f32 else BF16)
+        _lib.call("nsa_skinny_ln_gemm", _lib.ptr(r2), _lib.ptr(br), _lib.ptr(s_out), _lib.ptr(lw), _lib.ptr(lb),
+                  LN_EPS, _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(y), rows, N, C, 1 if gelu else 0,
+                  1 if out_f32 else 0, _lib.stream())
+        if pos_inc is not None:
+            pos_inc.add_(1)
         s_new = s_out.view(res.shape) if branch is not None else res
         return s_new, y.view(*res.shape[:-1], N)
     if branch is None:

@@ -215,6 +215,44 @@ def test_decode_skinny_gemm(kernels, monkeypatch, rows, N, K, bias, gelu, f32):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("rows", [2, 5, 16])
+@pytest.mark.parametrize("branch", [False, True])
+@pytest.mark.parametrize("N,K,bias,gelu,f32", [(2304, 768, True, False, False), (3072, 768, True, True, False),
+                                              (50304, 768, False, False, True), (6400, 1600, True, True, False),
+                                              (4800, 1600, True, False, False), (48, 1920, False, False, False)])
+def test_decode_skinny_ln_kernel(kernels, monkeypatch, rows, branch, N, K, bias, gelu, f32):
+    """Residual add + LayerNorm in the skinny GEMM's prologue (2..16 decode rows) against
+    fp32 torch on the same bf16-rounded LayerNorm output; s = res + branch in fp32."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional
+    import torch.nn.functional as F
+
+    monkeypatch.setattr(functional, "SKINNY_LN_MAX_ROWS", 16)  # exercise the kernel at every row count
+    calls = []
+    real_call = functional._lib.call
+    monkeypatch.setattr(functional._lib, "call", lambda name, *a: (calls.append(name), real_call(name, *a))[1])
+    torch.manual_seed(N + K + rows)
+    res = torch.randn(rows, 1, K, device=DEV) * 3 + 0.5
+    br = torch.randn(rows, 1, K, device=DEV).to(BF) if branch else None
+    lw = (1 + 0.1 * torch.randn(K, device=DEV)).to(BF)
+    lb = (0.1 * torch.randn(K, device=DEV)).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF) if bias else None
+    s, y = ops.decode_linear_ln(res, br, lw, lb, w, b, gelu=gelu, out_f32=f32)
+    assert "nsa_skinny_ln_gemm" in calls
+    s_ref = res + br.float() if branch else res
+    assert torch.allclose(s, s_ref) and (branch or s is res)
+    h = F.layer_norm(s_ref.view(rows, K), (K,), lw.float(), lb.float(), 1e-5).to(BF).float()
+    ref = h @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if gelu:
+        ref = F.gelu(ref)
+    assert y.shape == (rows, 1, N) and y.dtype == (torch.float32 if f32 else BF)
+    err = ((y.float().view(rows, N) - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
 @pytest.mark.parametrize("branch", [False, True])
 @pytest.mark.parametrize("N,K,bias,gelu,f32", [(2304, 768, True, False, False), (3072, 768, True, True, False),
                                               (50304, 768, False, False, True), (6400, 1600, True, True, False),
