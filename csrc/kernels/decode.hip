@@ -1139,8 +1139,10 @@ __global__ __launch_bounds__(256) void skinny_ln_gemm_kernel(const float* __rest
     }
   };
   load_a(w, a);
-  // prologue: LayerNorm of the M batch rows into LDS (rows M..15 stay unwritten: they only
-  // feed output columns m >= M, which are never stored)
+  // prologue: LayerNorm of the M batch rows into LDS; rows M..15 are zeroed (they only feed
+  // output columns m >= M, which are never stored)
+  for (int m = M + w; m < 16; m += 4)
+    for (int k = 8 * lane; k < K; k += 512) *reinterpret_cast<uint4*>(xs + m * KP + k) = uint4{0u, 0u, 0u, 0u};
   for (int m = w; m < M; m += 4) {
     const int mm = m;
     float v[4][8];
