@@ -94,7 +94,11 @@ def main():
         # HBM-sized micro-batch: the largest divisor of the per-rank batch whose activations
         # stay resident next to the model state (utils/memory.py); 120 for GPT-2 124M / 350M
         from nanosandbox_amd.utils.memory import choose_micro_batch
-        hbm = torch.cuda.get_device_properties(int(os.environ.get("LOCAL_RANK", "0"))).total_memory
+        # every rank of a one-GPU rehearsal (NSA_REHEARSAL_ONE_GPU, parallel/dist.py) runs on cuda:0
+        dev_index = 0 if os.environ.get("NSA_REHEARSAL_ONE_GPU") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+        hbm = torch.cuda.get_device_properties(dev_index).total_memory
+        if os.environ.get("NSA_REHEARSAL_ONE_GPU") == "1":
+            hbm //= world  # the ranks share the one GPU's HBM
         args.micro_batch, _ = choose_micro_batch(dims[0], dims[2], dims[1], 50304, args.block_size,
                                                  480 // world, hbm, fp32_residual=not args.bf16_residual)
     args.micro_batch, total_micro = batch_plan(world, args.micro_batch)
