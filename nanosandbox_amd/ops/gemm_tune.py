@@ -78,6 +78,8 @@ WGRAD_ALLOW_BF16 = os.environ.get("NSA_WGRAD_ALLOW_BF16", "0") == "1"
 # to pin); the embedding backward switches to its sorted, atomic-free kernel.
 DETERMINISTIC = False
 NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
+# weight-grad split counts that fill whole CU rounds as tuner candidates (NSA_WGRAD_FULL_ROUNDS=0: off)
+WGRAD_FULL_ROUNDS = os.environ.get("NSA_WGRAD_FULL_ROUNDS", "1") != "0"
 WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
 # input-grad candidates on the NT layout through the cached W^T (e.g. NSA_NT_VARIANTS=7,9:
 # ring64, persistent p8).  Off by default: on the GPT-2 shapes neither the plain nor the
@@ -366,6 +368,11 @@ def wgrad_acc(dy2, x2, g32):
     tiles = -(-N // _gemm.TILE) * -(-K // _gemm.TILE)
     extra = {_gemm.wgrad_splits_balanced(N, K, T)}
     extra.update(r * 256 // tiles for r in (1, 2, 3))
+    if WGRAD_FULL_ROUNDS:
+        # split counts up to 8 whose work items fill >= 95 % of their last CU round (the tied
+        # lm_head dW has 591 output tiles: 3 splits = 1773 items = 99 % of 7 rounds)
+        extra.update(sp for sp in range(1, 9)
+                     if tiles * sp / (256 * -(-(tiles * sp) // 256)) >= 0.95)
     for sb in sorted(x for x in extra if 1 <= x <= max(1, T // _gemm.BK) and x != sdef):
         cands.update({f"nsa{v}/s{sb}": cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v))
                       for v in WGRAD_VARIANTS})
