@@ -246,7 +246,7 @@ static bool ew_nt() {
 }
 
 NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
-  if (ew_nt())
+  if (ew_nt() && n * 2 >= NSA_NT_MIN_BYTES)
     gelu_fwd_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
   else
     gelu_fwd_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
@@ -254,7 +254,7 @@ NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s
 }
 
 NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
-  if (ew_nt())
+  if (ew_nt() && n * 2 >= NSA_NT_MIN_BYTES)
     gelu_bwd_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
   else
     gelu_bwd_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);

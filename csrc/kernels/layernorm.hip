@@ -316,7 +316,7 @@ bool ln_nt() {
 template <int NK, typename XT>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
                       void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
-  if (ln_nt())
+  if (ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
     ln_fwd_kernel<NK, XT, true><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
                                                             (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
                                                             (float*)mean, (float*)rstd, N, C, eps);
@@ -334,7 +334,7 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* 
   // bit 30 of nblk selects the non-pipelined body (A/B timing)
   const bool pipe = !(nblk & (1 << 30));
   nblk &= ~(1 << 30);
-  if (pipe && ln_nt())
+  if (pipe && ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
     ln_bwd_kernel<NK, true, XT, true><<<nblk, 256, 8 * C * sizeof(float), s>>>(
         (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
         (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);

@@ -237,7 +237,7 @@ NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_los
     xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, write_grad);
   else if (V % 8 == 0 && variant == 2 && V <= 512 * 8 * 13)
     xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0 && variant == 6 && V <= 1024 * 8 * 7)
+  else if (V % 8 == 0 && (variant == 6 || (int64_t)N * V * 2 < NSA_NT_MIN_BYTES) && V <= 1024 * 8 * 7)
     xent_reg_kernel<1024, 7, 0><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
   else if (V % 8 == 0 && V <= 1024 * 8 * 7)  // default: nontemporal loads + stores
     xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
