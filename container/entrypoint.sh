@@ -50,10 +50,25 @@ export NODE_RANK
 
 # RCCL transport preset: xGMI P2P inside one pod; socket fallback across pods
 # that do not share IPC (the reference's NCCL_IB_DISABLE/NCCL_SOCKET_IFNAME).
-if [[ "${NSA_RCCL_PRESET:-}" == "socket" ]]; then
-  export NCCL_IB_DISABLE="${NCCL_IB_DISABLE:-1}"
-  export NCCL_SOCKET_IFNAME="${NCCL_SOCKET_IFNAME:-eth0}"
-fi
+#   xgmi   all ranks in one pod: RCCL P2P over xGMI
+#   shm    pods of one node sharing the host /dev/shm (hostIPC + hostPath) and one
+#          NCCL_HOSTID: RCCL SHM through host memory (no peer GPU access across pods)
+#   socket pods that share nothing: TCP (the reference's NCCL_IB_DISABLE / SOCKET_IFNAME)
+case "${NSA_RCCL_PRESET:-xgmi}" in
+  socket)
+    export NCCL_IB_DISABLE="${NCCL_IB_DISABLE:-1}"
+    export NCCL_SOCKET_IFNAME="${NCCL_SOCKET_IFNAME:-eth0}"
+    ;;
+  shm)
+    export NCCL_SHM_DISABLE="${NCCL_SHM_DISABLE:-0}"
+    if [[ -z "${NCCL_HOSTID:-}" ]]; then
+      echo "entrypoint: WARNING NSA_RCCL_PRESET=shm without NCCL_HOSTID: RCCL will see each pod as its own host (NET transport)" >&2
+    fi
+    ;;
+esac
+# the transport facts that decide what RCCL can pick, for kubectl logs
+shm_fs="$(stat -f -c %T /dev/shm 2>/dev/null || echo '?')"
+echo "entrypoint: rccl preset=${NSA_RCCL_PRESET:-xgmi} NCCL_HOSTID=${NCCL_HOSTID:-<unset>} /dev/shm=${shm_fs}" >&2
 export HSA_ENABLE_IPC_MODE_LEGACY="${HSA_ENABLE_IPC_MODE_LEGACY:-0}"
 export TORCH_NCCL_HIGH_PRIORITY="${TORCH_NCCL_HIGH_PRIORITY:-1}"
 

@@ -57,6 +57,7 @@ TRAIN_DEFAULTS = dict(
     ddp_impl="flat",  # 'flat' (our bucketed RCCL reducer) | 'torch' (torch DDP)
     ddp_bucket_mb=64,  # gradient bucket cap; 64 MiB suits ring all-reduce over 7 xGMI links
     grad_reduce_dtype="float32",  # 'float32' | 'bfloat16' (compressed all-reduce)
+    rccl_report=True,  # at DDP start: per-peer RCCL transport (P2P/SHM/NET) + 64 MiB all-reduce bus bandwidth
     grad_ckpt=False,  # recompute each Block in backward (activation checkpointing)
     hbm_plan=True,  # grad_ckpt=False: turn checkpointing on only if the activation estimate exceeds free HBM
     fp32_residual=True,  # residual stream + its gradient in fp32 (nanoGPT autocast contract); False: bf16

@@ -1,8 +1,9 @@
 """Loader for the in-tree gfx950 kernel library ``nanosandbox_amd/lib/libnsa_kernels.so``.
 
 The kernels are plain HIP C++ (``csrc/kernels/*.hip``) compiled by ``hipcc
---offload-arch=gfx950`` into one shared object with a C ABI (see
-``csrc/kernels/nsa_api.h``).  We bind it with ctypes rather than a torch C++
+--offload-arch=gfx950`` into one shared object with a C ABI (every entry point is an
+``NSA_API`` function, ``csrc/kernels/common.h``; its ctypes signature is listed in
+``_SIGNATURES`` below).  We bind it with ctypes rather than a torch C++
 extension: the library does not depend on torch headers or ABI, builds in
 seconds, and every launch takes raw device pointers plus the current HIP
 stream, so it composes with torch's stream/graph semantics.
@@ -88,6 +89,8 @@ _SIGNATURES = {
     "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_gemm_nt": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                    c_int, c_int, c_int, c_int, c_void_p],
 }
 
 

@@ -97,6 +97,55 @@ def dgrad_t(dy2, wt, u=None, variant=None):
     return out
 
 
+# ---------------------------------------------------------------------------------
+# Persistent NT kernel (csrc/kernels/gemm_nt.hip): forward and input grads, both
+# operands K-contiguous; the input grad uses the cached weight transpose.
+# ---------------------------------------------------------------------------------
+NT_EPI_BF16, NT_EPI_GELU, NT_EPI_DGELU = 0, 1, 2
+_NCU = {}
+
+
+def num_cus(device=None):
+    d = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    if d not in _NCU:
+        _NCU[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _NCU[d]
+
+
+def nt_supported(M, N, K) -> bool:
+    return M >= 256 and N >= 256 and K >= BK and K % BK == 0 and N % 8 == 0
+
+
+NT_VAR = int(os.environ.get("NSA_NT_VAR", "0"))
+
+
+def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None):
+    var = NT_VAR if var is None else var
+    _lib.call("nsa_gemm_nt", epi | (probe << 8) | (var << 12), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
+              C.stride(0), _lib.ptr(C2), _lib.ptr(U), M, N, K, grid or num_cus(A.device), _lib.stream())
+
+
+def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None):
+    """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the persistent kernel.
+
+    epi NT_EPI_GELU returns (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u)."""
+    M, K = a.shape
+    N = b.shape[0]
+    _check(a, "a")
+    _check(b, "b")
+    out = torch.empty(M, N, device=a.device, dtype=BF16)
+    if epi == NT_EPI_GELU:
+        act = torch.empty_like(out)
+        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var)
+        return out, act
+    if epi == NT_EPI_DGELU:
+        _check(u, "u")
+        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var)
+        return out
+    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var)
+    return out
+
+
 def wgrad_splits(n_out, n_in, tokens, cus=256):
     """Largest split count with at most two rounds of blocks (one 512-thread block per CU)."""
     tiles = -(-n_out // TILE) * -(-n_in // TILE)

@@ -1,2 +1,3 @@
-from .dist import DistInfo, destroy, init_distributed, node_rank_from_hostname, rccl_env_defaults  # noqa: F401
+from .dist import (DistInfo, destroy, init_distributed, node_rank_from_hostname, parse_transports,  # noqa: F401
+                   rccl_env_defaults, report_transport, transport_kind)
 from .reducer import FlatBucketReducer  # noqa: F401

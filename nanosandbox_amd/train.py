@@ -121,7 +121,10 @@ class Trainer:
         model.grad_ckpt = c["grad_ckpt"]
         from . import ops as _ops
         _ops.set_deterministic(c["deterministic"])
-        _ops.rng_set(self.device, 0)  # this run's dropout stream starts at step 0
+        # the dropout kernels' device step counter: a fresh run starts its stream at 0, a
+        # resumed one continues where the checkpointed run stood (micro-steps taken so far)
+        # instead of replaying the first steps' masks
+        _ops.rng_set(self.device, self.iter_num * self.gas)
         print(f"number of parameters: {model.get_num_params() / 1e6:.2f}M")
 
         # ------------------------------------------- flat store + fused AdamW
@@ -177,6 +180,12 @@ class Trainer:
                 self.store.refresh_compute()
             else:
                 raise ValueError(f"unknown ddp_impl {self.ddp_impl!r}")
+
+        if info.ddp and c["rccl_report"]:
+            # which transport RCCL picked per peer (P2P over xGMI / SHM / NET) and the bus
+            # bandwidth of one 64 MiB all-reduce (docs/rccl.md)
+            from .parallel import report_transport
+            self.rccl_report = report_transport(info)
 
         self.batches = make_batch_source(c["dataset"], c["data_dir"], c["block_size"], c["batch_size"], self.device,
                                          seed=c["seed"] + info.seed_offset, vocab_size=model_args["vocab_size"])
@@ -272,7 +281,7 @@ class Trainer:
             if self.iter_num == 0 and c["eval_only"]:
                 break
             if c["fault_inject_iter"] == self.iter_num and c["fault_inject_rank"] == self.info.rank:
-                raise RuntimeError(f"injected fault at iter {self.iter_num} on rank {self.info.rank}")
+                self._inject_fault()
 
             loss, norm, X, Y = self.train_step(X, Y)
             if prof is not None:
@@ -297,6 +306,29 @@ class Trainer:
         if prof is not None:
             prof.stop()
         self.metrics.close()
+        if os.environ.get("NSA_PARAM_DIGEST") == "1":
+            # replica-consistency probe for the elastic-restart test: every rank prints a
+            # digest of its parameters; DDP replicas must agree bit for bit
+            import hashlib
+            h = hashlib.sha256()
+            for _, p in sorted(self.raw_model.state_dict().items()):
+                h.update(p.detach().float().cpu().numpy().tobytes())
+            print(f"param digest rank {self.info.rank}: {h.hexdigest()[:16]} iter {self.iter_num}", flush=True)
+
+    def _inject_fault(self):
+        """Fail this rank once per job (SURVEY.md §5.3 fault injection).
+
+        The fault fires only on the job's first attempt: a marker file in ``out_dir``
+        (shared storage: the PVC in the k8s topologies) records that it fired, and
+        torchrun's ``TORCHELASTIC_RESTART_COUNT`` > 0 also suppresses it, so an elastic
+        restart (``--max-restarts``) that auto-resumes from ``ckpt.pt`` runs through."""
+        marker = os.path.join(self.cfg["out_dir"], f".fault_injected_rank{self.info.rank}")
+        if os.path.exists(marker) or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) > 0:
+            return
+        os.makedirs(self.cfg["out_dir"], exist_ok=True)
+        with open(marker, "w") as f:
+            f.write(f"{self.iter_num}\n")
+        raise RuntimeError(f"injected fault at iter {self.iter_num} on rank {self.info.rank}")
 
     def _profiler(self):
         from torch.profiler import ProfilerActivity, profile, schedule, tensorboard_trace_handler

@@ -14,10 +14,12 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
-    import torch
-
-    if torch.cuda.is_available():
-        return
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return
+    except ImportError:  # the CI lint job runs the torch-free manifest tests only
+        pass
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for item in items:
         if "gpu" in item.keywords:

@@ -216,3 +216,30 @@ def test_from_pretrained_without_snapshot_says_why(tmp_path, monkeypatch):
     monkeypatch.setenv("HF_HOME", str(tmp_path))
     with pytest.raises(FileNotFoundError, match="NSA_HF_GPT2_DIR"):
         GPT.from_pretrained("gpt2-medium")
+
+
+def test_from_pretrained_matches_hf_gpt2_forward(tmp_path, monkeypatch):
+    """U-M8 parity against HuggingFace itself (offline): a random-init
+    ``transformers.GPT2LMHeadModel`` at gpt2 sizes, saved with ``save_pretrained``
+    (safetensors), loaded through ``GPT.from_pretrained('gpt2')`` — the Conv1D
+    transposes, tied lm_head and key mapping must reproduce HF's logits.
+    ``activation_function='gelu'`` because nanoGPT's MLP is the exact-erf GELU."""
+    transformers = pytest.importorskip("transformers")
+    torch.manual_seed(0)
+    hf_cfg = transformers.GPT2Config(n_layer=12, n_head=12, n_embd=768, n_positions=1024, vocab_size=50257,
+                                     activation_function="gelu", resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
+    hf = transformers.GPT2LMHeadModel(hf_cfg).eval()
+    snap = tmp_path / "gpt2"
+    hf.save_pretrained(str(snap), safe_serialization=True)
+    monkeypatch.setenv("NSA_HF_GPT2_DIR", str(tmp_path))
+    m = GPT.from_pretrained("gpt2").eval()
+    assert m.lm_head.weight is m.transformer.wte.weight
+    idx = torch.randint(0, 50257, (2, 64))
+    with torch.no_grad():
+        out = hf(idx, labels=idx)
+        ref = out.logits.float()
+        last, _ = m(idx)  # inference path: last-position logits
+        _, loss = m(idx[:, :-1], idx[:, 1:])  # training path: fused lm_head + cross-entropy
+    rel = ((last[:, -1].float() - ref[:, -1]).norm() / ref[:, -1].norm()).item()
+    assert rel < 1e-4, rel
+    assert abs(loss.item() - out.loss.item()) < 1e-4 * abs(out.loss.item()), (loss.item(), out.loss.item())

@@ -16,69 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENTRY = os.path.join(ROOT, "container", "entrypoint.sh")
 
 
-def _docs():
-    out = {}
-    for f in sorted(glob.glob(os.path.join(ROOT, "k8s", "**", "*.yaml"), recursive=True)):
-        for d in yaml.safe_load_all(open(f)):
-            if d:
-                out[(d["kind"], d["metadata"]["name"])] = d
-    return out
-
-
-def test_manifests_parse_and_names():
-    d = _docs()
-    assert ("Namespace", "disttrain") in d
-    assert ("ConfigMap", "proxy-config") in d
-    assert ("PersistentVolume", "disttrain-pv") in d and ("PersistentVolumeClaim", "disttrain-pvc") in d
-    assert d[("PersistentVolume", "disttrain-pv")]["spec"]["hostPath"]["path"] == "/var/lib/disttrain"
-    for k in [("Job", "download-tiny-shakespeare"), ("Job", "train-singlepod"), ("StatefulSet", "train-multipod"),
-              ("Service", "train-mp-headless"), ("Job", "prepare-owt-subset")]:
-        assert k in d, k
-        if k[0] != "PersistentVolume":
-            assert d[k]["metadata"].get("namespace", "disttrain") == "disttrain"
-
-
-def test_no_proxy_keeps_cluster_traffic_direct():
-    cm = _docs()[("ConfigMap", "proxy-config")]["data"]
-    for h in [".svc", ".cluster.local", "127.0.0.1", "localhost"]:
-        assert h in cm["NO_PROXY"]
-
-
-def _container(obj):
-    spec = obj["spec"]["template"]["spec"]
-    return spec, spec["containers"][0]
-
-
-def _env(c):
-    return {e["name"]: e.get("value") for e in c.get("env", [])}
-
-
-def test_singlepod_job_uses_all_gpus_standalone():
-    spec, c = _container(_docs()[("Job", "train-singlepod")])
-    env = _env(c)
-    assert c["resources"]["limits"]["amd.com/gpu"] == int(env["NPROC_PER_NODE"]) == 8
-    assert env["NNODES"] == "1"
-    assert any(m["mountPath"] == "/data" for m in c["volumeMounts"])
-    assert any(m["mountPath"] == "/dev/shm" for m in c["volumeMounts"])
-    assert "nvidia.com/gpu" not in str(spec)
-
-
-def test_statefulset_rendezvous_consistency():
-    d = _docs()
-    sts = d[("StatefulSet", "train-multipod")]
-    svc = d[("Service", "train-mp-headless")]
-    spec, c = _container(sts)
-    env = _env(c)
-    assert sts["spec"]["serviceName"] == svc["metadata"]["name"]
-    assert svc["spec"]["clusterIP"] == "None"
-    assert svc["spec"]["selector"] == sts["spec"]["selector"]["matchLabels"]
-    assert int(env["NNODES"]) == sts["spec"]["replicas"] == 8
-    assert env["NPROC_PER_NODE"] == "1" and c["resources"]["limits"]["amd.com/gpu"] == 1
-    assert env["MASTER_ADDR"] == f"{sts['metadata']['name']}-0.{svc['metadata']['name']}"
-    assert env["MASTER_PORT"] == str(svc["spec"]["ports"][0]["port"])
-    assert env["RDZV_BACKEND"] == "c10d"
-    assert any(e["name"] == "POD_NAME" for e in c["env"])
-    assert any(a.startswith("config/train_gpt2_350m.py") for a in c["args"])
+from test_manifests import _docs, _container  # noqa: E402
 
 
 def test_train_args_are_valid_config_overrides():
@@ -90,11 +28,6 @@ def test_train_args_are_valid_config_overrides():
         assert args[0] == "train.py"
         cfg = [os.path.join(ROOT, a) if not a.startswith("--") else a for a in args[1:]]
         apply_overrides(dict(TRAIN_DEFAULTS), cfg, verbose=False)  # raises on unknown keys / bad types
-
-
-@pytest.mark.parametrize("f", sorted(glob.glob(os.path.join(ROOT, "scripts", "*.sh"))) + [ENTRY])
-def test_shell_syntax(f):
-    subprocess.run(["bash", "-n", f], check=True)
 
 
 def _dry(env, *args):
@@ -163,3 +96,38 @@ def test_multipod_emulation(tmp_path, rdzv):
     assert "tokens per iteration will be: 4,096" in log  # 2 ranks x 1 micro-step x 16 x 128
     assert "iter 6:" in log and "saving checkpoint" in log
     assert (tmp_path / "out" / "ckpt.pt").exists()
+
+
+@pytest.mark.slow
+def test_elastic_restart_resumes_through_entrypoint(tmp_path):
+    """Elastic recovery end to end (README.md:116-120): 2 ranks launched
+    through the real entrypoint with MAX_RESTARTS=1; rank 1 fails at iter 5 (fault
+    injection); torchrun restarts the group, every rank auto-resumes from ckpt.pt at the
+    saved iter_num, the job finishes, and both replicas end bit-identical."""
+    from nanosandbox_amd.data.prepare import synthetic_corpus, write_char_dataset
+    write_char_dataset(str(tmp_path / "datasets" / "shakespeare_char"), synthetic_corpus(60_000))
+    env = dict(os.environ, HOSTNAME="train-singlepod", NNODES="1", NPROC_PER_NODE="2", MAX_RESTARTS="1",
+               PYTHON=sys.executable, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", NSA_PARAM_DIGEST="1",
+               MASTER_ADDR="127.0.0.1")
+    env.pop("POD_NAME", None)
+    env.pop("TORCHELASTIC_RESTART_COUNT", None)
+    p = subprocess.run(
+        ["bash", ENTRY, "--local-addr=127.0.0.1", os.path.join(ROOT, "train.py"),
+         os.path.join(ROOT, "config", "smoke_cpu.py"), f"--data_dir={tmp_path / 'datasets'}",
+         f"--out_dir={tmp_path / 'out'}", "--max_iters=8", "--eval_interval=4", "--eval_iters=2",
+         "--gradient_accumulation_steps=2", "--log_interval=1", "--always_save_checkpoint=True",
+         "--auto_resume=True", "--fault_inject_iter=5", "--fault_inject_rank=1"],
+        env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=str(tmp_path), timeout=400)
+    log = p.stdout
+    assert p.returncode == 0, log[-4000:]
+    assert "injected fault at iter 5 on rank 1" in log
+    assert "auto_resume: found" in log and "Resuming training from" in log
+    assert (tmp_path / "out" / ".fault_injected_rank1").exists()
+    digests = {}
+    for line in log.splitlines():
+        if "param digest rank" in line:
+            parts = line.split("param digest rank ")[1].split()
+            digests[int(parts[0].rstrip(":"))] = (parts[1], int(parts[3]))
+    assert set(digests) == {0, 1}, log[-3000:]
+    assert digests[0] == digests[1]  # identical replicas after the restart
+    assert digests[0][1] == 9  # iterations 0..max_iters ran, the last one after the resume

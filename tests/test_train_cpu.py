@@ -79,10 +79,13 @@ def test_fault_injection_and_auto_resume(cfg, tmp_path):
     with pytest.raises(RuntimeError, match="injected fault"):
         Trainer(c).fit()
     assert (tmp_path / "out" / "ckpt.pt").exists()  # saved at iter 6
-    c2 = dict(cfg, fault_inject_iter=-1, auto_resume=True)
-    tr = Trainer(c2)  # what a torchrun --max-restarts / k8s restart does
+    assert (tmp_path / "out" / ".fault_injected_rank0").exists()
+    # the same job configuration restarted (what torchrun --max-restarts / a k8s restart
+    # does): the fault fired once per job, so the restart resumes at 6 and runs through
+    tr = Trainer(c)
     assert tr.iter_num == 6
     tr.fit()
+    assert tr.iter_num == 13
 
 
 def test_eval_only(cfg, capsys):
