@@ -8,40 +8,50 @@
 //
 // Design (cdna_hip_programming.md §5 "256² 8-phase template", re-derived here):
 //  * 256x256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), each wave 128x64 =
-//    8x4 accumulators of v_mfma_f32_16x16x32_bf16 (swapped operands, so a lane holds
-//    4 consecutive output columns of one row: 8-byte stores straight from registers);
+//    8x4 accumulators of v_mfma_f32_16x16x32_bf16 (swapped operands: a lane holds 4
+//    consecutive output columns of one row);
 //  * one 64-deep K-tile (A image [256][64] + B image [256][64], 64 KiB, two buffers) is
 //    consumed in 4 PHASES of 16 MFMAs, one 64x32 quadrant (qm, qn) per phase in the
 //    order (0,0) (0,1) (1,1) (1,0): fragments are read at the head of the phase that
-//    first needs them (p0: A[qm0] + B[qn0], p1: B[qn1], p2: A[qm1], p3: none);
+//    first needs them (p0: A[qm0], p1: B[qn1], p2: A[qm1]), and phase 3 reads the NEXT
+//    K-tile's B[qn0] (8 / 4 / 8 / 4 fragment reads per phase);
 //  * staging is LDS-DMA only (global_load_lds_dwordx4, no VGPR round trip): each
 //    K-tile is 4 half-tiles of 16 KiB (A rows of quadrant 0 / 1, B columns of quadrant
-//    0 / 1), two 1-KiB pieces per wave each, one half-tile per phase, issued 6 phases
-//    ahead of its first read.  Every per-lane source offset is computed ONCE per kernel
+//    0 / 1), two 1-KiB pieces per wave each, one half-tile per phase, issued in the order
+//    B0 A0 B1 A1 5-6 phases ahead of its first read.  Every per-lane source offset is computed ONCE per kernel
 //    (the XOR swizzle lives in the source address, rule 21); per K-tile only two SGPR
-//    base pointers advance, so a DMA costs no VALU work.  Each phase retires what is
-//    four half-tiles old with `s_waitcnt vmcnt(8)` (never 0 in the loop) and a buffer is
-//    read one phase after that wait (RAW); a half-tile region is refilled >= 2 phases
-//    after its last read (WAR);
+//    base pointers advance, and both pieces of a wave share one M0 write, so a DMA costs
+//    no VALU work.  Each phase retires what is four half-tiles old with `s_waitcnt
+//    vmcnt(8)` (never 0 in the loop) and a buffer is read one phase after that wait
+//    (RAW); a half-tile region is refilled >= 2 phases after its last read (WAR);
 //  * the two wave groups (wm = 0 / 1, one wave of each on every SIMD) run one raw
 //    s_barrier apart, so each phase is [LDS reads + DMA | barrier | 16 MFMA | barrier]
 //    and one group's reads run beside the other group's MFMAs on every SIMD;
 //  * persistent: grid = #CUs, tiles walked in an XCD-grouped order; the DMA stream runs
 //    straight on into the next tile (its first 6 half-tiles are in flight during this
-//    tile's last K-tile), and the epilogue's stores drain under the next tile's MFMAs;
+//    tile's last K-tile);
+//  * epilogue through a wave-private LDS slice into whole-row 16-byte stores (see
+//    store_tile_lds), nontemporal for outputs larger than the Infinity Cache;
 //  * ragged edges without per-lane masks: a tail tile is shifted back inside the
 //    matrix (m0 = min(m0, M - 256)) and only its not-yet-covered rows / columns are
 //    stored, so M, N >= 256 and K % 64 == 0 are the only shape rules.
+//
+// Measured on MI355X (scripts/gemm_nt_ab.py, M = 122880, uniform random operands,
+// interleaved with hipBLASLt in one process; docs/performance.md has the table): the
+// epilogue decides the K = 768 shapes — the accumulator-order stores (16 rows x 64 B per
+// instruction) cost ~30 % of those GEMMs, whole-row stores through LDS and nontemporal
+// stores most of it back; the main loop runs ~73 % MFMA-busy (PMC) at K = 50304.
 #include "common.h"
 
 namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int NTHR = 512;
-constexpr int IMG = BM * BK * 2;  // 32 KiB: one operand's K-tile image [256][64] bf16, 128-B rows
-constexpr int BUF = 2 * IMG;      // A image then B image
-constexpr int SMEM = 2 * BUF;     // two K-tile buffers: 128 KiB
-constexpr int GM = 8;             // grouped tile order: row-blocks per group
+constexpr int IMG = BM * BK * 2;          // 32 KiB: one operand's K-tile image [256][64] bf16, 128-B rows
+constexpr int BUF = 2 * IMG;              // A image then B image
+constexpr int EPI_LDS = 2 * BUF;          // epilogue staging: 4 KiB per wave after the two buffers
+constexpr int SMEM = 2 * BUF + 8 * 4096;  // 160 KiB
+static_assert(SMEM <= 163840, "LDS budget");
 
 enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
@@ -54,21 +64,14 @@ struct NtArgs {
   int M, N, K;
   int lda, ldb, ldc;
   int tiles_m, tiles_n, tiles;
+  int gm;  // grouped tile order: row-blocks per group
 };
 
-// LDS-DMA of one 1-KiB piece: lane l's 16 bytes from sbase + voff land at lds + 16 l
-__device__ __forceinline__ void dma16(const char* sbase, uint32_t voff, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds)
-               : "memory");
-}
-
-// Both 1-KiB pieces of a wave's half-tile share one M0 write: piece 1 lands 1 KiB after
-// piece 0 in LDS, and the instruction offset (applied to the LDS destination AND the
-// global address) provides that 1 KiB, so its per-lane source offset carries -1024.
-// M0 is not preserved: nothing else in these kernels uses it (checked in the .s).
+// LDS-DMA of a wave's two 1-KiB pieces of a half-tile: lane l's 16 bytes from sbase + voff
+// land at lds + 16 l.  Piece 1 lands 1 KiB after piece 0 in LDS, and the instruction offset
+// (applied to the LDS destination AND the global address) provides that 1 KiB, so its
+// per-lane source offset carries -1024.  One M0 write for both.  M0 is not preserved:
+// nothing else in this kernel uses it (checked in the .s).
 __device__ __forceinline__ void dma16x2(const char* sbase, uint32_t voff0, uint32_t voff1m, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %3\n\tglobal_load_lds_dwordx4 %1, %3 offset:1024"
                :
@@ -86,13 +89,13 @@ __device__ __forceinline__ bf16x8 rd16(const char* p) {
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
 }
 
-// tile sequence number -> (row, col) origin, grouped GM row-blocks x all columns; tail
+// tile sequence number -> (row, col) origin, grouped g.gm row-blocks x all columns; tail
 // tiles are shifted back inside the matrix (lo = first row / column this tile owns)
 __device__ __forceinline__ void tile_coords(const NtArgs& g, int seq, int& m0, int& n0, int& mlo, int& nlo) {
-  const int per = GM * g.tiles_n;
+  const int per = g.gm * g.tiles_n;
   const int grp = seq / per;
-  const int first = grp * GM;
-  const int gm = min(GM, g.tiles_m - first);
+  const int first = grp * g.gm;
+  const int gm = min(g.gm, g.tiles_m - first);
   const int in = seq - grp * per;
   mlo = (first + in % gm) * BM;
   nlo = (in / gm) * BN;
@@ -132,82 +135,100 @@ __device__ __forceinline__ void cur_next(const NtArgs& g, Cur& c, int nk, int G)
   }
 }
 
-// Store one 64x32 quadrant (qm, qn) of a wave's 128x64 accumulator tile.  Lane
-// (r = lane & 15, q = lane >> 4) holds C[16 i + r][16 j + 4 q + e]; v_permlane16_swap on the
-// packed accumulator pair (j, j+1) gives every lane 8 consecutive columns (q even: tile j,
-// q odd: tile j+1; columns 8 (q >> 1) ..), so a quadrant leaves in 4 dwordx4 stores (64
-// contiguous bytes per row) instead of 8 dwordx2 (the store tail is issue-bound,
-// cdna_hip_programming.md T21).
-template <int EPI, bool LANE_ROWMAJOR = false>
-__device__ __forceinline__ void store_quad(const NtArgs& g, const f32x4 (&acc)[8][4], int qm, int qn, int m0, int n0,
-                                           int mlo, int nlo, int wm, int wn, int lane) {
-  const int q = lane >> 4;
-  const bool full = (m0 == mlo) & (n0 == nlo);  // wave-uniform: no row / column masks
-  const int col = LANE_ROWMAJOR ? n0 + wn * 64 + 32 * qn + 8 * (lane & 3)
-                                : n0 + wn * 64 + 32 * qn + 16 * (q & 1) + 8 * (q >> 1);
+typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void st16(bf16_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(nt_u32x4{a, b, c, d}, reinterpret_cast<nt_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+  }
+}
+
+// Epilogue through a wave-private 4-KiB LDS slice (the 32 KiB after the two K-tile buffers,
+// which no DMA touches, so it needs no barrier against the next tile's staging).  In the
+// accumulator layout consecutive lanes hold different rows, so a store straight from the
+// registers writes 16 rows x 64 B per instruction with no two adjacent lanes contiguous;
+// re-shaped through LDS, each store instruction writes 8 whole 128-byte row segments (lane
+// l: row l / 8, 16-byte chunk l % 8).  Four rounds of 32 rows x 64 columns per wave.  Image:
+// row r at 128 r, 16-byte chunk c at (c ^ (r & 7)) * 16 (writes 2-way, reads conflict-free).
+// EPI_DGELU: the U pieces of two rounds are in flight at a time (the first two before the
+// first round), so their latency runs under the LDS re-shaping and the other round's stores.
+template <int EPI, bool NT>
+__device__ __forceinline__ void store_tile_lds(const NtArgs& g, const f32x4 (&acc)[8][4], char* stage, int m0, int n0,
+                                               int mlo, int nlo, int wm, int wn, int lane) {
+  const bool full = (m0 == mlo) & (n0 == nlo);
+  const int r = lane & 15, q = lane >> 4;
+  const int rr = lane >> 3, cc = lane & 7;  // read / store lane map
+  const int col = n0 + wn * 64 + 8 * cc;
+  nt_u32x4 uv[2][4];  // U of rounds rd and rd + 1 (two rounds in flight)
+  auto load_u = [&](int rd, nt_u32x4 (&dst)[4]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = m0 + wm * 128 + 16 * (qm * 4 + i) + (LANE_ROWMAJOR ? (lane >> 2) : (lane & 15));
-    const f32x4 t0 = acc[qm * 4 + i][qn * 2], t1 = acc[qm * 4 + i][qn * 2 + 1];
-    const auto sl = __builtin_amdgcn_permlane16_swap(pack2(t0[0], t0[1]), pack2(t1[0], t1[1]), false, false);
-    const auto sh = __builtin_amdgcn_permlane16_swap(pack2(t0[2], t0[3]), pack2(t1[2], t1[3]), false, false);
-    uint32_t w[4] = {sl[0], sh[0], sl[1], sh[1]};
-    if (!full && (row < mlo || col < nlo)) continue;
-    const int64_t off = (int64_t)row * g.ldc + col;
-    if constexpr (EPI == EPI_DGELU) {
-      const uint4 u = *reinterpret_cast<const uint4*>(g.U + off);
-      const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int grow = m0 + wm * 128 + 32 * rd + 8 * s2 + rr;  // in bounds: tiles lie inside the matrix
+      dst[s2] = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(g.U + (int64_t)grow * g.ldc + col));
+    }
+  };
+  if constexpr (EPI == EPI_DGELU) {
+    load_u(0, uv[0]);
+    load_u(1, uv[1]);
+  }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(uu[e] << 16));
-        const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(uu[e] & 0xffff0000u));
-        w[e] = pack2(a0, a1);
+  for (int rd = 0; rd < 4; ++rd) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int row = 16 * i2 + r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 t = acc[2 * rd + i2][j];
+        const int chunk = (2 * j + (q >> 1)) ^ (row & 7);
+        *reinterpret_cast<uint2*>(stage + row * 128 + chunk * 16 + (q & 1) * 8) =
+            make_uint2(pack2(t[0], t[1]), pack2(t[2], t[3]));
       }
     }
-    *reinterpret_cast<uint4*>(g.C + off) = make_uint4(w[0], w[1], w[2], w[3]);
-    if constexpr (EPI == EPI_GELU) {
-      // gelu of the bf16-rounded pre-activation: what a separate GELU kernel would see
-      uint32_t gg[4];
+    uint4 v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
-      *reinterpret_cast<uint4*>(g.C2 + off) = make_uint4(gg[0], gg[1], gg[2], gg[3]);
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int row = 8 * s2 + rr;
+      v[s2] = *reinterpret_cast<const uint4*>(stage + row * 128 + ((cc ^ (row & 7)) << 4));
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int grow = m0 + wm * 128 + 32 * rd + 8 * s2 + rr;
+      if (!full && (grow < mlo || col < nlo)) continue;
+      const int64_t off = (int64_t)grow * g.ldc + col;
+      uint32_t w[4] = {v[s2].x, v[s2].y, v[s2].z, v[s2].w};
+      if constexpr (EPI == EPI_DGELU) {
+        const nt_u32x4 ur = uv[rd & 1][s2];
+        const uint32_t uu[4] = {ur[0], ur[1], ur[2], ur[3]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(uu[e] << 16));
+          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(uu[e] & 0xffff0000u));
+          w[e] = pack2(a0, a1);
+        }
+      }
+      st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
+      if constexpr (EPI == EPI_GELU) {
+        // gelu of the bf16-rounded pre-activation: what a separate GELU kernel would see
+        uint32_t gg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
+        st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
+      }
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      if (rd + 2 < 4) load_u(rd + 2, uv[rd & 1]);
     }
   }
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n (multiples of 4 up to 60; larger waits for 60)
-__device__ __forceinline__ void vm_wait_dyn(int n) {
-  if (n >= 60) asm volatile("s_waitcnt vmcnt(60)" ::: "memory");
-  else if (n >= 56) asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
-  else if (n >= 52) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
-  else if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-  else if (n >= 44) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
-  else if (n >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-  else if (n >= 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  else if (n >= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
-  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 }  // namespace
 
-// PROBE (timing only, wrong results): 1 = no DMA after the prologue, 2 = no vmcnt waits in
-// the loop, 3 = only one of the two pieces per phase, 4 = no epilogue stores (VAR 1), 5 =
-// PROBE 1 with VAR 1, 6 / 7 = workgroup start times staggered (VAR 1 / 0), 8 = epilogue
-// stores with row-major lane order (data misplaced; coalescing probe).
-// VAR 0: the epilogue of tile i is spread over the first K-tile of tile i+1 (quadrant p
-// leaves in phase p's LDS-read segment, right before phase p's MFMAs overwrite it), so the
-// stores interleave with the MFMAs of the other wave group instead of stalling it in one
-// burst; VAR 1: the whole epilogue between the tiles.  (EPI_DGELU always uses VAR 1: its U
-// loads would stall a spread epilogue phase by phase.)
-template <int EPI, int PROBE, int VAR>
+// NT: nontemporal epilogue stores.  PROBE (timing only, wrong results): 1 = no DMA after
+// the prologue (stale LDS), 4 = no epilogue stores.
+template <int EPI, bool NT, int PROBE, bool BAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -225,34 +246,34 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
     v = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + v / 8;
   }
   if (v >= g.tiles) return;
-  if constexpr (PROBE == 6) {
-    // probe: desynchronise the workgroups' tile boundaries (epilogue store bursts)
-    for (int d = 0; d < (v & 7); ++d) __builtin_amdgcn_s_sleep(80);
-  }
 
   // ---- per-lane DMA source offsets (bytes from the K-tile's row base), fixed for the kernel.
   // Half h of A = rows {r : (r >> 6) & 1 == h}; piece pc = 2 wave + j covers 8 rows.
   // Half h of B = columns {c : (c >> 5) & 1 == h}.  Image row r, physical 16-B chunk p
   // holds logical chunk p ^ ((r >> 1) & 7).
-  constexpr bool NODMA = PROBE == 1;
-  uint32_t voA[2][2], voB[2][2];
-  uint32_t ldA[2][2], ldB[2][2];
+  uint32_t voA[2], voB[2], voA1m[2], voB1m[2];  // [half]: piece 0, piece 1 - 1024
+  uint32_t ldA[2], ldB[2];                      // [half]: LDS address of piece 0
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int pc = 2 * wave + j;
       const int rbA = (pc >> 3) * 128 + h * 64 + (pc & 7) * 8;
       const int rbB = (pc >> 2) * 64 + h * 32 + (pc & 3) * 8;
       const int ra = rbA + (lane >> 3), rb = rbB + (lane >> 3);
-      voA[h][j] = (uint32_t)(ra * g.lda * 2 + (((lane & 7) ^ ((ra >> 1) & 7)) << 4));
-      voB[h][j] = (uint32_t)(rb * g.ldb * 2 + (((lane & 7) ^ ((rb >> 1) & 7)) << 4));
-      ldA[h][j] = lds0 + (uint32_t)(rbA * 128);
-      ldB[h][j] = lds0 + (uint32_t)(IMG + rbB * 128);
+      const uint32_t oa = (uint32_t)(ra * g.lda * 2 + (((lane & 7) ^ ((ra >> 1) & 7)) << 4));
+      const uint32_t ob = (uint32_t)(rb * g.ldb * 2 + (((lane & 7) ^ ((rb >> 1) & 7)) << 4));
+      if (j == 0) {
+        voA[h] = oa;
+        voB[h] = ob;
+        ldA[h] = lds0 + (uint32_t)(rbA * 128);
+        ldB[h] = lds0 + (uint32_t)(IMG + rbB * 128);
+      } else {  // rows 8 apart in the image = 1 KiB after piece 0 in LDS (dma16x2)
+        voA1m[h] = oa - 1024u;
+        voB1m[h] = ob - 1024u;
+      }
     }
-  // pieces 0 / 1 of a half are rows 8 apart in the image: 1 KiB apart in LDS (dma16x2)
-  const uint32_t voA1m[2] = {voA[0][1] - 1024u, voA[1][1] - 1024u};
-  const uint32_t voB1m[2] = {voB[0][1] - 1024u, voB[1][1] - 1024u};
+  }
 
   // ---- fragment read offsets: row wm*128 + 16 i + (lane & 15) (A) / wn*64 + ... (B),
   // logical chunk 4 kk + (lane >> 4)
@@ -265,59 +286,59 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
     offB[kk] = IMG + (wn * 64 + (lane & 15)) * 128 + ch;
   }
 
-  // ---- DMA stream: c1 = the K-tile after the one being multiplied, c2 = the one after that
+  // half-tile kinds: 0 = A half 0, 1 = B half 0, 2 = B half 1, 3 = A half 1
+  auto issue_half = [&](const Cur& c, int kind) {
+    if (kind == 0 || kind == 3) {
+      const int h = kind == 3;
+      dma16x2(c.a, voA[h], voA1m[h], ldA[h] + c.buf);
+    } else {
+      const int h = kind == 2;
+      dma16x2(c.b, voB[h], voB1m[h], ldB[h] + c.buf);
+    }
+  };
+
+  // ---- DMA stream: c1 = the K-tile after the one being multiplied, c2 = the one after that.
+  // Prologue: K-tile 0 (all four half-tiles) and K-tile 1's A0 / B0.
   Cur c1, c2;
   c1.buf = 0;
   cur_set_tile(g, c1, v);
-  // kind: 0 = A half 0, 1 = B half 0, 2 = B half 1, 3 = A half 1; piece j = 0 / 1.  NODMA
-  // (timing probe): only the prologue stages anything, later K-tiles re-read stale LDS
-  auto issue_piece = [&](const Cur& c, int kind, int j, bool prologue) {
-    if (!NODMA || prologue) {
-      if (kind == 0 || kind == 3) {
-        const int h = kind == 3;
-        dma16(c.a, voA[h][j], ldA[h][j] + c.buf);
-      } else {
-        const int h = kind == 2;
-        dma16(c.b, voB[h][j], ldB[h][j] + c.buf);
-      }
-    }
-  };
-  // prologue: K-tile 0 (all four half-tiles) and K-tile 1's A0 / B0
-#pragma unroll
-  for (int kind = 0; kind < 4; ++kind) {
-    issue_piece(c1, kind, 0, true);
-    issue_piece(c1, kind, 1, true);
-  }
+  // stream order per K-tile: B0, A0, B1, A1 (BAL) / A0, B0, B1, A1
+  issue_half(c1, BAL ? 1 : 0);
+  issue_half(c1, BAL ? 0 : 1);
+  issue_half(c1, 2);
+  issue_half(c1, 3);
   c2 = c1;
   cur_next(g, c2, nk, G);
-  bool more = c2.valid;
-  if (more) {
-    issue_piece(c2, 0, 0, true);
-    issue_piece(c2, 0, 1, true);
-    issue_piece(c2, 1, 0, true);
-    issue_piece(c2, 1, 1, true);
+  if (c2.valid) {
+    issue_half(c2, BAL ? 1 : 0);
+    issue_half(c2, BAL ? 0 : 1);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  // the multiplied K-tile's buffer; c1 <- K-tile 1, c2 <- K-tile 2
-  uint32_t bufc = 0;
+  uint32_t bufc = 0;  // the multiplied K-tile's buffer
   c1 = c2;
   cur_next(g, c2, nk, G);
   raw_barrier();
   if (wm == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
 
-  constexpr bool SPREAD = VAR == 0 && EPI != EPI_DGELU;
-  constexpr int SPQ = EPI == EPI_GELU ? 8 : 4;  // VMEM stores per spread quadrant
   int seq = v;
-  bool has_prev = false;  // a finished tile's accumulators wait to be stored (SPREAD)
-  int pm0 = 0, pn0 = 0, pmlo = 0, pnlo = 0;
-  int w1 = 0, w2 = 0, w3 = 0;  // stores issued in the previous 3 phases (vmcnt accounting)
   f32x4 acc[8][4];
-  bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+  bf16x8 af[4][2], b0f[2][2], b1f[2][2], b0n[2][2];
+  // B0 of K-tile 0 (retired with A0 by the prologue's wait); afterwards each K-tile's
+  // phase 3 reads the NEXT K-tile's B0, so the read load per phase is 8 / 4 / 8 / 4
+  // fragments instead of 12 / 4 / 8 / 0
+  if constexpr (BAL) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) b0f[j][kk] = rd16(smem + offB[kk] + (16 * j) * 128);
+  }
 
-// LDS fragment reads of phase P
-#define NT_READS(P)                                                                             \
+// one phase: P = 0..3, FIRST = first K-tile of an output tile (kk = 0 MFMAs start from 0).
+// [LDS reads | DMA of half-tile P+6 + counted wait retiring what phase P+1 reads | barrier |
+//  16 MFMAs | barrier]
+#define NT_PHASE(P, FIRST)                                                                      \
   {                                                                                            \
     const char* base_ = smem + bufc;                                                           \
     if (P == 0 || P == 2) {                                                                    \
@@ -325,63 +346,32 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
       _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
         af[i][kk] = rd16(base_ + offA[kk] + ((P >> 1) * 64 + 16 * i) * 128);                   \
     }                                                                                          \
-    if (P == 0) {                                                                              \
+    if (!BAL && P == 0) {                                                                      \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
       _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
         b0f[j][kk] = rd16(base_ + offB[kk] + (16 * j) * 128);                                  \
+    }                                                                                          \
+    if (BAL && P == 3) { /* the next K-tile's B0 (other buffer): b0n -> b0f after the MFMAs */ \
+      const char* nb_ = smem + (bufc ^ (uint32_t)BUF);                                         \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
+        b0n[j][kk] = rd16(nb_ + offB[kk] + (16 * j) * 128);                                    \
     }                                                                                          \
     if (P == 1) {                                                                              \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
       _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
         b1f[j][kk] = rd16(base_ + offB[kk] + (32 + 16 * j) * 128);                             \
     }                                                                                          \
-  }
-// DMA of phase P (half-tile P+6 of the stream) + the counted wait retiring what phase P+1 reads
-#define NT_DMA_WAIT(P)                                                                          \
-  {                                                                                            \
-    const Cur& cc_ = (P < 2) ? c1 : c2;                                                        \
-    constexpr int kind_ = P == 0 ? 2 : P == 1 ? 3 : P == 2 ? 0 : 1;                            \
-    if (cc_.valid) {                                                                           \
-      if constexpr (PROBE == 1) {                                                              \
-      } else if constexpr (PROBE == 3) {                                                       \
-        issue_piece(cc_, kind_, 0, false);                                                     \
-      } else if constexpr (VAR == 1) {                                                         \
-        issue_piece(cc_, kind_, 0, false);                                                     \
-        issue_piece(cc_, kind_, 1, false);                                                     \
-      } else if constexpr (kind_ == 0 || kind_ == 3) {                                         \
-        constexpr int h_ = kind_ == 3;                                                         \
-        dma16x2(cc_.a, voA[h_][0], voA1m[h_], ldA[h_][0] + cc_.buf);                           \
-      } else {                                                                                 \
-        constexpr int h_ = kind_ == 2;                                                         \
-        dma16x2(cc_.b, voB[h_][0], voB1m[h_], ldB[h_][0] + cc_.buf);                           \
-      }                                                                                        \
-      if constexpr (PROBE == 2) {                                                              \
-      } else if constexpr (PROBE == 3) {                                                       \
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                      \
-      } else if constexpr (SPREAD) {                                                           \
-        vm_wait_dyn(8 + st_ + w1 + w2 + w3);                                                   \
-      } else {                                                                                 \
+    {                                                                                          \
+      const Cur& cc_ = (P < 2) ? c1 : c2;                                                      \
+      if (cc_.valid) {                                                                         \
+        if constexpr (PROBE != 1)                                                              \
+          issue_half(cc_, P == 0 ? 2 : P == 1 ? 3 : P == 2 ? (BAL ? 1 : 0) : (BAL ? 0 : 1));     \
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                      \
-      }                                                                                        \
-    } else {                                                                                   \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
-    }                                                                                          \
-  }
-// one phase: P = 0..3, FIRST = first K-tile of an output tile (kk = 0 MFMAs start from 0)
-#define NT_PHASE(P, FIRST)                                                                      \
-  {                                                                                            \
-    int st_ = 0;                                                                               \
-    if constexpr (SPREAD && (FIRST)) {                                                         \
-      if (has_prev) {                                                                          \
-        store_quad<EPI>(g, acc, P == 2 || P == 3, P == 1 || P == 2, pm0, pn0, pmlo, pnlo, wm, wn, lane); \
-        st_ = SPQ;                                                                             \
+      } else {                                                                                 \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
       }                                                                                        \
     }                                                                                          \
-    NT_READS(P)                                                                                \
-    NT_DMA_WAIT(P)                                                                             \
-    w3 = w2;                                                                                   \
-    w2 = w1;                                                                                   \
-    w1 = st_;                                                                                  \
     raw_barrier();                                                                             \
     __builtin_amdgcn_s_setprio(1);                                                             \
     {                                                                                          \
@@ -396,6 +386,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
       }                                                                                        \
     }                                                                                          \
     __builtin_amdgcn_s_setprio(0);                                                             \
+    if (BAL && P == 3) {                                                                       \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) b0f[j][kk] = b0n[j][kk];                \
+    }                                                                                          \
     raw_barrier();                                                                             \
   }
 #define NT_KTILE(FIRST)              \
@@ -412,21 +406,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
   while (true) {
     NT_KTILE(true)
     for (int t = 1; t < nk; ++t) NT_KTILE(false)
-
     int m0, n0, mlo, nlo;
     tile_coords(g, seq, m0, n0, mlo, nlo);
-    if constexpr (SPREAD) {
-      has_prev = true;
-      pm0 = m0;
-      pn0 = n0;
-      pmlo = mlo;
-      pnlo = nlo;
-    } else if constexpr (PROBE != 4) {
-#pragma unroll
-      for (int qd = 0; qd < 4; ++qd)
-        store_quad<EPI, PROBE == 8>(g, acc, qd >> 1, qd & 1, m0, n0, mlo, nlo, wm, wn, lane);
+    if constexpr (PROBE != 4) {
+      store_tile_lds<EPI, NT>(g, acc, smem + EPI_LDS + wave * 4096, m0, n0, mlo, nlo, wm, wn, lane);
     } else {
-      // probe: keep the accumulators live without storing them
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -435,26 +419,25 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
     seq += G;
     if (seq >= g.tiles) break;
   }
-  if constexpr (SPREAD) {  // the last tile's epilogue has no next tile to hide under
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) store_quad<EPI>(g, acc, qd >> 1, qd & 1, pm0, pn0, pmlo, pnlo, wm, wn, lane);
-  }
 #undef NT_KTILE
 #undef NT_PHASE
-#undef NT_READS
-#undef NT_DMA_WAIT
   if (wm == 0) raw_barrier();  // close the stagger: both groups end at the same barrier count
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// epi: 0 = bf16 store, 1 = u + gelu(u) into C / C2, 2 = acc * gelu'(U); bits 8-11: timing
-// probe (see the kernel; wrong results); bits 12-15: variant.  grid = persistent workgroup count (#CUs).
+// epi: 0 = bf16 store, 1 = u + gelu(u) into C / C2, 2 = acc * gelu'(U).
+// bits 8-11: timing probe (1 no DMA, 4 no stores; wrong results).  bits 12-13: epilogue
+// store policy (0 = nontemporal when the output exceeds the 256 MiB Infinity Cache,
+// 1 = always, 2 = never); bit 14: phase-3 B0 prefetch off (A/B); bits 16-23: row-blocks
+// per tile group (0 = automatic).  grid = persistent workgroup count (#CUs).
 NSA_API hipError_t nsa_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
                                const void* U, int M, int N, int K, int grid, hipStream_t s) {
+  const int epi_full = epi;
   const int probe = (epi >> 8) & 0xf;
-  const int var = (epi >> 12) & 0xf;
+  const int stp = (epi >> 12) & 0x3;
+  const bool bal = !((epi >> 14) & 1);
   epi &= 0xff;
-  if (M < BM || N < BN || K < BK || K % BK != 0 || lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K ||
+  if (M < BM || N < BN || K < BK || K % BK != 0 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K ||
       ldc < N || grid < 1)
     return hipErrorInvalidValue;
   if ((int64_t)BM * lda * 2 >= (1ll << 31) || (int64_t)BN * ldb * 2 >= (1ll << 31)) return hipErrorInvalidValue;
@@ -474,18 +457,21 @@ NSA_API hipError_t nsa_gemm_nt(int epi, const void* A, int lda, const void* B, i
   a.tiles_m = (M + BM - 1) / BM;
   a.tiles_n = (N + BN - 1) / BN;
   a.tiles = a.tiles_m * a.tiles_n;
+  // Tile order.  The 32 workgroups of an XCD take 32 consecutive tiles.  Narrow outputs
+  // (<= 16 column tiles: every GPT-2 linear but the lm_head) go row-major, so a row panel of
+  // A — streamed from HBM when K is large — is read by all its column tiles on one XCD at
+  // the same time; wide outputs (the lm_head's 197 column tiles) in groups of 8 row-blocks.
+  const int gmsel = (epi_full >> 16) & 0xff;
+  a.gm = gmsel ? gmsel : (a.tiles_n <= 16 ? 1 : 8);
+  const int64_t out_bytes = (int64_t)M * N * 2 * (epi == EPI_GELU ? 2 : 1);
+  const bool nt = stp == 1 || (stp == 0 && out_bytes >= NSA_NT_MIN_BYTES);
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
-#define NT_LAUNCH(E)                                                        \
-  if (probe == 1) gemm_nt_kernel<E, 1, 0><<<gr, NTHR, 0, s>>>(a);           \
-  else if (probe == 2) gemm_nt_kernel<E, 2, 0><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 3) gemm_nt_kernel<E, 3, 0><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 4) gemm_nt_kernel<E, 4, 1><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 5) gemm_nt_kernel<E, 1, 1><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 6) gemm_nt_kernel<E, 6, 1><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 7) gemm_nt_kernel<E, 6, 0><<<gr, NTHR, 0, s>>>(a);      \
-  else if (probe == 8) gemm_nt_kernel<E, 8, 1><<<gr, NTHR, 0, s>>>(a);      \
-  else if (var == 1) gemm_nt_kernel<E, 0, 1><<<gr, NTHR, 0, s>>>(a);        \
-  else gemm_nt_kernel<E, 0, 0><<<gr, NTHR, 0, s>>>(a);
+#define NT_LAUNCH(E)                                                          \
+  if (probe == 1) gemm_nt_kernel<E, true, 1, true><<<gr, NTHR, 0, s>>>(a);    \
+  else if (probe == 4) gemm_nt_kernel<E, true, 4, true><<<gr, NTHR, 0, s>>>(a); \
+  else if (!bal) gemm_nt_kernel<E, true, 0, false><<<gr, NTHR, 0, s>>>(a);    \
+  else if (nt) gemm_nt_kernel<E, true, 0, true><<<gr, NTHR, 0, s>>>(a);       \
+  else gemm_nt_kernel<E, false, 0, true><<<gr, NTHR, 0, s>>>(a);
   switch (epi) {
     case EPI_BF16: NT_LAUNCH(EPI_BF16) break;
     case EPI_GELU: NT_LAUNCH(EPI_GELU) break;

@@ -334,10 +334,11 @@ class GPT(nn.Module):
         return idx
 
     @torch.no_grad()
-    def generate_cached(self, idx, max_new_tokens, temperature=1.0, top_k=None, use_graph=None):
+    def generate_cached(self, idx, max_new_tokens, temperature=1.0, top_k=None, use_graph=None, decoder=None):
         """``generate`` with per-layer KV caches: the prompt is encoded once and every
         new token runs one position through the model (a replayed HIP graph on the GPU;
         ``runtime/decode.py``).  Same sampling; falls back to ``generate`` when prompt +
         new tokens exceed block_size."""
         from ..runtime.decode import generate_cached
-        return generate_cached(self, idx, max_new_tokens, temperature=temperature, top_k=top_k, use_graph=use_graph)
+        return generate_cached(self, idx, max_new_tokens, temperature=temperature, top_k=top_k, use_graph=use_graph,
+                               decoder=decoder)

@@ -243,10 +243,12 @@ class EmbeddingFn(torch.autograd.Function):
             assert dx.dtype in (F32, BF16)
             if _tune.DETERMINISTIC:
                 # atomic-free: token positions stably sorted by id, one writer per vocab row
+                # segment starts by binary search over the sorted ids: no host sync
+                # (torch.bincount reads its max back to the host, which HIP-graph
+                # capture forbids)
                 flat = idx.view(-1)
-                order = torch.argsort(flat, stable=True)
-                seg = torch.zeros(V + 1, device=dx.device, dtype=torch.int64)
-                torch.cumsum(torch.bincount(flat, minlength=V), 0, out=seg[1:])
+                ids, order = torch.sort(flat, stable=True)
+                seg = torch.searchsorted(ids, torch.arange(V + 1, device=dx.device, dtype=ids.dtype))
                 _lib.call("nsa_embedding_bwd_det", _lib.ptr(order), _lib.ptr(seg), _lib.ptr(dx), _lib.ptr(gwte),
                           _lib.ptr(gwpe), B, T, C, V, 1 if dx.dtype == F32 else 0, ctx.p, ctx.seed, _lib.stream())
             else:
@@ -545,7 +547,7 @@ class MLPFn(torch.autograd.Function):
             return dx.view(ctx.xshape), gw_fc, out["gw"]
         gw_proj = weight_grad(w_proj, dy2, g)
         if FUSE_GELU_EPILOGUE:
-            du = _gemm.dgrad(dy2, wp, u=u)
+            du = _gemm.dgrad(dy2, wp, u=u, wt=_tune._wt(wp))
         else:
             du = _tune.dgrad_dgelu(dy2, wp, u)
         gw_fc = weight_grad(w_fc, du, x2)

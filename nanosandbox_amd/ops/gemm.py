@@ -1,14 +1,13 @@
-"""Python front-end of our gfx950 MFMA GEMM (``csrc/kernels/gemm.hip``).
+"""Python front-end of our gfx950 MFMA GEMMs.
 
-Three layouts cover every nn.Linear GEMM of training (no transposed copies):
-
-* ``fwd(x, w)``            Y  = X · W^T            (x [M,K], w [N,K])
-* ``dgrad(dy, w)``         dX = dY · W             (dy [M,N], w [N,K])
-* ``wgrad_acc(dy, x, g)``  g += dY^T · X  (fp32)   split over the token dim,
-                                                    atomically accumulated into the
-                                                    flat fp32 gradient (no bf16 dW)
-plus fused epilogues: ``fwd_gelu`` (pre-activation + GELU in one pass) and
-``dgrad_dgelu`` (dX * gelu'(u), the MLP backward through the activation).
+* ``nt(a, b)``             C  = A · B^T   (both K-contiguous; ``csrc/kernels/gemm_nt.hip``):
+                                           every forward Y = X · W^T and, on the cached
+                                           weight transpose, every input grad dX = dY · W;
+                                           fused GELU / GELU' epilogues
+* ``fwd``, ``dgrad``, ``fwd_gelu``         convenience wrappers over ``nt``
+* ``wgrad_acc(dy, x, g)``  g += dY^T · X  (fp32; ``csrc/kernels/gemm.hip``) split over the
+                                           token dim, atomically accumulated into the flat
+                                           fp32 gradient (no bf16 dW)
 """
 
 from __future__ import annotations
@@ -20,12 +19,11 @@ import torch
 from . import _lib
 
 BF16 = torch.bfloat16
-LAYOUT_NT, LAYOUT_NN, LAYOUT_TN = 0, 1, 2
-EPI_STORE, EPI_ATOMIC, EPI_GELU, EPI_DGELU, EPI_STORE_F32 = 0, 1, 2, 3, 4
+LAYOUT_TN = 2
+EPI_ATOMIC, EPI_STORE_F32 = 1, 4
 BK = 64
 TILE = 256
-# pipeline variant (csrc/kernels/gemm.hip nsa_gemm): 0 = register-staged, 1-4 = 32-deep LDS-DMA ring,
-# 5/6 = pipelined ring, 7/8 = ring64 (default 7)
+# weight-grad variant (csrc/kernels/gemm.hip nsa_gemm): 1 = ring (32-deep slices), 7 = ring64 (default)
 VARIANT = int(os.environ.get("NSA_GEMM_VARIANT", "7"))
 
 
@@ -40,61 +38,10 @@ def supported(M, N, K) -> bool:
     return M % 8 == 0 and N % 8 == 0 and K % BK == 0 and M >= 8 and N >= 8
 
 
-def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, C2=None, U=None, variant=None):
+def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, variant=None):
     epi = epi | ((VARIANT if variant is None else variant) << 8)
-    _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, _lib.ptr(C2),
-              _lib.ptr(U), M, N, K, splits, _lib.stream())
-
-
-def fwd(x2, w, epi=EPI_STORE, variant=None):
-    M, K = x2.shape
-    N = w.shape[0]
-    _check(x2, "x")
-    _check(w, "w")
-    out = torch.empty(M, N, device=x2.device, dtype=BF16)
-    if epi == EPI_GELU:
-        act = torch.empty_like(out)
-        _call(LAYOUT_NT, EPI_GELU, x2, K, w, K, out, N, M, N, K, C2=act, variant=variant)
-        return out, act
-    _call(LAYOUT_NT, EPI_STORE, x2, K, w, K, out, N, M, N, K, variant=variant)
-    return out
-
-
-def fwd_gelu(x2, w, variant=None):
-    """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
-    return fwd(x2, w, epi=EPI_GELU, variant=variant)
-
-
-def dgrad(dy2, w, u=None, variant=None):
-    """dX = dY @ W; with ``u`` also multiplies by gelu'(u) (fused activation backward)."""
-    M, N = dy2.shape
-    K = w.shape[1]
-    _check(dy2, "dy")
-    _check(w, "w")
-    out = torch.empty(M, K, device=dy2.device, dtype=BF16)
-    if u is not None:
-        _check(u, "u")
-        _call(LAYOUT_NN, EPI_DGELU, dy2, N, w, K, out, K, M, K, N, U=u, variant=variant)
-    else:
-        _call(LAYOUT_NN, EPI_STORE, dy2, N, w, K, out, K, M, K, N, variant=variant)
-    return out
-
-
-def dgrad_t(dy2, wt, u=None, variant=None):
-    """dX = dY @ W from the cached K-contiguous transpose ``wt`` = W^T ([K_in, N_out]):
-    the forward's NT layout (ds_read_b128 fragments for both operands instead of the
-    NN layout's transposed reads); with ``u`` also multiplies by gelu'(u)."""
-    M, N = dy2.shape
-    K = wt.shape[0]
-    _check(dy2, "dy")
-    _check(wt, "wt")
-    out = torch.empty(M, K, device=dy2.device, dtype=BF16)
-    if u is not None:
-        _check(u, "u")
-        _call(LAYOUT_NT, EPI_DGELU, dy2, N, wt, N, out, K, M, K, N, U=u, variant=variant)
-    else:
-        _call(LAYOUT_NT, EPI_STORE, dy2, N, wt, N, out, K, M, K, N, variant=variant)
-    return out
+    _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, None, None,
+              M, N, K, splits, _lib.stream())
 
 
 # ---------------------------------------------------------------------------------
@@ -116,16 +63,16 @@ def nt_supported(M, N, K) -> bool:
     return M >= 256 and N >= 256 and K >= BK and K % BK == 0 and N % 8 == 0
 
 
-NT_VAR = int(os.environ.get("NSA_NT_VAR", "0"))
+NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 
-def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None):
+def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None, gm=0):
     var = NT_VAR if var is None else var
-    _lib.call("nsa_gemm_nt", epi | (probe << 8) | (var << 12), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
+    _lib.call("nsa_gemm_nt", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
               C.stride(0), _lib.ptr(C2), _lib.ptr(U), M, N, K, grid or num_cus(A.device), _lib.stream())
 
 
-def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None):
+def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0):
     """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the persistent kernel.
 
     epi NT_EPI_GELU returns (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u)."""
@@ -136,14 +83,33 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None):
     out = torch.empty(M, N, device=a.device, dtype=BF16)
     if epi == NT_EPI_GELU:
         act = torch.empty_like(out)
-        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var)
+        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var, gm=gm)
         return out, act
     if epi == NT_EPI_DGELU:
         _check(u, "u")
-        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var)
+        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var, gm=gm)
         return out
-    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var)
+    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var, gm=gm)
     return out
+
+
+def fwd(x2, w):
+    """Y = X · W^T (nn.Linear forward, bf16)."""
+    return nt(x2, w)
+
+
+def fwd_gelu(x2, w):
+    """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
+    return nt(x2, w, epi=NT_EPI_GELU)
+
+
+def dgrad(dy2, w, u=None, wt=None):
+    """dX = dY · W through W^T (``wt``, K-contiguous; transposed here when not given);
+    with ``u`` also multiplied by gelu'(u)."""
+    wt = w.t().contiguous() if wt is None else wt
+    if u is None:
+        return nt(dy2, wt)
+    return nt(dy2, wt, epi=NT_EPI_DGELU, u=u)
 
 
 def wgrad_splits(n_out, n_in, tokens, cus=256):

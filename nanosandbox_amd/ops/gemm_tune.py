@@ -14,13 +14,14 @@ from one pass) and ``dgrad_dgelu`` (dY·W scaled by gelu'(u)) time the fused
 epilogue variants of our kernel against "best GEMM + standalone GELU kernel",
 so a fusion is used exactly where it measures faster.
 
-Candidate names: ``hipblaslt``, ``nsa<v>`` (our kernel, pipeline variant v of
-``csrc/kernels/gemm.hip``: 1 = 32-deep LDS-DMA ring, 7/8 = 64-deep ring64 with
-LDS-staged / direct-store epilogue),
-``fused<v>`` (our kernel with the GELU epilogue), ``nsat<v>`` / ``fusedt<v>`` (input
-grads on the forward's NT layout through the cached weight transpose, plain or with
-the GELU' epilogue).  Weight-gradient candidates are
-timed into a scratch buffer so the real accumulator is touched exactly once.
+Candidate names: ``hipblaslt`` / ``hipblaslt_t`` (the library, input grads also on the
+cached weight transpose), ``nt`` (our persistent NT kernel, ``csrc/kernels/gemm_nt.hip``:
+forward and — through the cached K-contiguous weight transpose — input grads),
+``ntgelu`` / ``ntdgelu`` (the same kernel with the GELU / GELU' epilogue), ``nsa<v>``
+(weight grads: split-K kernel variant v of ``csrc/kernels/gemm.hip``).  Weight-gradient
+candidates are timed into a scratch buffer so the real accumulator is touched exactly once.
+Our kernels win ties: a library candidate is picked only when it is more than
+``NSA_NATIVE_MARGIN`` (default 3 %) faster than the best native one.
 ``NSA_GEMM_BACKEND=nsa|hipblaslt`` pins a backend family (tests, A/B runs).
 """
 
@@ -77,14 +78,10 @@ WGRAD_ALLOW_BF16 = os.environ.get("NSA_WGRAD_ALLOW_BF16", "0") == "1"
 # GEMM is left out of the weight-gradient race (its split-K reduction order is not ours
 # to pin); the embedding backward switches to its sorted, atomic-free kernel.
 DETERMINISTIC = False
-NSA_VARIANTS = (7, 8)     # forward / input-grad candidates (ring64: LDS-staged / direct epilogue)
+NATIVE_MARGIN = float(os.environ.get("NSA_NATIVE_MARGIN", "0.03"))
 # weight-grad split counts that fill whole CU rounds as tuner candidates (NSA_WGRAD_FULL_ROUNDS=0: off)
 WGRAD_FULL_ROUNDS = os.environ.get("NSA_WGRAD_FULL_ROUNDS", "1") != "0"
-WGRAD_VARIANTS = (1, 7)   # weight-grad (fp32 atomic epilogue) candidates
-# input-grad candidates on the NT layout through the cached W^T (e.g. NSA_NT_VARIANTS=7,9:
-# ring64, persistent p8).  Off by default: on the GPT-2 shapes neither the plain nor the
-# GELU'-fused form ever beat hipBLASLt on the same transpose (+ the GELU kernel)
-NT_VARIANTS = tuple(int(v) for v in os.environ.get("NSA_NT_VARIANTS", "").split(",") if v)
+WGRAD_VARIANTS = (1, 7, 9)   # weight-grad (fp32 atomic epilogue) candidates: ring, ring64, phase
 
 
 def _time_all(candidates: dict, rounds=3, reps=3):
@@ -112,11 +109,19 @@ def _time_all(candidates: dict, rounds=3, reps=3):
     return {n: sorted(v)[len(v) // 2] for n, v in samples.items()}
 
 
-def choose(key, candidates: dict) -> str:
-    """Return the name of the fastest candidate for ``key`` (timed once, then cached)."""
+def _is_library(name: str) -> bool:
+    return name.startswith("hipblaslt") or name == "split_lib"
+
+
+def choose(key, candidates: dict, fixed: str | None = None) -> str:
+    """Return the name of the fastest candidate for ``key`` (timed once, then cached).
+
+    Native candidates win within ``NATIVE_MARGIN`` of the fastest library candidate."""
     if FORCE:
         for name in candidates:
-            if name.startswith(FORCE) or (FORCE == "nsa" and name.startswith("fused")):
+            if FORCE == "nsa" and not _is_library(name):
+                return name
+            if FORCE != "nsa" and name.startswith(FORCE):
                 return name
         return next(iter(candidates))
     _load()
@@ -124,11 +129,47 @@ def choose(key, candidates: dict) -> str:
     if hit in candidates:
         return hit
     with _lock:
-        times = _time_all(candidates)
-        best = min(times, key=times.get)
+        if DETERMINISTIC:
+            # no timing race: a fixed rule, identical in every run: the native
+            # candidate (or the caller's ``fixed`` pick), else the first one
+            best = fixed if fixed in candidates else next(
+                (n for n in candidates if n.startswith("nt") or n.startswith("det")), next(iter(candidates)))
+        else:
+            best = _pick_timed(candidates)
+        best = _agree(best)
         _table[key] = best
         _save()
     return best
+
+
+VERBOSE = os.environ.get("NSA_GEMM_TUNE_VERBOSE", "0") == "1"
+
+
+def _pick_timed(candidates: dict) -> str:
+    times = _time_all(candidates)
+    if VERBOSE:
+        print("gemm tune:", {n: round(t * 1e3, 1) for n, t in sorted(times.items(), key=lambda kv: kv[1])},
+              flush=True)
+    best = min(times, key=times.get)
+    native = {n: t for n, t in times.items() if not _is_library(n)}
+    if _is_library(best) and native:
+        nb = min(native, key=native.get)
+        if native[nb] <= times[best] * (1.0 + NATIVE_MARGIN):
+            best = nb
+    return best
+
+
+def _agree(best: str) -> str:
+    """Under DDP every rank must run the same kernels (identical numerics, one tuning pass
+    instead of eight racing under shared power/thermal limits): rank 0's pick is broadcast.
+    Every rank reaches each tuning decision at the same point of the same program, so the
+    broadcasts pair up in order."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return best
+    obj = [best]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
 
 
 def table():
@@ -167,12 +208,12 @@ def fwd(x2, w):
     """y = x2 @ w^T (bf16)."""
     M, K = x2.shape
     N = w.shape[0]
-    if not (_nsa_ok(x2, w) and _gemm.supported(M, N, K)):
+    if not (_nsa_ok(x2, w) and _gemm.nt_supported(M, N, K)):
         return x2 @ w.t()
     cands = {"hipblaslt": lambda: x2 @ w.t()} if _library_ok(M, N, K) else {}
-    cands.update({f"nsa{v}": (lambda v=v: _gemm.fwd(x2, w, variant=v)) for v in NSA_VARIANTS})
+    cands["nt"] = lambda: _gemm.nt(x2, w)
     name = choose(("fwd", M, N, K), cands)
-    return x2 @ w.t() if name == "hipblaslt" else _gemm.fwd(x2, w, variant=_variant(name))
+    return x2 @ w.t() if name == "hipblaslt" else _gemm.nt(x2, w)
 
 
 # Weight generation: bumped whenever the bf16 compute weights are rewritten outside
@@ -227,19 +268,16 @@ def dgrad(dy2, w):
     streams.before_compute(dy2)  # the side stream's weight GEMMs never share the GPU with this one
     M, N = dy2.shape
     K = w.shape[1]
-    if not (_nsa_ok(dy2, w) and _gemm.supported(M, K, N)):
+    if not (_nsa_ok(dy2, w) and _gemm.nt_supported(M, K, N)):
         return dy2 @ w
     cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
-    cands.update({f"nsa{v}": (lambda v=v: _gemm.dgrad(dy2, w, variant=v)) for v in NSA_VARIANTS})
-    cands.update({f"nsat{v}": (lambda v=v: _gemm.dgrad_t(dy2, _wt(w), variant=v)) for v in NT_VARIANTS})
+    cands["nt"] = lambda: _gemm.nt(dy2, _wt(w))
     name = choose(("dgrad", M, N, K), cands)
     if name == "hipblaslt":
         return dy2 @ w
     if name == "hipblaslt_t":
         return dy2 @ _wt(w).t()
-    if name.startswith("nsat"):
-        return _gemm.dgrad_t(dy2, _wt(w), variant=_variant(name))
-    return _gemm.dgrad(dy2, w, variant=_variant(name))
+    return _gemm.nt(dy2, _wt(w))
 
 
 def _gelu_fwd(u):
@@ -262,7 +300,7 @@ def fwd_gelu(x2, w):
     """(u, gelu(u)) with u = x2 @ w^T: fused GEMM epilogue or GEMM + GELU kernel, whichever is faster."""
     M, K = x2.shape
     N = w.shape[0]
-    if not (_nsa_ok(x2, w) and _gemm.supported(M, N, K)):
+    if not (_nsa_ok(x2, w) and _gemm.nt_supported(M, N, K)):
         u = x2 @ w.t()
         return u, _gelu_fwd(u)
 
@@ -270,10 +308,9 @@ def fwd_gelu(x2, w):
         u = fwd(x2, w)
         return u, _gelu_fwd(u)
 
-    cands = {"split": split}
-    cands.update({f"fused{v}": (lambda v=v: _gemm.fwd_gelu(x2, w, variant=v)) for v in NSA_VARIANTS})
+    cands = {"split": split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)}
     name = choose(("fwd_gelu", M, N, K), cands)
-    return split() if name == "split" else _gemm.fwd_gelu(x2, w, variant=_variant(name))
+    return split() if name == "split" else _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)
 
 
 def dgrad_dgelu(dy2, w, u, between=None):
@@ -284,7 +321,7 @@ def dgrad_dgelu(dy2, w, u, between=None):
     stream's weight-GEMM fork point (ops/streams.py)."""
     M, N = dy2.shape
     K = w.shape[1]
-    if not (_nsa_ok(dy2, w, u) and _gemm.supported(M, K, N)):
+    if not (_nsa_ok(dy2, w, u) and _gemm.nt_supported(M, K, N)):
         dg = dy2 @ w
         if between is not None:
             between()
@@ -296,17 +333,11 @@ def dgrad_dgelu(dy2, w, u, between=None):
             hook()
         return _gelu_bwd(dg, u)
 
-    cands = {"split": split}
-    cands.update({f"fused{v}": (lambda v=v: _gemm.dgrad(dy2, w, u=u, variant=v)) for v in NSA_VARIANTS})
-    # the same epilogue on the NT layout through the cached weight transpose
-    cands.update({f"fusedt{v}": (lambda v=v: _gemm.dgrad_t(dy2, _wt(w), u=u, variant=v)) for v in NT_VARIANTS})
+    cands = {"split": split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)}
     name = choose(("dgrad_dgelu", M, N, K), cands)
     if name == "split":
         return split(between)
-    if name.startswith("fusedt"):
-        du = _gemm.dgrad_t(dy2, _wt(w), u=u, variant=_variant(name))
-    else:
-        du = _gemm.dgrad(dy2, w, u=u, variant=_variant(name))
+    du = _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)
     if between is not None:
         between()
     return du
@@ -352,7 +383,7 @@ def wgrad_acc(dy2, x2, g32):
         dc = {f"det{v}/s{sb}": cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v,
                                                                                 deterministic=True))
               for v in WGRAD_VARIANTS for sb in sorted(x for x in splits if 1 <= x <= max(1, T // _gemm.BK))}
-        name = choose(("wgrad_det", T, N, K), dc)
+        name = choose(("wgrad_det", T, N, K), dc, fixed=f"det{WGRAD_VARIANTS[-1]}/s{sdef}")
         _gemm.wgrad_acc(dy2, x2, g32, splits=_splits(name), variant=_variant(name), deterministic=True)
         return
     # every default candidate keeps dW in fp32 until it is added into the fp32

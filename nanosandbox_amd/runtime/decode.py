@@ -58,6 +58,11 @@ class Decoder:
         self.gen = torch.zeros(batch_size, self.T + 1, device=self.device, dtype=torch.int64)
         self.salt = int(torch.randint(0, 2 ** 62, (1,)).item())  # sampling stream (torch.manual_seed governs)
         self.use_graph = (self.device.type == "cuda") if use_graph is None else use_graph
+        if self.use_graph and not self.graph_capable(model):
+            # the fused decode kernels cover head_dim 64, bf16 and V <= 53248; the fallback
+            # ops read the position back to the host (pos.item()) or refuse wider vocabs,
+            # which a captured graph cannot do: run those configs eagerly
+            self.use_graph = False
         self.graph = None      # step(): logits only
         self.sgraphs = {}      # run(): step + sampling + token feedback, per (temperature, top_k)
         self.logits = None
@@ -73,6 +78,12 @@ class Decoder:
                 if c is None or c.dtype != self.dtype:
                     prm.compute = prm.detach().to(self.dtype)
                     self._shadowed.append(prm)
+
+    @staticmethod
+    def graph_capable(model) -> bool:
+        cfg = model.config
+        return (cfg.n_embd // cfg.n_head == 64 and model.compute_dtype == torch.bfloat16
+                and cfg.vocab_size <= 53248)
 
     def release(self):
         """Drop the weight shadows this decoder created and its captured graph."""
@@ -229,18 +240,25 @@ def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: int | Non
 
 @torch.no_grad()
 def generate_cached(model, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0,
-                    top_k: int | None = None, use_graph: bool | None = None) -> torch.Tensor:
-    """``model.generate`` with KV caches: same sampling, one token's forward per new token."""
+                    top_k: int | None = None, use_graph: bool | None = None,
+                    decoder: "Decoder | None" = None) -> torch.Tensor:
+    """``model.generate`` with KV caches: same sampling, one token's forward per new token.
+
+    ``decoder``: a Decoder to reuse across calls (same batch size): its weight shadows and
+    captured graphs survive, so ``sample.py``'s num_samples loop captures once.  The caller
+    releases it; without one, a temporary decoder is built and released here."""
     B, T0 = idx.shape
     if max_new_tokens <= 0:
         return idx
     if T0 + max_new_tokens - 1 > model.config.block_size:
         # the caches hold block_size positions; nanoGPT crops the context beyond that
         return model.generate(idx, max_new_tokens, temperature=temperature, top_k=top_k)
-    dec = Decoder(model, B, max_len=model.config.block_size, use_graph=use_graph)
+    own = decoder is None or decoder.B != B
+    dec = Decoder(model, B, max_len=model.config.block_size, use_graph=use_graph) if own else decoder
     try:
         dec.sample_into(dec.prefill(idx), temperature, top_k)  # pos = T0: gen[:, T0]
         dec.run(max_new_tokens - 1, temperature, top_k)
         return torch.cat([idx, dec.gen[:, T0:T0 + max_new_tokens]], dim=1)
     finally:
-        dec.release()
+        if own:
+            dec.release()

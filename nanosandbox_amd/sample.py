@@ -89,14 +89,27 @@ def main(argv=None):
             start = f.read()
     x = torch.tensor(encode(start), dtype=torch.long, device=device)[None, ...]
     outs = []
-    with torch.no_grad():
-        for _ in range(c["num_samples"]):
-            gen = model.generate_cached if c["kv_cache"] else model.generate
-            y = gen(x, c["max_new_tokens"], temperature=c["temperature"], top_k=c["top_k"])
-            text = decode(y[0].tolist())
-            outs.append(text)
-            print(text)
-            print("---------------")
+    dec = None
+    if c["kv_cache"]:
+        # one decoder for all samples: weight shadows and the captured step graph are
+        # built once, not per sample
+        from .runtime.decode import Decoder
+        dec = Decoder(model, x.shape[0], max_len=model.config.block_size)
+    try:
+        with torch.no_grad():
+            for _ in range(c["num_samples"]):
+                if dec is not None:
+                    y = model.generate_cached(x, c["max_new_tokens"], temperature=c["temperature"], top_k=c["top_k"],
+                                              decoder=dec)
+                else:
+                    y = model.generate(x, c["max_new_tokens"], temperature=c["temperature"], top_k=c["top_k"])
+                text = decode(y[0].tolist())
+                outs.append(text)
+                print(text)
+                print("---------------")
+    finally:
+        if dec is not None:
+            dec.release()
     return outs
 
 

@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--shapes", default="c_attn,attn.c_proj,c_fc,mlp.c_proj,lm_head,c_attn.dx,c_fc.dx,"
                                         "mlp.c_proj.dx,lm_head.dx")
     ap.add_argument("--epi", action="store_true", help="also time the GELU / GELU' epilogues")
-    ap.add_argument("--vars", default="0", help="DMA placement variants to time")
+    ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
     a = ap.parse_args()
     M = a.m
     # name -> (N, K): C[M, N] = A[M, K] B[N, K]^T
@@ -65,7 +65,8 @@ def main():
         tail = ((got[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
         print(json.dumps({"check": name, "rel_err": err, "tail_maxabs": tail}), flush=True)
         del ref
-        cands = {"hipblaslt": lambda: x @ w.t()}
+        cands = {"hipblaslt": lambda: x @ w.t(), "nt_gm8": lambda: gemm.nt(x, w, gm=8),
+                 "nt_gm1": lambda: gemm.nt(x, w, gm=1), "nt_gm4": lambda: gemm.nt(x, w, gm=4)}
         for v in [int(t) for t in a.vars.split(",")]:
             cands[f"nt_v{v}"] = lambda v=v: gemm.nt(x, w, var=v)
             if v:
@@ -73,7 +74,7 @@ def main():
                 e = ((got[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
                 print(json.dumps({"check": f"{name}/v{v}", "rel_err": e}), flush=True)
         if a.probe:
-            for pr, nm in ((4, "nostore"), (8, "rowmajor_lanes")):
+            for pr, nm in ((1, "nodma"), (4, "nostore")):
                 cands[f"nt_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr)
         if a.epi and name in ("c_fc", "mlp.c_proj.dx"):
             if name == "c_fc":

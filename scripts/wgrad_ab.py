@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--shapes", default="c_attn,attn.c_proj,c_fc,mlp.c_proj,lm_head,sq4096")
     ap.add_argument("--bmm-splits", default="2,4,7,8,14")
     ap.add_argument("--check", action="store_true")
-    ap.add_argument("--variants", default="7,14,15,16")
+    ap.add_argument("--variants", default="1,7")
     ap.add_argument("--only", default="", help="comma list of candidate names to keep (e.g. nsa7/s7,nsa11/s7)")
     a = ap.parse_args()
     T = a.m
@@ -61,11 +61,9 @@ def main():
             sdef = gemm.wgrad_splits(N, K, T)
             tiles = -(-N // gemm.TILE) * -(-K // gemm.TILE)
             ss = {sdef, gemm.wgrad_splits_balanced(N, K, T)} | {r * 256 // tiles for r in (1, 2, 3)}
-            # variant -> output tiles per 256x256 tile (14: 256x128, 15/16: 128x128)
-            tile_mult = {7: 1, 12: 1, 14: 2, 15: 4, 16: 4}
             for s in sorted(x for x in ss if 1 <= x <= T // gemm.BK):
                 for v in [int(t) for t in a.variants.split(",")]:
-                    sv = max(1, s // tile_mult.get(v, 1))
+                    sv = s
                     cands[f"nsa{v}/s{sv}"] = (lambda sv=sv, v=v: gemm.wgrad_acc(dy, x, g, splits=sv, variant=v))
         for S in [int(v) for v in a.bmm_splits.split(",") if v]:
             if T % S or (T // S) % 8:
