@@ -52,6 +52,12 @@ constexpr int BUF = 2 * IMG;              // A image then B image
 constexpr int EPI_LDS = 2 * BUF;          // epilogue staging: 4 KiB per wave after the two buffers
 constexpr int SMEM = 2 * BUF + 8 * 4096;  // 160 KiB
 static_assert(SMEM <= 163840, "LDS budget");
+#ifndef NSA_NT_DEF
+#define NSA_NT_DEF 4  // epilogue rounds (of 4) deferred into the next tile's first K-tile
+#endif
+#ifndef NSA_NT_RPP
+#define NSA_NT_RPP 4  // deferred rounds stored per phase
+#endif
 
 enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
@@ -77,6 +83,12 @@ __device__ __forceinline__ void dma16x2(const char* sbase, uint32_t voff0, uint3
                :
                : "v"(voff0), "v"(voff1m), "s"(lds), "s"(sbase)
                : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_imm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -224,10 +236,98 @@ __device__ __forceinline__ void store_tile_lds(const NtArgs& g, const f32x4 (&ac
   }
 }
 
+// One round of a wave's output rows (32 rows x 64 columns): 4 (EPI_GELU: 8) stores.
+template <int EPI, bool NT>
+__device__ __forceinline__ void issue_round(const NtArgs& g, const uint4 (&v)[4], int m0, int n0, int wm, int wn,
+                                            int lane, int rd) {
+  const int rr = lane >> 3, cc = lane & 7;
+  const int col = n0 + wn * 64 + 8 * cc;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    const int grow = m0 + wm * 128 + 32 * rd + 8 * s2 + rr;
+    const int64_t off = (int64_t)grow * g.ldc + col;
+    st16<NT>(g.C + off, v[s2].x, v[s2].y, v[s2].z, v[s2].w);
+    if constexpr (EPI == EPI_GELU) {
+      const uint32_t w[4] = {v[s2].x, v[s2].y, v[s2].z, v[s2].w};
+      uint32_t gg[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
+      st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
+    }
+  }
+}
+
+// Deferred epilogue: the same LDS re-shaping as store_tile_lds (and the GELU' product) for
+// a full tile, but the last DEF rounds' whole-row pieces stay in registers (16 VGPRs per
+// round) and go out in phase 0 of the next tile's first K-tile (issue_round), under that
+// tile's MFMAs.
+template <int EPI, bool NT, int DEF>
+__device__ __forceinline__ void stage_tile(const NtArgs& g, const f32x4 (&acc)[8][4], char* stage, int m0, int n0,
+                                           int wm, int wn, int lane, uint4 (&pst)[DEF][4]) {
+  const int r = lane & 15, q = lane >> 4;
+  const int rr = lane >> 3, cc = lane & 7;
+  const int col = n0 + wn * 64 + 8 * cc;
+  nt_u32x4 uv[2][4];
+  auto load_u = [&](int rd, nt_u32x4 (&dst)[4]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int grow = m0 + wm * 128 + 32 * rd + 8 * s2 + rr;
+      dst[s2] = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(g.U + (int64_t)grow * g.ldc + col));
+    }
+  };
+  if constexpr (EPI == EPI_DGELU) {
+    load_u(0, uv[0]);
+    load_u(1, uv[1]);
+  }
+#pragma unroll
+  for (int rd = 0; rd < 4; ++rd) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int row = 16 * i2 + r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 t = acc[2 * rd + i2][j];
+        const int chunk = (2 * j + (q >> 1)) ^ (row & 7);
+        *reinterpret_cast<uint2*>(stage + row * 128 + chunk * 16 + (q & 1) * 8) =
+            make_uint2(pack2(t[0], t[1]), pack2(t[2], t[3]));
+      }
+    }
+    uint4 v[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int row = 8 * s2 + rr;
+      v[s2] = *reinterpret_cast<const uint4*>(stage + row * 128 + ((cc ^ (row & 7)) << 4));
+    }
+    if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const nt_u32x4 ur = uv[rd & 1][s2];
+        uint32_t w[4] = {v[s2].x, v[s2].y, v[s2].z, v[s2].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(ur[e] << 16));
+          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(ur[e] & 0xffff0000u));
+          w[e] = pack2(a0, a1);
+        }
+        v[s2] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      if (rd + 2 < 4) load_u(rd + 2, uv[rd & 1]);
+    }
+    if (rd < 4 - DEF) {
+      issue_round<EPI, NT>(g, v, m0, n0, wm, wn, lane, rd);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) pst[rd - (4 - DEF)][s2] = v[s2];
+    }
+  }
+}
+
 }  // namespace
 
-// NT: nontemporal epilogue stores.  PROBE (timing only, wrong results): 1 = no DMA after
-// the prologue (stale LDS), 4 = no epilogue stores.
+// NT: nontemporal epilogue stores.  PROBE: 1 = no DMA after the prologue (stale LDS, wrong
+// results), 2 = synchronous epilogue (no deferred stores; A/B, correct), 4 = no epilogue
+// stores (wrong).
 template <int EPI, bool NT, int PROBE, bool BAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -323,6 +423,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
   if (wm == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
 
   int seq = v;
+  // pend: the previous tile stored its first 4 - DEF rounds at its end and staged the last
+  // DEF in pst; they go out RPP per phase at the head of this tile's first K-tile, after
+  // the phase's DMA (registers: the accumulators of the later quadrants are not live yet
+  // there).  vmcnt is in order, so a wait counts every store issued after the half-tile it
+  // retires (SR stores per round): in K-tile 0 the 4 - DEF stored at the tile end plus the
+  // deferred ones issued so far, in K-tile 1 the deferred ones issued from phase P on.
+  constexpr int SR = EPI == EPI_GELU ? 8 : 4;
+  constexpr int DEF = NSA_NT_DEF, RPP = NSA_NT_RPP;
+  static_assert(DEF >= 1 && DEF <= 4 && RPP >= 1 && 8 + 4 * SR < 64, "deferred-store accounting");
+  bool pend = false;
+  int pm0 = 0, pn0 = 0;
+  uint4 pst[DEF][4];
   f32x4 acc[8][4];
   bf16x8 af[4][2], b0f[2][2], b1f[2][2], b0n[2][2];
   // B0 of K-tile 0 (retired with A0 by the prologue's wait); afterwards each K-tile's
@@ -335,10 +447,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
       for (int kk = 0; kk < 2; ++kk) b0f[j][kk] = rd16(smem + offB[kk] + (16 * j) * 128);
   }
 
-// one phase: P = 0..3, FIRST = first K-tile of an output tile (kk = 0 MFMAs start from 0).
+// one phase: P = 0..3, FIRST = first K-tile of an output tile (kk = 0 MFMAs start from 0),
+// KT = 1 / 2 / 0: the tile's first / second / any later K-tile (deferred-store accounting).
 // [LDS reads | DMA of half-tile P+6 + counted wait retiring what phase P+1 reads | barrier |
 //  16 MFMAs | barrier]
-#define NT_PHASE(P, FIRST)                                                                      \
+#define NT_PHASE(P, FIRST, KT)                                                                    \
   {                                                                                            \
     const char* base_ = smem + bufc;                                                           \
     if (P == 0 || P == 2) {                                                                    \
@@ -364,10 +477,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
     }                                                                                          \
     {                                                                                          \
       const Cur& cc_ = (P < 2) ? c1 : c2;                                                      \
+      if (cc_.valid && PROBE != 1)                                                             \
+        issue_half(cc_, P == 0 ? 2 : P == 1 ? 3 : P == 2 ? (BAL ? 1 : 0) : (BAL ? 0 : 1));       \
+      if (KT == 1 && RPP * P < DEF && pend) {                                                  \
+        _Pragma("unroll") for (int d_ = RPP * P; d_ < DEF && d_ < RPP * (P + 1); ++d_)          \
+          issue_round<EPI, NT>(g, pst[d_], pm0, pn0, wm, wn, lane, 4 - DEF + d_);              \
+      }                                                                                        \
       if (cc_.valid) {                                                                         \
-        if constexpr (PROBE != 1)                                                              \
-          issue_half(cc_, P == 0 ? 2 : P == 1 ? 3 : P == 2 ? (BAL ? 1 : 0) : (BAL ? 0 : 1));     \
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                      \
+        if ((KT == 1 || (KT == 2 && RPP * P < DEF)) && pend) {                                 \
+          vm_wait_imm<8 + (KT == 1 ? (4 - DEF) * SR + SR * (DEF < RPP * (P + 1) ? DEF : RPP * (P + 1)) \
+                                   : SR * (DEF > RPP * P ? DEF - RPP * P : 0))>();              \
+        } else {                                                                               \
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                    \
+        }                                                                                      \
       } else {                                                                                 \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
       }                                                                                        \
@@ -392,24 +514,44 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
     }                                                                                          \
     raw_barrier();                                                                             \
   }
-#define NT_KTILE(FIRST)              \
+#define NT_KTILE(FIRST, KT)          \
   {                                  \
-    NT_PHASE(0, FIRST)               \
-    NT_PHASE(1, FIRST)               \
-    NT_PHASE(2, FIRST)               \
-    NT_PHASE(3, FIRST)               \
+    constexpr int KT_ = KT;          \
+    NT_PHASE(0, FIRST, KT_)          \
+    NT_PHASE(1, FIRST, KT_)          \
+    NT_PHASE(2, FIRST, KT_)          \
+    NT_PHASE(3, FIRST, KT_)          \
     bufc ^= (uint32_t)BUF;           \
     c1 = c2;                         \
     cur_next(g, c2, nk, G);          \
   }
 
   while (true) {
-    NT_KTILE(true)
-    for (int t = 1; t < nk; ++t) NT_KTILE(false)
+    NT_KTILE(true, 1)
+    if (nk > 1) {
+      NT_KTILE(false, 2)
+      pend = false;
+      for (int t = 2; t < nk; ++t) NT_KTILE(false, 0)
+    }
     int m0, n0, mlo, nlo;
     tile_coords(g, seq, m0, n0, mlo, nlo);
     if constexpr (PROBE != 4) {
-      store_tile_lds<EPI, NT>(g, acc, smem + EPI_LDS + wave * 4096, m0, n0, mlo, nlo, wm, wn, lane);
+      // defer when another tile follows and spans >= 2 K-tiles, and no store is masked
+      // off (the wait counts above assume every store of a round is issued)
+      if (PROBE != 1 && PROBE != 2 && nk > 1 && seq + G < g.tiles && (m0 == mlo) & (n0 == nlo)) {
+        stage_tile<EPI, NT, DEF>(g, acc, smem + EPI_LDS + wave * 4096, m0, n0, wm, wn, lane, pst);
+        pend = true;
+        pm0 = m0;
+        pn0 = n0;
+      } else {
+        store_tile_lds<EPI, NT>(g, acc, smem + EPI_LDS + wave * 4096, m0, n0, mlo, nlo, wm, wn, lane);
+        // redefine pst on this path too: otherwise the previous tile's staged values flow
+        // round the loop here and stay allocated through every K-tile (spills)
+#pragma unroll
+        for (int d = 0; d < DEF; ++d)
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) pst[d][s2] = make_uint4(0, 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -426,7 +568,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
 }
 
 // epi: 0 = bf16 store, 1 = u + gelu(u) into C / C2, 2 = acc * gelu'(U).
-// bits 8-11: timing probe (1 no DMA, 4 no stores; wrong results).  bits 12-13: epilogue
+// bits 8-11: probe (1 no DMA, 4 no stores: timing only; 2 no post-epilogue window).  bits 12-13: epilogue
 // store policy (0 = nontemporal when the output exceeds the 256 MiB Infinity Cache,
 // 1 = always, 2 = never); bit 14: phase-3 B0 prefetch off (A/B); bits 16-23: row-blocks
 // per tile group (0 = automatic).  grid = persistent workgroup count (#CUs).
@@ -468,6 +610,7 @@ NSA_API hipError_t nsa_gemm_nt(int epi, const void* A, int lda, const void* B, i
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
 #define NT_LAUNCH(E)                                                          \
   if (probe == 1) gemm_nt_kernel<E, true, 1, true><<<gr, NTHR, 0, s>>>(a);    \
+  else if (probe == 2) gemm_nt_kernel<E, true, 2, true><<<gr, NTHR, 0, s>>>(a); \
   else if (probe == 4) gemm_nt_kernel<E, true, 4, true><<<gr, NTHR, 0, s>>>(a); \
   else if (!bal) gemm_nt_kernel<E, true, 0, false><<<gr, NTHR, 0, s>>>(a);    \
   else if (nt) gemm_nt_kernel<E, true, 0, true><<<gr, NTHR, 0, s>>>(a);       \

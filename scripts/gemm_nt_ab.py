@@ -4,10 +4,14 @@ Correctness: each shape is checked against an fp32 product of the same bf16 oper
 Timing: interleaved rounds in one process on uniform [-1, 1) operands
 (cdna_hip_programming.md §5.4 rules 24/25).
 
-    python scripts/gemm_nt_ab.py [--m 122880] [--rounds 5] [--probe]
+    python scripts/gemm_nt_ab.py [--m 122880] [--rounds 5] [--probe] [--tuned]
+
+--tuned replays the TunableOp hipBLASLt/rocBLAS solution table the trainer and bench.py
+use (ops/blas_tuning.py), i.e. the library GEMM the tuner actually races against.
 """
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -36,9 +40,33 @@ def main():
     ap.add_argument("--shapes", default="c_attn,attn.c_proj,c_fc,mlp.c_proj,lm_head,c_attn.dx,c_fc.dx,"
                                         "mlp.c_proj.dx,lm_head.dx")
     ap.add_argument("--epi", action="store_true", help="also time the GELU / GELU' epilogues")
+    ap.add_argument("--tuned", action="store_true", help="hipBLASLt with the tuned solution table")
+    ap.add_argument("--alt", default="", help="NAME=PATH,... stand-alone NT builds (scripts/build_nt_variants.sh)")
+    ap.add_argument("--gms", default="", help="extra tile-group sizes to time, e.g. 1,4,8")
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
     a = ap.parse_args()
     M = a.m
+    alts = {}
+    for spec in [t for t in a.alt.split(",") if t]:
+        nm, path = spec.split("=", 1)
+        L = ctypes.CDLL(os.path.abspath(path))
+        L.nsa_gemm_nt.argtypes = _lib._SIGNATURES["nsa_gemm_nt"]
+        L.nsa_gemm_nt.restype = ctypes.c_int
+        alts[nm] = L
+
+    def alt_nt(L, x, w, epi=0, u=None):
+        Mx, Kx = x.shape
+        Nx = w.shape[0]
+        out = torch.empty(Mx, Nx, device=x.device, dtype=torch.bfloat16)
+        act = torch.empty_like(out) if epi == gemm.NT_EPI_GELU else None
+        err = L.nsa_gemm_nt(epi, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+                            None if act is None else act.data_ptr(), None if u is None else u.data_ptr(), Mx, Nx, Kx,
+                            gemm.num_cus(), _lib.stream())
+        assert err == 0, err
+        return (out, act) if act is not None else out
+    if a.tuned:
+        from nanosandbox_amd.ops import blas_tuning
+        print(json.dumps({"tuned_table": blas_tuning.enable()}), flush=True)
     # name -> (N, K): C[M, N] = A[M, K] B[N, K]^T
     shapes = {"c_attn": (2304, 768), "attn.c_proj": (768, 768), "c_fc": (3072, 768), "mlp.c_proj": (768, 3072),
               "lm_head": (50304, 768), "c_attn.dx": (768, 2304), "c_fc.dx": (768, 3072),
@@ -65,9 +93,15 @@ def main():
         tail = ((got[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
         print(json.dumps({"check": name, "rel_err": err, "tail_maxabs": tail}), flush=True)
         del ref
-        cands = {"hipblaslt": lambda: x @ w.t(), "nt_gm8": lambda: gemm.nt(x, w, gm=8),
-                 "nt_gm1": lambda: gemm.nt(x, w, gm=1), "nt_gm4": lambda: gemm.nt(x, w, gm=4)}
-        for v in [int(t) for t in a.vars.split(",")]:
+        cands = {"hipblaslt": lambda: x @ w.t(), "nt": lambda: gemm.nt(x, w),
+                 "nt_nopost": lambda: gemm.nt(x, w, probe=2)}
+        for nm, L in alts.items():
+            cands[f"nt_{nm}"] = lambda L=L: alt_nt(L, x, w)
+            e = ((alt_nt(L, x, w)[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
+            print(json.dumps({"check": f"{name}/{nm}", "rel_err": e}), flush=True)
+        for gm_ in [int(t) for t in a.gms.split(",") if t]:
+            cands[f"nt_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_)
+        for v in [int(t) for t in a.vars.split(",") if t and t != "0"]:
             cands[f"nt_v{v}"] = lambda v=v: gemm.nt(x, w, var=v)
             if v:
                 got = gemm.nt(x, w, var=v)
@@ -91,6 +125,9 @@ def main():
                     _lib.call("nsa_gelu_fwd", _lib.ptr(uu), _lib.ptr(gg), uu.numel(), _lib.stream())
                 cands["hipblaslt+gelu"] = split
                 cands["nt_gelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+                cands["nt_gelu_nopost"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU, probe=2)
+                for nm, L in alts.items():
+                    cands[f"nt_gelu_{nm}"] = lambda L=L: alt_nt(L, x, w, epi=gemm.NT_EPI_GELU)
             else:
                 u = uni(M, N, scale=3.0)
                 got = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u)
@@ -109,6 +146,9 @@ def main():
                     _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
                 cands["hipblaslt+dgelu"] = split2
                 cands["nt_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u)
+                cands["nt_dgelu_nopost"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, probe=2)
+                for nm, L in alts.items():
+                    cands[f"nt_dgelu_{nm}"] = lambda L=L: alt_nt(L, x, w, epi=gemm.NT_EPI_DGELU, u=u)
         for fn in cands.values():
             fn()
         torch.cuda.synchronize()
