@@ -39,17 +39,24 @@ def _free_port():
     return p
 
 
-def _batches():
+# production-kernel rehearsal: every GEMM dimension >= 256 so the forward / input-grad
+# GEMMs can take our NT kernel and the weight grads our split-K kernel (tiny widths
+# fall back to the library whatever the tuner says)
+CFG_PROD = dict(n_layer=2, n_head=4, n_embd=256, block_size=256, vocab_size=1024, bias=False, dropout=0.0)
+
+
+def _batches(cfg=CFG):
     g = torch.Generator().manual_seed(7)
-    return [[torch.randint(0, 512, (MB, 65), generator=g) for _ in range(GLOBAL_MICRO)] for _ in range(STEPS)]
+    T, V = cfg["block_size"], cfg["vocab_size"]
+    return [[torch.randint(0, V, (MB, T + 1), generator=g) for _ in range(GLOBAL_MICRO)] for _ in range(STEPS)]
 
 
-def _build(seed):
+def _build(seed, cfg=CFG):
     from nanosandbox_amd.models import GPT, GPTConfig
     from nanosandbox_amd.optim import FlatParamStore
 
     torch.manual_seed(seed)
-    m = GPT(GPTConfig(**CFG)).to("cuda:0").set_compute_dtype(torch.bfloat16)
+    m = GPT(GPTConfig(**cfg)).to("cuda:0").set_compute_dtype(torch.bfloat16)
     store = FlatParamStore(m, "cuda:0", compute_dtype=torch.bfloat16)
     opt = m.configure_optimizers(0.1, 3e-3, (0.9, 0.95), "cuda", store=store)
     return m, store, opt
@@ -107,5 +114,74 @@ def test_ddp_gpu_two_ranks_match_single_process(tmp_path, monkeypatch):
     # the remaining differences: summation order (gloo's rank sum vs sequential
     # accumulation, embedding/LayerNorm-partial atomics); Adam turns that noise into
     # <= lr-sized steps on near-zero gradients
+    assert d.max() <= STEPS * 3e-3 + 1e-6
+    assert d.mean() < 2e-5
+
+
+def _worker_prod(rank, world, port, out_dir, mode):
+    """As _worker, but with the production GEMM selection: the timed autotuner (rank 0's
+    picks broadcast to every rank, gemm_tune._agree) or deterministic mode's fixed
+    native picks.  Collectives still run over gloo (one GPU)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1")
+    os.environ.pop("NSA_GEMM_BACKEND", None)
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import gemm_tune
+    from nanosandbox_amd.parallel import FlatBucketReducer
+    from nanosandbox_amd.parallel.dist import init_distributed
+
+    gemm_tune.FORCE = ""
+    ops.set_deterministic(mode == "deterministic")
+    info = init_distributed("nccl", "cuda")
+    assert info.world_size == world
+    gas = GLOBAL_MICRO // world
+    mine = [[b[rank * gas + i] for i in range(gas)] for b in _batches(CFG_PROD)]
+    model, store, opt = _build(seed=300 + rank, cfg=CFG_PROD)
+    red = FlatBucketReducer(store, bucket_cap_mb=1)
+    red.broadcast_parameters()
+    opt.grad_scale = red.grad_scale
+    final = _train(model, store, opt, mine, gas, before=red.prepare, after=red.finish)
+    table = {repr(k): v for k, v in gemm_tune.table().items()}
+    torch.save({"final": final, "n_buckets": len(red.buckets), "table": table},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["tuned", "deterministic"])
+def test_ddp_gpu_production_kernels(tmp_path, monkeypatch, mode):
+    """The flat reducer's bucket hooks, our split-K weight-gradient kernels accumulating
+    into the flat gradient and the NT forward / input-gradient GEMMs, together under DDP
+    (VERDICT r2 'do this' 4.1).  Ranks must agree bitwise (same kernels on every rank);
+    the single-process reference replays rank 0's kernel table, so only the gradient
+    summation order differs."""
+    import ast
+
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import gemm_tune
+
+    port = _free_port()
+    mp.spawn(_worker_prod, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    assert res[0]["n_buckets"] > 1
+    assert res[0]["table"] == res[1]["table"], "ranks tuned different kernels"
+    picks = res[0]["table"]
+    # our kernels actually ran: native weight-grad picks (nsa*/det*) and, for the
+    # deterministic rule, native forward / input-grad picks
+    assert any(k.startswith(("('wgrad'", "('wgrad_det'")) and not v.startswith("hipblaslt")
+               for k, v in picks.items()), picks
+    if mode == "deterministic":
+        assert all(v.startswith(("nt", "det")) for k, v in picks.items() if k.startswith(("('fwd'", "('dgrad'"))), picks
+    assert torch.equal(res[0]["final"], res[1]["final"]), "ranks diverged"
+    monkeypatch.setattr(gemm_tune, "FORCE", "")
+    monkeypatch.setattr(gemm_tune, "_table", {ast.literal_eval(k): v for k, v in picks.items()})
+    monkeypatch.setattr(gemm_tune, "_loaded", True)
+    ops.set_deterministic(mode == "deterministic")
+    try:
+        model, store, opt = _build(seed=300, cfg=CFG_PROD)
+        ref = _train(model, store, opt, _batches(CFG_PROD), GLOBAL_MICRO)
+    finally:
+        ops.set_deterministic(False)
+    d = (res[0]["final"] - ref).abs()
     assert d.max() <= STEPS * 3e-3 + 1e-6
     assert d.mean() < 2e-5
