@@ -238,11 +238,23 @@ __global__ __launch_bounds__(kBlock) void scale_bf16_kernel(const bf16_t* __rest
 }  // namespace
 
 // nontemporal loads / stores in the GELU passes (default; NSA_EW_NT=0 turns them off, read
-// per launch for A/B runs).  scripts/membound_ab.py at 122880 x 3072: fwd 282.7 -> 278.3 us,
+// once, nsa_ew_set_nt for A/B runs).  scripts/membound_ab.py at 122880 x 3072: fwd 282.7 -> 278.3 us,
 // bwd 428.4 -> 410.9 us (5.29 -> 5.51 TB/s)
-static bool ew_nt() {
-  const char* e = getenv("NSA_EW_NT");
-  return !(e && e[0] == '0');
+// resolved once from NSA_EW_NT (0 = plain loads / stores); nsa_ew_set_nt switches it (A/B)
+static int& ew_nt_flag() {
+  static int f = [] {
+    const char* e = getenv("NSA_EW_NT");
+    return !(e && e[0] == '0') ? 1 : 0;
+  }();
+  return f;
+}
+static bool ew_nt() { return ew_nt_flag() != 0; }
+
+// set the streaming-store policy of the elementwise kernels (on < 0: keep); returns the old one
+NSA_API int nsa_ew_set_nt(int on) {
+  const int prev = ew_nt_flag();
+  if (on >= 0) ew_nt_flag() = on ? 1 : 0;
+  return prev;
 }
 
 NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {

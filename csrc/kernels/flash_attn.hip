@@ -17,12 +17,13 @@
 //   O^T[d][q] += V^T · P^T        A = V^T (LDS, ds_read_b64_tr_b16 transposed
 //        read of the row-major V tile), B = P^T straight from the S^T
 //        accumulator registers (bf16-converted, permuted k order).
-// backward (default "split" mode: dK/dV kernel + separate dQ kernel, see bwd_launch;
-// the "atomic" mode below keeps dQ in the dK/dV kernel), per wave = 32 keys, loop over 64-query blocks:
+// backward: a dK/dV kernel (per wave = 32 keys, loop over query blocks) and a separate
+// dQ kernel (per wave = 32 queries, loop over key tiles), so dQ is written once, in bf16,
+// with no atomics and no fp32 accumulator:
 //   S = Q·K^T, dP = dO·V^T        key on the lane; K, V fragments live in registers
 //   dV^T += dO^T · P,  dK^T += Q^T · dS      accumulators as B operands, A by tr reads
-//   dQ   += dS · K                dS crosses LDS once (as dS^T), fp32 atomics whose
-//        wave-instructions are two 128-B row segments (full atomic rate).
+//   dQ^T += K^T · dS^T            (dQ kernel) the query on the lane, recomputing S and dP
+// Kernel variants are chosen once per process (FlashConfig below), not per launch.
 //
 // LDS images are XOR-swizzled per 16-byte chunk with a bit-reversed row key:
 //   phys_chunk = chunk ^ bitrev((row / rows_per_bank_row) mod chunks_per_row)
@@ -110,11 +111,28 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
   t = u % n_tiles;
 }
 
-// NSA_ATTN_ORDER = 0 / 1 (see attn_order); read per launch so A/B runs can switch it
-int attn_order_env() {
-  const char* e = getenv("NSA_ATTN_ORDER");
-  return e ? (e[0] == '1') : ATTN_ORDER_DEFAULT;
+// Kernel selection, resolved once (first launch) from the environment and changed only
+// through nsa_flash_set_variant (tests / A/B scripts):
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3: D = 64 forward kernel; auto = v3
+//         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
+//   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
+//   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3 };
+enum { BWD_V1 = 1, BWD_V2 = 2 };
+struct FlashConfig {
+  int fwd, bwd, order;
+};
+FlashConfig& flash_config() {
+  static FlashConfig c = [] {
+    FlashConfig d{FWD_AUTO, BWD_V2, ATTN_ORDER_DEFAULT};
+    if (const char* e = getenv("NSA_FLASH_FWD")) d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1 : (e[0] == 'v' && e[1] == '3') ? FWD_V3 : FWD_AUTO;
+    if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
+    if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
+    return d;
+  }();
+  return c;
 }
+int attn_order_env() { return flash_config().order; }
 
 // accumulator register i of a 32x32 tile holds row (i&3) + 8*(i>>2) + 4*h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
@@ -651,16 +669,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
 }
 
 // =============================================================================
-// backward preprocessing, one pass over [B, T, C]:
-//   delta[b, h, t] = rowsum(dO * O)  (fp32)   and   dq_acc[b, t, :] = 0
-// The zeroing rides along with the delta reads (same rows, same threads), so the
-// fp32 dQ accumulator needs no separate fill launch.
+// backward preprocessing (generic path), one pass over [B, T, C]:
+//   delta[b, h, t] = rowsum(dO * O)  (fp32)
 // =============================================================================
 template <int D>
 __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ o,
                                                            const bf16_t* __restrict__ dout,
-                                                           float* __restrict__ delta, float* __restrict__ dq_acc,
-                                                           int B, int T, int H) {
+                                                           float* __restrict__ delta, int B, int T, int H) {
   constexpr int LPR = D / 8;  // lanes per (b, t, h) row, 8 elements each
   const int C = H * D;
   const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -680,40 +695,16 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 #pragma unroll
   for (int k = LPR / 2; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
   if (sub == 0) delta[((int64_t)b * H + hh) * T + t] = s;
-  if (dq_acc != nullptr) {  // in-kernel-dQ mode only (the split mode writes dQ once, no accumulator)
-    float4* z = reinterpret_cast<float4*>(dq_acc + off);
-    z[0] = float4{0.f, 0.f, 0.f, 0.f};
-    z[1] = float4{0.f, 0.f, 0.f, 0.f};
-  }
 }
 
 // =============================================================================
-// backward main kernel: one workgroup = KB keys (KB/32 waves x 32) of one (b, h)
+// backward dK/dV kernel (generic path): one workgroup = KB keys (KB/32 waves x 32) of
+// one (b, h); KB = 256 keys (8 waves) for D = 64, 128 (4 waves) for D = 32 / 128.
 // =============================================================================
-// Geometry: KB = 256 keys (8 waves) for D = 64 (GPT-2), 128 (4 waves) for D = 32
-// (Q-tile staging needs >= 1 chunk per thread) and D = 128 (LDS).
-// dQ leaves the workgroup as fp32 atomics, one 64 x D tile per (q-block, key-block)
-// pair; the chip-wide atomic rate (~1.3 TB/s, MI355X_MICROARCH.md) made those the
-// bound at 128 keys, so the larger key block halves the atomic bytes.  The dQ tile
-// of a q-block is split over the waves by (q-half, d-tile) and, when there are more
-// waves than tiles, by key range; key-range partials are summed in LDS so only one
-// wave per tile issues atomics.
 template <int D>
 struct BwdGeo {
-  static constexpr int QB = 64;
-#ifndef NSA_BWD_KB64
-#define NSA_BWD_KB64 256  // keys per workgroup at D = 64 (A/B probe: build_variant with -DNSA_BWD_KB64=128)
-#endif
-  static constexpr int KB = D == 64 ? NSA_BWD_KB64 : 128;
+  static constexpr int KB = D == 64 ? 256 : 128;
   static constexpr int NW = KB / 32;
-  static constexpr int NTILES = 2 * (D / 32);            // (q-half, d-tile) pairs of the dQ tile
-  static constexpr int SPLIT = NW > NTILES ? NW / NTILES : 1;
-  static constexpr int TPW = NTILES > NW ? NTILES / NW : 1;
-  static constexpr int QT_BYTES = QB * D * 2;
-  static constexpr int K_BYTES = KB * D * 2;
-  static constexpr int DS_BYTES = KB * QB * 2;
-  static constexpr int RED_BYTES = (SPLIT - 1) * NTILES * 64 * 16 * 4;
-  static constexpr int LDS_BYTES = 4 * QT_BYTES + K_BYTES + DS_BYTES + RED_BYTES + 4 * QB * 4;
 };
 
 // P and dS of one 32-query half for this lane's key -> bf16 MFMA fragments (i order).
@@ -777,36 +768,24 @@ __device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpac
     ld_lds[2 * QB + (BUF) * QB + tid] = dst;                                             \
   }
 
-// DQ = true: dQ is accumulated here too (dS^T through LDS, split-K over the
-// workgroup's keys, fp32 atomics into dq_acc).  DQ = false: this kernel makes only
-// dK / dV; flash_bwd_dq_kernel forms dQ per query tile with no atomics, and without
-// the K / dS / reduction LDS two workgroups fit per CU.
-template <int D, bool DROP, bool DQ>
-__global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kernel(
+// dK / dV only: flash_bwd_dq_kernel forms dQ per query tile (two workgroups per CU).
+template <int D, bool DROP>
+__global__ __launch_bounds__(BwdGeo<D>::NW * 64, 2) void flash_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
-    float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed) {
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale, float scale_log2,
+    uint32_t drop_thresh, float drop_scale, uint64_t seed) {
   using G = BwdGeo<D>;
-#ifndef NSA_BWD_QB_SPLIT
-#define NSA_BWD_QB_SPLIT 64  // queries per staged block in the dK/dV-only kernel (128: 1288 -> 1331 us)
-#endif
-  constexpr int QB = DQ ? G::QB : NSA_BWD_QB_SPLIT, KB = G::KB, NT = G::NW * 64;
+  constexpr int QB = 64, KB = G::KB, NT = G::NW * 64;  // QB: queries per staged block (128 measured slower)
   constexpr int CPR = D / 8;
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
   constexpr int QT_BYTES = QB * D * 2;
   constexpr int QCH = QB * CPR / NT;  // 16-byte chunks per thread per Q (or dO) tile
-  constexpr int KCH = KB * CPR / NT;
   static_assert(QCH >= 1 && QB * CPR == QCH * NT, "Q tile staging must divide evenly");
-  constexpr int LDS_TOTAL = DQ ? G::LDS_BYTES : 4 * QT_BYTES + 4 * QB * 4;
-  __shared__ __attribute__((aligned(16))) char smem[LDS_TOTAL];
-  char* const qs_lds = smem;                         // Q[2]
-  char* const do_lds = smem + 2 * QT_BYTES;          // dO[2]
-  char* const k_lds = smem + 4 * QT_BYTES;           // K (workgroup keys)           [DQ only]
-  char* const ds_lds = k_lds + G::K_BYTES;           // dS^T [KB keys][QB q]          [DQ only]
-  float* const red_lds = reinterpret_cast<float*>(ds_lds + G::DS_BYTES);  // split-K dQ partials [DQ only]
-  float* const ld_lds = reinterpret_cast<float*>(DQ ? ds_lds + G::DS_BYTES + G::RED_BYTES
-                                                    : smem + 4 * QT_BYTES);  // lse2[2][QB], delta[2][QB]
+  __shared__ __attribute__((aligned(16))) char smem[4 * QT_BYTES + 4 * QB * 4];
+  char* const qs_lds = smem;                                               // Q[2]
+  char* const do_lds = smem + 2 * QT_BYTES;                                // dO[2]
+  float* const ld_lds = reinterpret_cast<float*>(smem + 4 * QT_BYTES);     // lse2[2][QB], delta[2][QB]
 
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
@@ -838,19 +817,6 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kern
       vf[ks] = as_frag(*reinterpret_cast<const uint4*>(vbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
     }
   }
-  // workgroup K tile -> LDS (B operand of dQ = dS·K by transposed reads)
-  if constexpr (DQ) {
-#pragma unroll
-  for (int c = 0; c < KCH; ++c) {
-    const int e = tid + NT * c;
-    const int row = e / CPR, ch = e % CPR;
-    int key = k0 + row;
-    key = key < T ? key : T - 1;
-    *reinterpret_cast<uint4*>(k_lds + swz<D>(row, ch)) =
-        *reinterpret_cast<const uint4*>(kbase + (int64_t)key * row_stride + ch * 8);
-  }
-  }
-
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
@@ -913,86 +879,9 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, DQ ? 1 : 2) void flash_bwd_kern
           dk[dt] = mfma(qa, dsfr[s], dk[dt]);
         }
       }
-      // dS^T -> LDS: row = key (32w + r), columns = q (qs*32 + 8g + 4h + 0..3); the bf16
-      // values are the dK operand's, 4 per g: dsfr[g >> 1] elements 4(g & 1) .. +3
-      if constexpr (DQ)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int qcol = qs * 32 + 8 * g + 4 * h;
-        const uint4 u4 = __builtin_bit_cast(uint4, dsfr[g >> 1]);
-        uint2 u;
-        u.x = (g & 1) ? u4.z : u4.x;
-        u.y = (g & 1) ? u4.w : u4.y;
-        *reinterpret_cast<uint2*>(ds_lds + swz<QB>(32 * w + r, qcol >> 3) + ((qcol >> 2) & 1) * 8) = u;
-      }
     }
-    if constexpr (DQ) {
-    __syncthreads();
-    // stage the next Q/dO tile now: buffer cur^1 was last read before the previous
-    // barrier, and doing it before the dQ atomics keeps their vmcnt out of its wait
+    // buffer cur^1 was last read in the previous iteration, which ended in a barrier
     { NSA_BWD_STAGE_WRITE(cur ^ 1) }
-
-    // dQ[64 x D] += dS[64 x KB] · K[KB x D]  (scaled)
-    constexpr int KSPAN = KB / G::SPLIT;  // keys per split part
-#pragma unroll
-    for (int t = 0; t < G::TPW; ++t) {
-      const int tile = (w % G::NTILES) + G::NW * t;
-      const int part = w / G::NTILES;  // 0 .. SPLIT-1 (0 when TPW > 1)
-      const int qh = tile & 1, dt = tile >> 1;
-      f32x16 dqa = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < KSPAN / 16; ++ks) {
-        const int kr = part * KSPAN + 16 * ks + 8 * h;
-        const bf16x8 a = tr_frag<QB>(ds_lds, kr, kr + 4, qh * 32, lane);
-        const bf16x8 bk = tr_frag<D>(k_lds, kr, kr + 4, 32 * dt, lane);
-        dqa = mfma(a, bk, dqa);
-      }
-      if constexpr (G::SPLIT > 1) {
-        if (part > 0) {
-          // [v][lane] layout: a wave's 16-byte stores / loads are 64 consecutive chunks
-          // (a [lane][v] layout put lanes 64 B apart: 4-way bank conflicts, PMC-measured)
-          f32x4* dst4 = reinterpret_cast<f32x4*>(red_lds) + ((part - 1) * G::NTILES + tile) * 256 + lane;
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            dst4[64 * v] = f32x4{dqa[4 * v], dqa[4 * v + 1], dqa[4 * v + 2], dqa[4 * v + 3]};
-        }
-        __syncthreads();
-        if (part == 0) {
-#pragma unroll
-          for (int p2 = 1; p2 < G::SPLIT; ++p2) {
-            const f32x4* src4 = reinterpret_cast<const f32x4*>(red_lds) + ((p2 - 1) * G::NTILES + tile) * 256 + lane;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const f32x4 x = src4[64 * v];
-              dqa[4 * v] += x[0];
-              dqa[4 * v + 1] += x[1];
-              dqa[4 * v + 2] += x[2];
-              dqa[4 * v + 3] += x[3];
-            }
-          }
-        }
-      }
-      // Measured (kernel_bench, B120 T1024): the dQ writes are the expensive part of this
-      // loop — plain stores instead of atomics save only 2 %, while letting every split
-      // part issue its own atomics (2x the writes, no LDS reduction / barrier) costs +40 %
-      // (1270 -> 1783 us); so the partials are reduced in LDS and written once.
-      if (part == 0) {
-        float* dqrow = dq_acc + (int64_t)b * T * C + hh * D + 32 * dt + r;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = qb * QB + qh * 32 + acc_row(i, h);
-#ifdef NSA_PROBE_DQ_STORE  // A/B timing probe only (see build.build_variant): wrong dQ
-          if (q < T) dqrow[(int64_t)q * C] = dqa[i] * scale;
-#else
-          if (q < T) atomicAdd(dqrow + (int64_t)q * C, dqa[i] * scale);
-#endif
-        }
-      }
-    }
-    } else {
-      // buffer cur^1 was last read in the previous iteration, which ended in a barrier
-      { NSA_BWD_STAGE_WRITE(cur ^ 1) }
-    }
     __syncthreads();
   }
 
@@ -1182,20 +1071,6 @@ __global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
   }
 }
 
-// dq_acc (fp32 [B, T, C]) -> dqkv[:, :, 0:C] (bf16)
-__global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv,
-                                                        int64_t rows, int C) {
-  const int octs = C / 8;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= rows * octs) return;
-  const int64_t row = i / octs;
-  const int c = (int)(i % octs) * 8;
-  const float4 a = *reinterpret_cast<const float4*>(dq + row * C + c);
-  const float4 bq = *reinterpret_cast<const float4*>(dq + row * C + c + 4);
-  const float f[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
-  store8(dqkv + row * 3 * C + c, f);
-}
-
 // =============================================================================
 // Backward v2 (D = 64, the GPT-2 head size): dK/dV kernel, templated on
 //   NKB = 32-key blocks per wave (1 or 2) and NW = waves per workgroup (4 or 8).
@@ -1365,86 +1240,11 @@ __device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, cons
   }
 }
 
-// The two halves of a slice, for the software-pipelined loop (PIPE): the S / dP MFMA
-// chains of slice j+1 (dkdv_sdp) go into the same basic block as the softmax and the
-// dV / dK MFMAs of slice j (dkdv_finish), so each wave has two independent chains to
-// interleave instead of one dependent one.
-template <int NKB, bool DROP>
-__device__ __forceinline__ void dkdv_sdp(const char* qt, const char* dot, const float* ld,
-                                         const bf16x8 (&kf)[NKB][4], const bf16x8 (&vf)[NKB][4],
-                                         f32x16 (&sacc)[NKB], f32x16 (&pacc)[NKB], int h, int r) {
-  constexpr int D = 64;
-  bf16x8 qa[4], da[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qa[ks] = as_frag(lds_b128(qt, swz<D>(r, 2 * ks + h)));
-    da[ks] = as_frag(lds_b128(dot, swz<D>(r, 2 * ks + h)));
-  }
-#pragma unroll
-  for (int kb = 0; kb < NKB; ++kb) {
-    sacc[kb] = row_consts(ld, h);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) sacc[kb] = mfma(qa[ks], kf[kb][ks], sacc[kb]);
-  }
-#pragma unroll
-  for (int kb = 0; kb < NKB; ++kb) {
-    pacc[kb] = DROP ? f32x16{} : row_consts(ld + 32, h);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) pacc[kb] = mfma(da[ks], vf[kb][ks], pacc[kb]);
-  }
-}
-
-template <int NKB, bool MASK, bool DROP>
-__device__ __forceinline__ void dkdv_finish(const char* qt, const char* dot, const float* ld,
-                                            const f32x16 (&sacc)[NKB], const f32x16 (&pacc)[NKB],
-                                            f32x16 (&dk)[NKB][2], f32x16 (&dv)[NKB][2], int q0, int kw, int h,
-                                            int r, int lane, float scale_log2, const DropArgs& dr) {
-  constexpr int D = 64;
-  bf16x8 pfr[NKB][2], dsfr[NKB][2];
-#pragma unroll
-  for (int kb = 0; kb < NKB; ++kb) {
-    const int key = kw + 32 * kb + r;
-    f32x16 nd;
-    if constexpr (DROP) nd = row_consts(ld + 32, h);
-    float pv[16], dsv[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p = fast_exp2(sacc[kb][i] * scale_log2);
-      if constexpr (MASK) p = key > q0 + acc_row(i, h) ? 0.0f : p;
-      if constexpr (DROP) {
-        const int q = q0 + acc_row(i, h);
-        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)q) * (uint64_t)dr.T + (uint64_t)key;
-        const bool keep = nsa_keep(dr.seed, id, dr.thresh);
-        pv[i] = keep ? p * dr.scale : 0.0f;
-        dsv[i] = p * ((keep ? pacc[kb][i] * dr.scale : 0.0f) + nd[i]);
-      } else {
-        pv[i] = p;
-        dsv[i] = p * pacc[kb][i];
-      }
-    }
-    pack16(pv, pfr[kb]);
-    pack16(dsv, dsfr[kb]);
-  }
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int r0 = 16 * s + 4 * h;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      const bf16x8 doa = tr_frag<D>(dot, r0, r0 + 8, 32 * dt, lane);
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) dv[kb][dt] = mfma(doa, pfr[kb][s], dv[kb][dt]);
-      const bf16x8 qta = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) dk[kb][dt] = mfma(qta, dsfr[kb][s], dk[kb][dt]);
-    }
-  }
-}
-
 #ifndef NSA_DKDV_NS
 #define NSA_DKDV_NS 4  // LDS ring slots of the v2 dK/dV kernel (NS - 1 slices in flight)
 #endif
 
-template <int NKB, int NW, bool DROP, bool PIPE = false>
+template <int NKB, int NW, bool DROP>
 __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
     const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
@@ -1453,8 +1253,7 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   constexpr int KPW = 32 * NKB;       // keys per wave
   constexpr int KWG = KPW * NW;       // keys per workgroup
   constexpr int SLOT = V2Geo<NW>::SLOT;
-  // PIPE keeps slice j's tiles in use after slice j+1's barrier: one slot less in flight
-  constexpr int NS = NSA_DKDV_NS, LA = PIPE ? NS - 2 : NS - 1;
+  constexpr int NS = NSA_DKDV_NS, LA = NS - 1;
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
@@ -1563,53 +1362,13 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   const int j_full = min(NKB * w + NKB, n_mine);
   int j = 0;
   for (; j < j_diag; ++j) open_slice(j);
-  if constexpr (!PIPE) {
-    for (; j < j_full; ++j) {
-      open_slice(j);
-      slice_diag(j);
-    }
-    for (; j < n_mine; ++j) {
-      open_slice(j);
-      slice_full(j);
-    }
-  } else if (j < n_mine) {
-    // software pipeline: iteration j opens slice j+1 and issues its S / dP chains
-    // beside slice j's softmax and dV / dK MFMAs
-    f32x16 sacc[NKB], pacc[NKB];
+  for (; j < j_full; ++j) {
     open_slice(j);
-    {
-      auto f = [&](auto slot) {
-        const char* qt = smem + decltype(slot)::value * SLOT;
-        dkdv_sdp<NKB, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, kf, vf, sacc,
-                            pacc, h, r);
-      };
-      slot_dispatch<0, NS>(j % NS, f);
-    }
-    auto step = [&](int jj, auto mask) {
-      constexpr bool M = decltype(mask)::value;
-      const bool more = jj + 1 < n_mine;
-      if (more) open_slice(jj + 1);
-      auto f = [&](auto slot) {
-        constexpr int K = decltype(slot)::value;
-        constexpr int KN = (K + 1) % NS;
-        const char* qt = smem + K * SLOT;
-        const char* qn = smem + KN * SLOT;
-        f32x16 sn[NKB], pn[NKB];
-        if (more)
-          dkdv_sdp<NKB, DROP>(qn, qn + V2_QT, reinterpret_cast<const float*>(qn + 2 * V2_QT) + w * 64, kf, vf, sn,
-                              pn, h, r);
-        dkdv_finish<NKB, M, DROP>(qt, qt + V2_QT, reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64, sacc,
-                                  pacc, dk, dv, (s_first + jj) * 32, kw, h, r, lane, scale_log2, dr);
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          sacc[kb] = sn[kb];
-          pacc[kb] = pn[kb];
-        }
-      };
-      slot_dispatch<0, NS>(jj % NS, f);
-    };
-    for (; j < j_full; ++j) step(j, std::integral_constant<bool, true>{});
-    for (; j < n_mine; ++j) step(j, std::integral_constant<bool, false>{});
+    slice_diag(j);
+  }
+  for (; j < n_mine; ++j) {
+    open_slice(j);
+    slice_full(j);
   }
 
   // epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T -> dqkv[:, :, C + ...] and [2C + ...]
@@ -1848,442 +1607,133 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
   }
 }
 
-// =============================================================================
-// Forward v2 (D = 64, opt-in: NSA_FLASH_FWD=v2s3): the v1 forward's math (swapped
-// S^T = K·Q^T with the query on the lane, deferred max-rescale, O^T += V^T·P^T from
-// the accumulator registers) on the v2 backward's plumbing: 64-key K / V tiles by
-// LDS-DMA into an NS-slot ring (NS - 1 tiles in flight; v1 stages one tile through
-// registers and parks ~54 % of wave cycles on its waits, PMC), slot-dispatched
-// branch-free bodies, the loop split into fully visible tiles / the wave's diagonal
-// tile / trailing masked tiles, and pairwise bf16 packing of P.  Measured slower than
-// v1 (see fwd_launch): the deeper ring costs the occupancy that hid those waits.
-// =============================================================================
-template <bool MASK, bool DROP>
-__device__ __forceinline__ void fwd2_tile(const char* kt, const char* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2],
-                                          float& m_i, float& l_i, int kv0, int qpos, int h, int r, int lane,
-                                          float scale_log2, const DropArgs& dr) {
-  constexpr int D = 64;
-  f32x16 st[2];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[sb] = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-  }
-  if constexpr (MASK) {
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
-  }
-  float mt = st[0][0];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = (sb == 0 ? 1 : 0); i < 16; ++i) mt = fmaxf(mt, st[sb][i]);
-  mt = half_swap_max(mt);
-  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
-  if (__builtin_amdgcn_ballot_w64(grow)) {  // wave-uniform: rescale only when some lane's max moved
-    const float m_new = grow ? mt : m_i;
-    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
-    l_i *= alpha;
-    m_i = m_new;
-    o[0] *= alpha;
-    o[1] *= alpha;
-  }
-  const float mc = m_i * scale_log2;
-  float rs = 0.0f;
-  bf16x8 pf[2][2];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    float pv[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p = fast_exp2(st[sb][i] * scale_log2 - mc);
-      rs += p;
-      if constexpr (DROP) {
-        const int kpos = kv0 + 32 * sb + acc_row(i, h);
-        const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
-        p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
-      }
-      pv[i] = p;
-    }
-    pack16(pv, pf[sb]);
-  }
-  l_i += half_swap_sum(rs);
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int r0 = 32 * sb + 16 * s2 + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s2], o[dt]);
-    }
-}
-
-template <int NS, bool DROP>
-#ifndef NSA_FWD2_MINW
-#define NSA_FWD2_MINW 2
-#endif
-__global__ __launch_bounds__(256, NSA_FWD2_MINW) void flash_fwd2_kernel(const bf16_t* __restrict__ qkv,
-                                                                         bf16_t* __restrict__ out,
-                                                                         float* __restrict__ lse_out, int B, int T,
-                                                                         int H, float scale_log2,
-                                                                         uint32_t drop_thresh, float drop_scale,
-                                                                         uint64_t seed) {
-  constexpr int D = 64;
-  constexpr int SLOT = 2 * DQ2_T;  // K, V [64][64]
-  constexpr int LA = NS - 1;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 127) / 128;
-  const int qt = n_qt - 1 - (int)(blockIdx.x / BH);  // heaviest (longest causal) tiles first
-  const int bh = blockIdx.x % BH;
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, r = lane & 31;
-  const int q0w = qt * 128 + 32 * w;
-  const int qpos = q0w + r;
-  const int qc = qpos < T ? qpos : T - 1;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-
-  // K / V tile j -> ring slot (the dQ v2 kernel's piece layout)
-  const int prow = 16 * w + (lane >> 3);
-  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
-  const bf16_t* krow = base + C + hh * D + (int64_t)prow * row_stride;
-  const int kv_end = min(T, qt * 128 + 128);
-  const int n_tiles = (kv_end + 63) / 64;
-  auto issue = [&](int j, int slot) {
-    const uint32_t sb = lds0 + (uint32_t)(slot * SLOT) + (uint32_t)(16 * w * 128);
-    const int64_t o = (int64_t)j * 64 * row_stride;
-    int64_t o0 = 0, o8 = 8 * row_stride;
-    if (j * 64 + 64 > T) {
-      const int k = j * 64 + prow;
-      o0 = (int64_t)(min(k, T - 1) - k) * row_stride;
-      o8 = (int64_t)(min(k + 8, T - 1) - k) * row_stride;
-    }
-    const bf16_t* k0 = krow + o + o0 + pch0 * 8;
-    const bf16_t* k8 = krow + o + o8 + pch1 * 8;
-    glds16(k0, sb);
-    glds16(k8, sb + 1024);
-    glds16(k0 + C, sb + DQ2_T);
-    glds16(k8 + C, sb + DQ2_T + 1024);
-  };
-  for (int j = 0; j < LA && j < n_tiles; ++j) issue(j, j);
-
-  // Q^T fragments (B operand): lane holds Q[qpos][16ks + 8h .. +8]
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
-  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // retire before the ring loop
-  f32x16 o[2];
-  o[0] = f32x16{};
-  o[1] = f32x16{};
-  float m_i = -1e30f, l_i = 0.0f;
-
-  auto open_tile = [&](int j) {
-    vm_wait(4 * min(LA - 1, n_tiles - 1 - j));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (j + LA < n_tiles) issue(j + LA, (j + LA) % NS);
-  };
-  auto tile = [&](int j, auto mask) {
-    constexpr bool M = decltype(mask)::value;
-    auto f = [&](auto slot) {
-      const char* kt = smem + decltype(slot)::value * SLOT;
-      fwd2_tile<M, DROP>(kt, kt + DQ2_T, qf, o, m_i, l_i, 64 * j, qpos, h, r, lane, scale_log2, dr);
-    };
-    slot_dispatch<0, NS>(j % NS, f);
-  };
-  const int m = min(q0w / 64, n_tiles);
-  int j = 0;
-  for (; j < m; ++j) {
-    open_tile(j);
-    tile(j, std::integral_constant<bool, false>{});
-  }
-  if (j < n_tiles) {
-    open_tile(j);
-    tile(j, std::integral_constant<bool, true>{});
-    ++j;
-  }
-  for (; j < n_tiles; ++j) open_tile(j);
-
-  // epilogue: O = O^T / l ; lane owns query qpos, registers hold d
-  if (qpos < T) {
-    const float inv_l = 1.0f / l_i;
-    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 u;
-        u.x = cvt2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
-        u.y = cvt2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
-        *reinterpret_cast<uint2*>(orow + d) = u;
-      }
-    }
-    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
-  }
-}
-
-// v2 backward's row constants, both [B, H, T]: nd = -rowsum(dO * O) (= -delta) and
-// nls = -lse / scale (the initial accumulators of dP' and S')
-template <int D>
-__global__ __launch_bounds__(256) void flash_bwd_pre2_kernel(const bf16_t* __restrict__ o,
-                                                            const bf16_t* __restrict__ dout,
-                                                            const float* __restrict__ lse, float* __restrict__ nd,
-                                                            float* __restrict__ nls, float inv_scale, int B, int T,
-                                                            int H) {
-  constexpr int LPR = D / 8;
-  const int C = H * D;
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t row = gid / LPR;  // (b*T + t)*H + h
-  const int sub = gid % LPR;
-  if (row >= (int64_t)B * T * H) return;
-  const int hh = row % H;
-  const int64_t bt = row / H;
-  const int t = bt % T, b = bt / T;
-  const int64_t off = bt * C + hh * D + sub * 8;
-  float a[8], g[8];
-  load8(o + off, a);
-  load8(dout + off, g);
-  float s = 0.0f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s += a[j] * g[j];
-#pragma unroll
-  for (int k = LPR / 2; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
-  const int64_t idx = ((int64_t)b * H + hh) * T + t;
-  if (sub == 0) nd[idx] = -s;
-  if (sub == 1) nls[idx] = -lse[idx] * inv_scale;
-}
-
 template <int D>
 hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H, float scale, float p,
                       uint64_t seed, hipStream_t s) {
   const int n_qt = (T + 127) / 128;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const int order = attn_order_env();
   if constexpr (D == 64) {
-    // NSA_FLASH_FWD = v1 (default: the register-staged kernel below) | v2s2 / v2s3 / v2s4
-    // (LDS-DMA ring slots).  A/B at B120 T1024 H12: v1 382, v2s2 420, v2s3 395, v2s4
-    // 424 us: v1's 127 VGPRs keep 4 waves per SIMD, v2's 168 three at most, and the
-    // deeper ring does not buy that back (identical outputs).
-    const char* e = getenv("NSA_FLASH_FWD");
+    // v3 (64 queries per wave, 4-slot K/V ring) by default without dropout once the grid
+    // has >= 4096 workgroups.  B120 T1024 H12 (5760 v3 workgroups): v1 377, v3 344 us
+    // (step 465.3 -> 463.9 ms); v3 halves the K/V re-reads, which pays once qkv (566 MB)
+    // no longer sits in the 256 MB Infinity Cache.  B60: v1 159 vs v3 188 us; with
+    // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
-    // default (no NSA_FLASH_FWD or "auto"): v3s4 without dropout once the grid has at least
-    // 8 rounds of 512 resident workgroups.  B120 T1024 H12 (5760 v3 workgroups): v1 377,
-    // v3s2 354, v3s3 383, v3s4 344 us (step 465.3 -> 463.9 ms); v3 halves the K/V re-reads,
-    // which pays once qkv (566 MB) no longer sits in the 256 MB Infinity Cache.  B60
-    // (2880): v1 159 vs v3 188 us; B32 T1000: v1 88 vs v3 99-108 us.  With dropout v1 (the
-    // per-element hash doubles v3's VALU chain: 109 vs 158 us at B16)
-    const bool v3_auto = (!e || e[0] == 'a') && !th && (int64_t)n_qt3 * B * H >= 4096;
-    if (v3_auto || (e && e[0] == 'v' && e[1] == '3')) {
-      // v3 = 64 queries per wave; v3s<NS> picks the K/V ring depth (default 4)
-      const int ns3 = (e && e[0] == 'v' && e[2] == 's' && e[3] >= '2' && e[3] <= '4') ? e[3] - '0' : 4;
-#define NSA_FWD3(NS)                                                                                          \
-  do {                                                                                                        \
-    if (th)                                                                                                   \
-      flash_fwd3_kernel<true, NS><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, \
-                                                                B, T, H, scale * kLog2e, th, dscale, seed);   \
-    else                                                                                                      \
-      flash_fwd3_kernel<false, NS><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out,             \
-                                                                 (float*)lse, B, T, H, scale * kLog2e, th,    \
-                                                                 dscale, seed);                               \
-    return hipGetLastError();                                                                                 \
-  } while (0)
-      if (ns3 == 2) NSA_FWD3(2);
-      if (ns3 == 3) NSA_FWD3(3);
-      NSA_FWD3(4);
-#undef NSA_FWD3
-    }
-    const int ns = (!e || e[0] != 'v' || e[1] == '1') ? 0 : (e[3] - '0');
-#define NSA_FWD2(NS)                                                                                            \
-  do {                                                                                                          \
-    if (th)                                                                                                     \
-      flash_fwd2_kernel<NS, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, \
-                                                               T, H, scale * kLog2e, th, dscale, seed);          \
-    else                                                                                                        \
-      flash_fwd2_kernel<NS, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,   \
-                                                                B, T, H, scale * kLog2e, th, dscale, seed);     \
-    return hipGetLastError();                                                                                   \
-  } while (0)
-    if (ns == 2) NSA_FWD2(2);
-    if (ns == 3) NSA_FWD2(3);
-    if (ns == 4) NSA_FWD2(4);
-#undef NSA_FWD2
-  }
-  if constexpr (D == 64) {
-    // v1 with LDS-DMA K/V staging (default) | NSA_FLASH_FWD=v1r: register staging
-    const char* e = getenv("NSA_FLASH_FWD");
-    if (!(e && e[0] == 'v' && e[1] == '1' && e[2] == 'r')) {
+    const int sel = flash_config().fwd;
+    const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
+    if (v3) {
       if (th)
-        flash_fwd_kernel<D, true, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
-                                                                     B, T, H, scale * kLog2e, th, dscale, seed,
-                                                                     attn_order_env());
+        flash_fwd3_kernel<true, 4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
+                                                                 H, scale * kLog2e, th, dscale, seed);
       else
-        flash_fwd_kernel<D, false, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out,
-                                                                      (float*)lse, B, T, H, scale * kLog2e, th,
-                                                                      dscale, seed, attn_order_env());
+        flash_fwd3_kernel<false, 4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B,
+                                                                  T, H, scale * kLog2e, th, dscale, seed);
       return hipGetLastError();
     }
+    // v1 with LDS-DMA K/V staging
+    if (th)
+      flash_fwd_kernel<D, true, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B,
+                                                                   T, H, scale * kLog2e, th, dscale, seed, order);
+    else
+      flash_fwd_kernel<D, false, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
+                                                                    B, T, H, scale * kLog2e, th, dscale, seed, order);
+    return hipGetLastError();
   }
+  // D = 32 / 128: register-staged v1
   if (th)
     flash_fwd_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                           scale * kLog2e, th, dscale, seed, attn_order_env());
+                                                           scale * kLog2e, th, dscale, seed, order);
   else
-    flash_fwd_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
-                                                            H, scale * kLog2e, th, dscale, seed, attn_order_env());
+    flash_fwd_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+                                                            scale * kLog2e, th, dscale, seed, order);
   return hipGetLastError();
 }
 
+// generic backward (any D, any T): delta pre-pass -> dK/dV kernel -> dQ kernel.
+// ws[0] = delta [B, H, T].
 template <int D>
-hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const void* lse, void* delta, void* dq_acc,
-                      void* dqkv, int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
-  // dq_acc == nullptr selects the split mode: dK/dV kernel + per-query-tile dQ kernel
-  const bool split = dq_acc == nullptr;
-  const int64_t rows = (int64_t)B * T * H;
-  const int64_t threads = rows * (D / 8);
-  flash_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-      (const bf16_t*)o, (const bf16_t*)dout, (float*)delta, (float*)dq_acc, B, T, H);
+hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const void* lse, void* delta, void* dqkv,
+                      int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
+  const int64_t threads = (int64_t)B * T * H * (D / 8);
+  flash_bwd_pre_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)dout,
+                                                                             (float*)delta, B, T, H);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_kb = (T + BwdGeo<D>::KB - 1) / BwdGeo<D>::KB;
   const dim3 grid(n_kb * B * H), block(BwdGeo<D>::NW * 64);
-#define NSA_BWD_ARGS                                                                                  \
-  (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (float*)dq_acc,  \
-      (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale, seed
-  if (th) {
-    if (split) flash_bwd_kernel<D, true, false><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
-    else flash_bwd_kernel<D, true, true><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
-  } else {
-    if (split) flash_bwd_kernel<D, false, false><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
-    else flash_bwd_kernel<D, false, true><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
-  }
+#define NSA_BWD_ARGS                                                                                        \
+  (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H, \
+      scale, scale * kLog2e, th, dscale, seed
+  if (th) flash_bwd_kernel<D, true><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
+  else flash_bwd_kernel<D, false><<<grid, block, 0, s>>>(NSA_BWD_ARGS);
 #undef NSA_BWD_ARGS
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (split) {
-    const int n_qt = (T + 127) / 128;
-    if (th)
-      flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
-          scale, scale * kLog2e, th, dscale, seed, 1.0f);
-    else
-      flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>(
-          (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
-          scale, scale * kLog2e, th, dscale, seed, 1.0f);
-    return hipGetLastError();
-  }
-  const int C = H * D;
-  const int64_t work = (int64_t)B * T * (C / 8);
-  dq_convert_kernel<<<(unsigned)((work + 255) / 256), 256, 0, s>>>((const float*)dq_acc, (bf16_t*)dqkv,
-                                                                   (int64_t)B * T, C);
+  const int n_qt = (T + 127) / 128;
+  if (th)
+    flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>(
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
+        scale, scale * kLog2e, th, dscale, seed, 1.0f);
+  else
+    flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>(
+        (const bf16_t*)qkv, (const bf16_t*)dout, (const float*)lse, (const float*)delta, (bf16_t*)dqkv, B, T, H,
+        scale, scale * kLog2e, th, dscale, seed, 1.0f);
   return hipGetLastError();
 }
 
-// v2 backward (D = 64, T % 32 == 0): dQ v2 kernel (also forms the row constants -delta,
-// -lse/scale) -> dK/dV v2 kernel.  ws = 2 x [B, H, T] fp32.  NSA_FLASH_DQ2=0: pre2 ->
-// dK/dV v2 -> v1 dQ kernel.
+// v2 backward (D = 64, T % 32 == 0): the dQ v2 kernel (which also forms the row
+// constants -delta, -lse/scale) -> the dK/dV v2 kernel, 1 key block per wave, 4 waves
+// (two independent workgroups per CU).  ws = 2 x [B, H, T] fp32.  A/B at B120 T1024 H12
+// (whole backward): v1 1307, 2 key blocks per wave 1304, 8 waves 1203, this 1189 us.
 hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws, void* dqkv,
                          int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
-  constexpr int D = 64;
   float* nd = (float*)ws;
   float* nls = nd + (int64_t)B * H * T;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_qt = (T + 127) / 128;
-  hipError_t e;
-  const char* dq2 = getenv("NSA_FLASH_DQ2");
-  const bool use_dq2 = !(dq2 && dq2[0] == '0');
-  if (use_dq2) {
-    // dQ first: it also writes the row constants (-delta, -lse/scale) the dK/dV kernel reads
-    if (th)
-      flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                              (const bf16_t*)o, (const float*)lse, nls, nd,
-                                                              (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                              dscale, seed, attn_order_env());
-    else
-      flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                               (const bf16_t*)o, (const float*)lse, nls, nd,
-                                                               (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                               dscale, seed, attn_order_env());
-  } else {
-    const int64_t threads = (int64_t)B * T * H * (D / 8);
-    flash_bwd_pre2_kernel<D><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(
-        (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, nd, nls, 1.0f / scale, B, T, H);
-  }
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  // geometry (NSA_FLASH_DKDV): k1w4 = 1 key block per wave, 4 waves (default: 216 VGPRs,
-  // two independent workgroups per CU), k1w8, k2w4 (2 key blocks per wave, 1 wave/SIMD).
-  // A/B at B120 T1024 H12 (whole backward incl. the dQ kernel): v1 1307, k2w4 1304,
-  // k1w8 1203, k1w4 1189 us.
   const int order = attn_order_env();
-  const char* g = getenv("NSA_FLASH_DKDV");
-  const int geo = (g && g[0] == 'k' && g[1] == '2') ? 0 : (g && g[0] == 'k' && g[3] == '8') ? 1
-                  : (g && g[0] == 'k' && g[4] == 'p') ? 3 : 2;
-#define NSA_DKDV2(NKB, NW, PIPE)                                                                              \
-  do {                                                                                                        \
-    const int n_kb = (T + 32 * NKB * NW - 1) / (32 * NKB * NW);                                              \
-    if (th)                                                                                                   \
-      flash_bwd_dkdv2_kernel<NKB, NW, true, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                           \
-          (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
-          dscale, seed, order);                                                                               \
-    else                                                                                                      \
-      flash_bwd_dkdv2_kernel<NKB, NW, false, PIPE><<<n_kb * B * H, NW * 64, 0, s>>>(                          \
-          (const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, \
-          dscale, seed, order);                                                                               \
-  } while (0)
-  if (geo == 1) NSA_DKDV2(1, 8, false);
-  else if (geo == 2) NSA_DKDV2(1, 4, false);
-  else if (geo == 3) NSA_DKDV2(1, 4, true);
-  else NSA_DKDV2(2, 4, false);
-#undef NSA_DKDV2
-  e = hipGetLastError();
-  if (e != hipSuccess || use_dq2) return e;
-  // NSA_FLASH_DQ2=0: the v1 dQ kernel (reads -delta with delta_sign = -1)
   if (th)
-    flash_bwd_dq_kernel<D, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                              (const float*)lse, nd, (bf16_t*)dqkv, B, T, H, scale,
-                                                              scale * kLog2e, th, dscale, seed, -1.0f);
+    flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                            (const bf16_t*)o, (const float*)lse, nls, nd, (bf16_t*)dqkv,
+                                                            B, T, H, scale, scale * kLog2e, th, dscale, seed, order);
   else
-    flash_bwd_dq_kernel<D, false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                               (const float*)lse, nd, (bf16_t*)dqkv, B, T, H, scale,
-                                                               scale * kLog2e, th, dscale, seed, -1.0f);
+    flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                             (const bf16_t*)o, (const float*)lse, nls, nd,
+                                                             (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th, dscale,
+                                                             seed, order);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int n_kb = (T + 127) / 128;
+  if (th)
+    flash_bwd_dkdv2_kernel<1, 4, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
+                                                                   (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
+                                                                   dscale, seed, order);
+  else
+    flash_bwd_dkdv2_kernel<1, 4, false><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls,
+                                                                    nd, (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e,
+                                                                    th, dscale, seed, order);
   return hipGetLastError();
-}
-
-bool bwd2_enabled() {
-  const char* e = getenv("NSA_FLASH_BWD");
-  return !(e && e[0] == 'v' && e[1] == '1');
 }
 
 }  // namespace
 
 // Backward with a 2 x [B, H, T] fp32 workspace.  D = 64 with T % 32 == 0 runs the v2
-// dK/dV kernel (NSA_FLASH_BWD=v1 selects the 32-keys-per-wave kernel instead, for
-// A/B); every other shape runs the split-mode v1 backward with ws[0] as delta.
+// kernels (unless the bwd variant is v1); every other shape the generic backward with
+// ws[0] as delta.
 NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (D == 64 && T % 32 == 0 && bwd2_enabled())
+  if (D == 64 && T % 32 == 0 && flash_config().bwd == BWD_V2)
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
-    case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
-    case 64: return bwd_launch<64>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
-    case 128: return bwd_launch<128>(qkv, o, dout, lse, ws, nullptr, dqkv, B, T, H, scale, p, seed, s);
+    case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
+    case 64: return bwd_launch<64>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
+    case 128: return bwd_launch<128>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2300,13 +1750,14 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
   }
 }
 
-NSA_API hipError_t nsa_flash_bwd(const void* qkv, const void* o, const void* dout, const void* lse, void* delta,
-                                 void* dq_acc, void* dqkv, int B, int T, int H, int D, float scale, float p,
-                                 uint64_t seed, hipStream_t s) {
-  switch (D) {
-    case 32: return bwd_launch<32>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
-    case 64: return bwd_launch<64>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
-    case 128: return bwd_launch<128>(qkv, o, dout, lse, delta, dq_acc, dqkv, B, T, H, scale, p, seed, s);
-    default: return hipErrorInvalidValue;
-  }
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3, bwd 1 v1 / 2 v2, order
+// 0 / 1; a negative value keeps the current setting.  Returns the previous selection as
+// fwd | bwd << 4 | order << 8.
+NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
+  FlashConfig& c = flash_config();
+  const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3) c.fwd = fwd;
+  if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
+  if (order == 0 || order == 1) c.order = order;
+  return prev;
 }

@@ -305,13 +305,17 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
   }
 }
 
-// nontemporal streams in the LayerNorm passes (default; NSA_LN_NT=0 turns them off, read per
-// launch for A/B runs).  GPT-2 124M step, same box, interleaved: 462.7 / 463.3 ms without,
+// nontemporal streams in the LayerNorm passes (default; NSA_LN_NT=0 turns them off, read once;
+// nsa_ln_set_nt switches them for A/B runs).  GPT-2 124M step, same box, interleaved: 462.7 / 463.3 ms without,
 // 461.6 / 461.7 ms with
-bool ln_nt() {
-  const char* e = getenv("NSA_LN_NT");
-  return !(e && e[0] == '0');
+int& ln_nt_flag() {  // resolved once from NSA_LN_NT (0 = plain); nsa_ln_set_nt for A/B
+  static int f = [] {
+    const char* e = getenv("NSA_LN_NT");
+    return !(e && e[0] == '0') ? 1 : 0;
+  }();
+  return f;
 }
+bool ln_nt() { return ln_nt_flag() != 0; }
 
 template <int NK, typename XT>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
@@ -396,4 +400,11 @@ NSA_API hipError_t nsa_layernorm_bwd_x32(const void* dy, const void* x, const vo
   if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
   NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
                                                         N, C, nblk, s)));
+}
+
+// set the streaming-store policy of the LayerNorm kernels (on < 0: keep); returns the old one
+NSA_API int nsa_ln_set_nt(int on) {
+  const int prev = ln_nt_flag();
+  if (on >= 0) ln_nt_flag() = on ? 1 : 0;
+  return prev;
 }

@@ -63,8 +63,9 @@ _SIGNATURES = {
     "nsa_clip_coef": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p],
     "nsa_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_flash_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
-    "nsa_flash_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                      c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
+    "nsa_flash_set_variant": [c_int, c_int, c_int],
+    "nsa_ew_set_nt": [c_int],
+    "nsa_ln_set_nt": [c_int],
     "nsa_kv_append": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_decode_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                         c_float, c_int, c_void_p],
@@ -132,6 +133,14 @@ def ptr(t):
 
 def stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+def call_ret(name, *args):
+    """Call an entry point that returns a value (not a hipError_t)."""
+    fn = getattr(lib(), name, None)
+    if fn is None:
+        raise KernelLibraryMissing(f"{name} missing from {LIB_PATH}; rebuild the kernel library")
+    return fn(*args)
 
 
 def call(name, *args):

@@ -31,6 +31,7 @@ and the gradcheck tests).
 
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from typing import NamedTuple
@@ -617,12 +618,23 @@ def _attn_reference(q, k, v, p, seed):
     return att @ v
 
 
-# Flash-attention backward dQ strategy (csrc/kernels/flash_attn.hip bwd_launch):
-#   split  — dK/dV kernel (no dQ work, 34 KB LDS) + a per-query-tile dQ kernel that
-#            recomputes S and dP and writes dQ once in bf16 (no atomics, no fp32 buffer)
-#   atomic — one kernel; dS crosses LDS, dQ partials are atomically added into an fp32
-#            accumulator, then converted
-FLASH_DQ_SPLIT = os.environ.get("NSA_FLASH_DQ", "split") == "split"
+_FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3}
+_FLASH_BWD = {"v1": 1, "v2": 2}
+
+
+@contextlib.contextmanager
+def flash_variant(fwd: str | None = None, bwd: str | None = None, order: int | None = None):
+    """Select flash-attention kernels for the duration of a ``with`` block (tests, A/B).
+
+    The library resolves its choice once per process (``NSA_FLASH_FWD`` / ``NSA_FLASH_BWD``
+    / ``NSA_ATTN_ORDER``, csrc/kernels/flash_attn.hip FlashConfig); this switches it through
+    ``nsa_flash_set_variant`` and restores the previous selection afterwards."""
+    prev = _lib.call_ret("nsa_flash_set_variant", _FLASH_FWD[fwd] if fwd else -1, _FLASH_BWD[bwd] if bwd else -1,
+                         -1 if order is None else int(order))
+    try:
+        yield
+    finally:
+        _lib.call_ret("nsa_flash_set_variant", prev & 0xF, (prev >> 4) & 0xF, (prev >> 8) & 0xF)
 
 
 class AttentionFn(torch.autograd.Function):
@@ -657,20 +669,12 @@ class AttentionFn(torch.autograd.Function):
             qkv, y, lse = ctx.saved_tensors
             dy = dy.contiguous()
             dqkv = torch.empty_like(qkv)
-            # delta = rowsum(dO * O) filled by the kernel's one-pass preprocessing (which also
-            # zeroes dq_acc in the atomic mode; the split mode writes dQ once, in bf16)
             _streams.before_compute(dy)
-            if FLASH_DQ_SPLIT:
-                # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
-                # D = 64 runs the 64-keys-per-wave dK/dV kernel (NSA_FLASH_BWD=v1: the older one)
-                ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
-                _lib.call("nsa_flash_bwd2", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(ws),
-                          _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
-                return dqkv, None, None
-            dq_acc = torch.empty(B, T, C, device=dy.device, dtype=F32)
-            delta = torch.empty(B, H, T, device=dy.device, dtype=F32)
-            _lib.call("nsa_flash_bwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(delta),
-                      _lib.ptr(dq_acc), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
+            # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
+            # dQ is written once, in bf16, by its own kernel (no atomics)
+            ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
+            _lib.call("nsa_flash_bwd2", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(ws),
+                      _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
             return dqkv, None, None
         (qkv,) = ctx.saved_tensors
         with torch.enable_grad():

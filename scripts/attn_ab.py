@@ -1,12 +1,13 @@
 """A/B of flash-attention kernel variants at the GPT-2 training shape (one process,
 interleaved rounds, random data; cdna_hip_programming.md §5.4 rules 24-25).
 
-Variants are selected per launch through environment switches read by the kernel
-library (e.g. NSA_FLASH_BWD=v1 for the 32-keys-per-wave dK/dV kernel).  Also checks that
-every variant's outputs match the first variant's.
+Variants are "name:key=value,..." with keys fwd (auto / v1 / v3), bwd (v2 / v1) and
+order (0 / 1), switched through ops.functional.flash_variant (the library resolves its
+selection once; nsa_flash_set_variant changes it).  Also checks that every variant's
+outputs match the first variant's.
 
     python scripts/attn_ab.py [--B 120] [--T 1024] [--H 12] [--D 64] [--rounds 7]
-        [--bwd "v2:NSA_FLASH_BWD=v2;v1:NSA_FLASH_BWD=v1"] [--fwd "default:"]
+        [--bwd "v2:bwd=v2;v1:bwd=v1"] [--fwd "auto:;v1:fwd=v1"]
 """
 
 import argparse
@@ -36,16 +37,11 @@ def parse(spec):
 
 
 def with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    from nanosandbox_amd.ops.functional import flash_variant
+
+    with flash_variant(fwd=env.get("fwd"), bwd=env.get("bwd"),
+                       order=int(env["order"]) if "order" in env else None):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def main():
@@ -57,8 +53,8 @@ def main():
     ap.add_argument("--p", type=float, default=0.0)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--bwd", default="v2:NSA_FLASH_BWD=v2;v1:NSA_FLASH_BWD=v1")
-    ap.add_argument("--fwd", default="default:")
+    ap.add_argument("--bwd", default="v2:bwd=v2;v1:bwd=v1")
+    ap.add_argument("--fwd", default="auto:")
     a = ap.parse_args()
     B, T, H, D = a.B, a.T, a.H, a.D
     C = H * D

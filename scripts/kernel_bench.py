@@ -69,18 +69,16 @@ def main():
         lse = torch.empty(B, H, T, device=dev)
         dy = torch.randn(B, T, C, device=dev).to(BF)
         dqkv = torch.empty_like(qkv)
-        delta = torch.empty(B, H, T, device=dev)
-        dq = torch.zeros(B, T, C, device=dev)
         sc = 1.0 / math.sqrt(D)
 
         def fwd():
             _lib.call("nsa_flash_fwd", qkv.data_ptr(), y.data_ptr(), lse.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
-        split = os.environ.get("NSA_FLASH_DQ", "split") == "split"
+        ws = torch.empty(2, B, H, T, device=dev)
 
-        def bwd():  # the kernel's preprocessing pass zeroes dq itself (atomic mode)
-            _lib.call("nsa_flash_bwd", qkv.data_ptr(), y.data_ptr(), dy.data_ptr(), lse.data_ptr(), delta.data_ptr(),
-                      None if split else dq.data_ptr(), dqkv.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
+        def bwd():
+            _lib.call("nsa_flash_bwd2", qkv.data_ptr(), y.data_ptr(), dy.data_ptr(), lse.data_ptr(), ws.data_ptr(),
+                      dqkv.data_ptr(), B, T, H, D, sc, 0.0, 0, st())
 
         flops = 4.0 * B * H * T * T * D / 2  # causal
         tf = timeit(fwd)

@@ -101,11 +101,11 @@ def main():
             "copy": (lambda: g.copy_(u), 2 * n * 2),
         }
 
-        def plain(fn):  # same kernel without nontemporal loads / stores (NSA_EW_NT=0, read per launch)
+        def plain(fn):  # same kernel without nontemporal loads / stores (nsa_ew_set_nt)
             def run_plain():
-                os.environ["NSA_EW_NT"] = "0"
+                prev = _lib.call_ret("nsa_ew_set_nt", 0)
                 fn()
-                os.environ.pop("NSA_EW_NT")
+                _lib.call_ret("nsa_ew_set_nt", prev)
             return run_plain
         cands["gelu_fwd_plain"] = (plain(cands["gelu_fwd"][0]), cands["gelu_fwd"][1])
         cands["gelu_bwd_plain"] = (plain(cands["gelu_bwd"][0]), cands["gelu_bwd"][1])

@@ -2,6 +2,7 @@
 
 dW[N_out, K_in] (fp32) += dY[T, N_out]^T · X[T, K_in] over T tokens, as:
   * nsa<v>/s<S>   our split-K kernel (fp32 atomics), the tuner's candidates
+  * det<v>/s<S>   the same kernel storing per-split partials + one ordered reduction (--det)
   * blt           one hipBLASLt addmm with fp32 output
   * bmm<S>        hipBLASLt strided-batched split-K: S partial [N_out, K_in] fp32 products
                   (bmm out_dtype=fp32), then one fixed-order reduction pass (nsa_splitk_reduce)
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--bmm-splits", default="2,4,7,8,14")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--variants", default="1,7")
+    ap.add_argument("--det", action="store_true", help="also the deterministic form (partials + ordered reduce)")
     ap.add_argument("--only", default="", help="comma list of candidate names to keep (e.g. nsa7/s7,nsa11/s7)")
     a = ap.parse_args()
     T = a.m
@@ -65,6 +67,9 @@ def main():
                 for v in [int(t) for t in a.variants.split(",")]:
                     sv = s
                     cands[f"nsa{v}/s{sv}"] = (lambda sv=sv, v=v: gemm.wgrad_acc(dy, x, g, splits=sv, variant=v))
+                    if a.det and sv > 1:
+                        cands[f"det{v}/s{sv}"] = (lambda sv=sv, v=v: gemm.wgrad_acc(dy, x, g, splits=sv, variant=v,
+                                                                                    deterministic=True))
         for S in [int(v) for v in a.bmm_splits.split(",") if v]:
             if T % S or (T // S) % 8:
                 continue

@@ -257,13 +257,30 @@ def attn_ref(qkv, H):
     return y.transpose(1, 2).reshape(B, T, C)
 
 
-@pytest.mark.parametrize("fwd", ["v2s3", "v2s2", "v2s4", "v1", "v3s2", "v3s3", "v3s4", "auto"])
+@pytest.fixture
+def flash_variant(kernels):
+    """ops.functional.flash_variant as a fixture: selects kernels for one test, restores after."""
+    from nanosandbox_amd.ops.functional import flash_variant as fv
+
+    stack = []
+
+    def select(**kw):
+        cm = fv(**kw)
+        cm.__enter__()
+        stack.append(cm)
+
+    yield select
+    while stack:
+        stack.pop().__exit__(None, None, None)
+
+
+@pytest.mark.parametrize("fwd", ["v1", "v3", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
-def test_flash_attention(kernels, monkeypatch, B, T, H, D, fwd):
+def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
     from nanosandbox_amd import ops
 
-    monkeypatch.setenv("NSA_FLASH_FWD", fwd)  # forward variant (D = 64 only; others ignore it)
+    flash_variant(fwd=fwd)  # forward variant (D = 64 only; others ignore it)
 
     torch.manual_seed(0)
     C = H * D
@@ -282,9 +299,9 @@ def test_flash_attention(kernels, monkeypatch, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v2s3", "v1", "v3s4"])
+@pytest.mark.parametrize("fwd", ["v1", "v3"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes"])
-def test_flash_attention_deferred_rescale(kernels, monkeypatch, pattern, fwd):
+def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
 
     "rising": every tile's max exceeds the running max by more than the defer
@@ -295,7 +312,7 @@ def test_flash_attention_deferred_rescale(kernels, monkeypatch, pattern, fwd):
     """
     from nanosandbox_amd import ops
 
-    monkeypatch.setenv("NSA_FLASH_FWD", fwd)
+    flash_variant(fwd=fwd)
     torch.manual_seed(1)
     B, T, H, D = 1, 512, 2, 64
     C = H * D
@@ -331,11 +348,10 @@ def test_flash_attention_deferred_rescale(kernels, monkeypatch, pattern, fwd):
 
 @pytest.mark.parametrize("T", [320, 1024, 96])
 @pytest.mark.parametrize("p", [0.0, 0.2])
-@pytest.mark.parametrize("geo,dq2", [("k1w4", "1"), ("k1w8", "1"), ("k2w4", "1"), ("k1w4", "0")])
-def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo, dq2):
-    """The v2 backward (D = 64: LDS-DMA-fed dK/dV kernel in each geometry + the v2 dQ
-    kernel) against the v1 kernels, with and without dropout; T = 320 and 96 leave the
-    last key / query workgroups partial."""
+def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
+    """The v2 backward (D = 64: LDS-DMA-fed dK/dV kernel + the v2 dQ kernel) against the
+    generic kernels, with and without dropout; T = 320 and 96 leave the last key / query
+    workgroups partial."""
     from nanosandbox_amd.ops import functional as fn
 
     torch.manual_seed(0)
@@ -343,10 +359,8 @@ def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo, dq2):
     qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
     dy = torch.randn(B, T, H * D, device=DEV).to(BF)
     grads = {}
-    monkeypatch.setenv("NSA_FLASH_DKDV", geo)
-    monkeypatch.setenv("NSA_FLASH_DQ2", dq2)  # 0: pre-pass + v1 dQ kernel after the v2 dK/dV
     for ver in ("v1", "v2"):
-        monkeypatch.setenv("NSA_FLASH_BWD", ver)
+        flash_variant(bwd=ver)
         torch.manual_seed(5)
         x = qkv.clone().requires_grad_(True)
         fn.attention(x, H, p, True).backward(dy)
@@ -358,46 +372,36 @@ def test_flash_bwd_v2_matches_v1(kernels, monkeypatch, p, T, geo, dq2):
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])
-def test_flash_bwd_split_matches_atomic(kernels, monkeypatch, p):
-    """The two dQ strategies of the backward (split: separate dQ kernel, bf16 written
-    once; atomic: fp32 atomics from the dK/dV kernel) give the same gradients, with and
-    without dropout (same seed -> same regenerated mask)."""
-    from nanosandbox_amd.ops import functional as fn
-
-    torch.manual_seed(0)
-    B, T, H, D = 2, 320, 3, 64
-    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
-    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
-    grads = {}
-    for split in (True, False):
-        monkeypatch.setattr(fn, "FLASH_DQ_SPLIT", split)
-        torch.manual_seed(5)  # the dropout seed is drawn from torch's CPU generator
-        x = qkv.clone().requires_grad_(True)
-        fn.attention(x, H, p, True).backward(dy)
-        grads[split] = x.grad.float().view(B, T, 3, H * D)
-    for i, name in enumerate("qkv"):
-        e = rel_err(grads[True][:, :, i], grads[False][:, :, i])
-        assert e < 1e-2, f"d{name}: split vs atomic rel err {e}"
-
-
-@pytest.mark.parametrize("p", [0.0, 0.2])
-def test_flash_fwd_v2_matches_v1(kernels, monkeypatch, p):
-    """Forward v2 / v3 (LDS-DMA rings, every ring depth) against v1, with and without dropout
-    (the same counter-hash mask): outputs and LSE-dependent gradients agree."""
+def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
+    """Forward v3 (64 queries per wave, LDS-DMA ring) against v1, with and without dropout
+    (the same counter-hash mask)."""
     from nanosandbox_amd.ops import functional as fn
 
     torch.manual_seed(0)
     B, T, H, D = 2, 384, 3, 64
     qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
     outs = {}
-    for ver in ("v1", "v2s2", "v2s3", "v2s4", "v3s2", "v3s3", "v3s4"):
-        monkeypatch.setenv("NSA_FLASH_FWD", ver)
+    for ver in ("v1", "v3"):
+        flash_variant(fwd=ver)
         torch.manual_seed(5)
         outs[ver] = fn.attention(qkv, H, p, True).float()
         torch.cuda.synchronize()
-    for ver in ("v2s2", "v2s3", "v2s4", "v3s2", "v3s3", "v3s4"):
-        e = rel_err(outs[ver], outs["v1"])
-        assert e < 5e-3, f"{ver} vs v1 rel err {e}"
+    e = rel_err(outs["v3"], outs["v1"])
+    assert e < 5e-3, f"v3 vs v1 rel err {e}"
+
+
+def test_flash_variant_is_resolved_once(kernels, monkeypatch):
+    """The library reads NSA_FLASH_* once; a later environment change does not switch
+    kernels (only nsa_flash_set_variant does), and the context manager restores."""
+    from nanosandbox_amd.ops import _lib
+    from nanosandbox_amd.ops.functional import flash_variant as fv
+
+    before = _lib.call_ret("nsa_flash_set_variant", -1, -1, -1)
+    monkeypatch.setenv("NSA_FLASH_FWD", "v1" if (before & 0xF) != 1 else "v3")
+    assert _lib.call_ret("nsa_flash_set_variant", -1, -1, -1) == before
+    with fv(fwd="v1", bwd="v1", order=1):
+        assert _lib.call_ret("nsa_flash_set_variant", -1, -1, -1) == 1 | (1 << 4) | (1 << 8)
+    assert _lib.call_ret("nsa_flash_set_variant", -1, -1, -1) == before
 
 
 def test_flash_attention_dropout_statistics(kernels):
