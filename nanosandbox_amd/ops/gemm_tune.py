@@ -204,16 +204,20 @@ def _library_ok(M, N, K):
                 and M * N * K >= 2 ** 34)
 
 
-def fwd(x2, w):
-    """y = x2 @ w^T (bf16)."""
+def _fwd_pick(x2, w):
+    """The forward backend for this shape ("hipblaslt" / "nt"; tuned on first use)."""
     M, K = x2.shape
     N = w.shape[0]
     if not (_nsa_ok(x2, w) and _gemm.nt_supported(M, N, K)):
-        return x2 @ w.t()
+        return "hipblaslt"
     cands = {"hipblaslt": lambda: x2 @ w.t()} if _library_ok(M, N, K) else {}
     cands["nt"] = lambda: _gemm.nt(x2, w)
-    name = choose(("fwd", M, N, K), cands)
-    return x2 @ w.t() if name == "hipblaslt" else _gemm.nt(x2, w)
+    return choose(("fwd", M, N, K), cands)
+
+
+def fwd(x2, w):
+    """y = x2 @ w^T (bf16)."""
+    return x2 @ w.t() if _fwd_pick(x2, w) == "hipblaslt" else _gemm.nt(x2, w)
 
 
 # Weight generation: bumped whenever the bf16 compute weights are rewritten outside
@@ -261,18 +265,23 @@ def _transpose(w, out=None):
     return w.t().contiguous()
 
 
+def _dgrad_pick(dy2, w):
+    """The input-gradient backend for this shape (tuned on first use)."""
+    M, N = dy2.shape
+    K = w.shape[1]
+    if not (_nsa_ok(dy2, w) and _gemm.nt_supported(M, K, N)):
+        return "hipblaslt"
+    cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
+    cands["nt"] = lambda: _gemm.nt(dy2, _wt(w))
+    return choose(("dgrad", M, N, K), cands)
+
+
 def dgrad(dy2, w):
     """dx = dy2 @ w (bf16)."""
     from . import streams
 
     streams.before_compute(dy2)  # the side stream's weight GEMMs never share the GPU with this one
-    M, N = dy2.shape
-    K = w.shape[1]
-    if not (_nsa_ok(dy2, w) and _gemm.nt_supported(M, K, N)):
-        return dy2 @ w
-    cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
-    cands["nt"] = lambda: _gemm.nt(dy2, _wt(w))
-    name = choose(("dgrad", M, N, K), cands)
+    name = _dgrad_pick(dy2, w)
     if name == "hipblaslt":
         return dy2 @ w
     if name == "hipblaslt_t":
@@ -308,9 +317,12 @@ def fwd_gelu(x2, w):
         u = fwd(x2, w)
         return u, _gelu_fwd(u)
 
-    cands = {"split": split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)}
+    # the split form counts as a library candidate when its GEMM is the library's, so the
+    # fused kernel wins within NATIVE_MARGIN of it (as against a plain library GEMM)
+    sname = "split_lib" if _is_library(_fwd_pick(x2, w)) else "split"
+    cands = {sname: split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)}
     name = choose(("fwd_gelu", M, N, K), cands)
-    return split() if name == "split" else _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)
+    return split() if name.startswith("split") else _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)
 
 
 def dgrad_dgelu(dy2, w, u, between=None):
@@ -333,9 +345,10 @@ def dgrad_dgelu(dy2, w, u, between=None):
             hook()
         return _gelu_bwd(dg, u)
 
-    cands = {"split": split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)}
+    sname = "split_lib" if _is_library(_dgrad_pick(dy2, w)) else "split"
+    cands = {sname: split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)}
     name = choose(("dgrad_dgelu", M, N, K), cands)
-    if name == "split":
+    if name.startswith("split"):
         return split(between)
     du = _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)
     if between is not None:
