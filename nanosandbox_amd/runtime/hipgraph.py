@@ -23,8 +23,15 @@ Why it is sound here:
   (``ops.rng_advance``), so each replay draws fresh masks, identical between its
   forward and backward.
 
-When it is not used (eager fallback, decided by ``graph_capture_supported``):
-more than one rank (bucket-ready hooks are Python callbacks), CPU devices.
+More than one rank (flat bucket reducer only): the gradient-bucket hooks are Python
+callbacks that launch RCCL all-reduces as buckets complete, so the synchronising micro-step
+cannot be a replay.  The captured graph (reducer disarmed, no communication) runs the
+gas - 1 accumulation micro-steps; the last micro-step runs eagerly with the reducer armed,
+its bucket all-reduces overlapping its backward as without graphs.  At gas = 1 (one
+micro-step per rank, e.g. 8 ranks on the 480-sequence batch) nothing is captured.
+
+When it is not used (eager fallback, decided by ``graph_capture_supported``): CPU
+devices, and torch's own DDP wrapper (its reducer hooks autograd itself).
 """
 
 from __future__ import annotations
@@ -32,11 +39,14 @@ from __future__ import annotations
 import torch
 
 
-def graph_capture_supported(device: str, dropout: float, world_size: int) -> tuple[bool, str]:
+def graph_capture_supported(device: str, dropout: float, world_size: int, ddp_impl: str = "flat",
+                            gas: int = 2) -> tuple[bool, str]:
     if not str(device).startswith("cuda") or not torch.cuda.is_available():
         return False, "graph capture needs a GPU device"
-    if world_size > 1:
-        return False, "world_size > 1: gradient-bucket hooks run in Python during backward"
+    if world_size > 1 and ddp_impl != "flat":
+        return False, "torch DDP: its reducer hooks autograd (use ddp_impl='flat')"
+    if world_size > 1 and gas < 2:
+        return False, "one micro-step per rank: the synchronising micro-step always runs eagerly"
     return True, ""
 
 

@@ -155,10 +155,12 @@ class Trainer:
         self.graph = None
         self.use_graph = False
         if c["compile"]:
-            ok, why = graph_capture_supported(self.device, c["dropout"], info.world_size)
+            ok, why = graph_capture_supported(self.device, c["dropout"], info.world_size, self.ddp_impl, self.gas)
             self.use_graph = ok
-            print("compile=True: micro-step captured as a HIP graph" if ok
-                  else f"compile=True: eager micro-steps ({why})")
+            if self.master:
+                print(("compile=True: micro-step captured as a HIP graph" +
+                       (" (the synchronising micro-step runs eagerly)" if info.world_size > 1 else "")) if ok
+                      else f"compile=True: eager micro-steps ({why})")
 
         # ----------------------------------------------------------------- DDP
         self.raw_model = model
@@ -223,19 +225,19 @@ class Trainer:
 
         Returns (last micro-step loss tensor, grad-norm tensor or None, next X, next Y)."""
         c = self.cfg
-        if self.use_graph:
+        # with a reducer (world > 1) the synchronising last micro-step runs eagerly below
+        n_graph = (self.gas - 1 if self.reducer is not None else self.gas) if self.use_graph else 0
+        if n_graph > 0:
             if self.graph is None:
+                if self.reducer is not None:
+                    self.reducer.prepare(False)  # capture with the bucket hooks disarmed
                 self.graph = MicroStepGraph(self.model, X, Y, self.gas,
                                             zero_grad=lambda: self.optimizer.zero_grad(set_to_none=True),
                                             dropout=c["dropout"] > 0.0)
-            for _ in range(self.gas):
+            for _ in range(n_graph):
                 loss = self.graph.run(X, Y)
                 X, Y = self.batches.get_batch("train")
-            norm = self.optimizer.clip_grad_norm_(c["grad_clip"]) if c["grad_clip"] != 0.0 else None
-            self.optimizer.step()
-            self.optimizer.zero_grad(set_to_none=True)
-            return loss, norm, X, Y
-        for micro_step in range(self.gas):
+        for micro_step in range(n_graph, self.gas):
             sync = micro_step == self.gas - 1
             if self.reducer is not None:
                 self.reducer.prepare(sync)

@@ -185,3 +185,58 @@ def test_ddp_gpu_production_kernels(tmp_path, monkeypatch, mode):
     d = (res[0]["final"] - ref).abs()
     assert d.max() <= STEPS * 3e-3 + 1e-6
     assert d.mean() < 2e-5
+
+
+def _worker_trainer(rank, world, port, out_dir, cfg, compile_):
+    """Trainer-level DDP rehearsal (flat reducer over gloo, one GPU): compile=True captures
+    the accumulation micro-steps as a HIP graph and runs the synchronising one eagerly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1", NSA_GEMM_BACKEND=_PINNED_GEMM)
+    from nanosandbox_amd.train import Trainer
+
+    torch.manual_seed(0)
+    c = dict(cfg, compile=compile_, out_dir=os.path.join(out_dir, f"c{int(compile_)}_r{rank}"))
+    tr = Trainer(c)
+    X, Y = tr.batches.get_batch("train")
+    losses = []
+    for _ in range(4):
+        for g in tr.optimizer.param_groups:
+            g["lr"] = 1e-3
+        loss, _, X, Y = tr.train_step(X, Y)
+        losses.append(loss.item() * tr.gas)
+    torch.cuda.synchronize()
+    torch.save({"losses": losses, "final": tr.store.master.detach().cpu().clone(), "use_graph": tr.use_graph,
+                "replays": tr.graph.replays if tr.graph is not None else 0, "gas": tr.gas},
+               os.path.join(out_dir, f"t{int(compile_)}_rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_gpu_compile_graph_with_reducer(tmp_path):
+    """compile=True at world_size 2: the gas - 1 accumulation micro-steps
+    replay a HIP graph captured with the bucket hooks disarmed, the last one runs eagerly
+    with the reducer armed; ranks stay bitwise identical and training tracks eager DDP."""
+    from nanosandbox_amd.config import TRAIN_DEFAULTS
+    from nanosandbox_amd.data.prepare import synthetic_corpus, write_char_dataset
+
+    write_char_dataset(str(tmp_path / "data" / "chars"), synthetic_corpus(200_000))
+    cfg = dict(TRAIN_DEFAULTS)
+    cfg.update(dataset="chars", data_dir=str(tmp_path / "data"), n_layer=2, n_head=4, n_embd=256, block_size=256,
+               batch_size=4, gradient_accumulation_steps=6, max_iters=10, eval_interval=1000, eval_iters=1,
+               log_interval=1000, device="cuda", backend="nccl", dropout=0.0, bias=False, seed=1234,
+               ddp_impl="flat", ddp_bucket_mb=1, tensorboard_dir="", always_save_checkpoint=False)
+    res = {}
+    for compile_ in (True, False):
+        port = _free_port()
+        mp.spawn(_worker_trainer, args=(2, port, str(tmp_path), cfg, compile_), nprocs=2, join=True)
+        res[compile_] = [torch.load(os.path.join(tmp_path, f"t{int(compile_)}_rank{r}.pt"), weights_only=True)
+                         for r in range(2)]
+    g, e = res[True], res[False]
+    assert g[0]["use_graph"] and not e[0]["use_graph"]
+    assert g[0]["gas"] == 3 and g[0]["replays"] == 4 * (g[0]["gas"] - 1)
+    for r in (g, e):
+        assert torch.equal(r[0]["final"], r[1]["final"]), "ranks diverged"
+    for a, b in zip(g[0]["losses"], e[0]["losses"]):
+        assert abs(a - b) < 2e-2 * abs(b), (g[0]["losses"], e[0]["losses"])
+    d = (g[0]["final"] - e[0]["final"]).abs()
+    assert d.max() < 4 * 3e-3 and d.mean() < 2e-5

@@ -32,9 +32,12 @@ def test_nt_forward_and_gelu_epilogue(kernels, M, N, K):
         assert torch.equal(gemm.nt(x, w, var=st), y)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 3072, 768), (264, 512, 256), (2048, 50304, 768)])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 3072, 768), (264, 512, 256), (2048, 50304, 768),
+                                   (8192, 768, 3072), (8200, 768, 3072)])
 def test_nt_input_grad_and_dgelu_epilogue(kernels, M, N, K):
-    """dX = dY·W through the K-contiguous W^T, plain and with the GELU' epilogue."""
+    """dX = dY·W through the K-contiguous W^T, plain and with the GELU' epilogue; the
+    8192-row shapes give every workgroup several output tiles (deferred epilogue stores,
+    and with 8200 rows a shifted tail tile among them)."""
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
     dy = torch.randn(M, N, device=DEV).to(BF)

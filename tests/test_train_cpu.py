@@ -114,3 +114,20 @@ def test_nanogpt_checkpoint_with_compile_prefix_loads(cfg, tmp_path):
     assert tr2.iter_num == 3 and tr2.best_val_loss == 2.5
     for (k, a), b in zip(tr2.raw_model.state_dict().items(), m.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+def test_graph_capture_policy(monkeypatch):
+    """compile=True at world_size > 1 captures the accumulation micro-steps with the flat
+    reducer (the synchronising one runs eagerly); torch DDP and gas = 1 stay eager."""
+    import torch
+
+    from nanosandbox_amd.runtime.hipgraph import graph_capture_supported
+
+    assert not graph_capture_supported("cpu", 0.0, 1)[0]
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    assert graph_capture_supported("cuda:0", 0.0, 1)[0]
+    assert graph_capture_supported("cuda:0", 0.2, 8, "flat", 4)[0]
+    ok, why = graph_capture_supported("cuda:0", 0.0, 8, "flat", 1)
+    assert not ok and "one micro-step" in why
+    ok, why = graph_capture_supported("cuda:0", 0.0, 2, "torch", 4)
+    assert not ok and "torch DDP" in why
