@@ -77,6 +77,39 @@ __device__ __forceinline__ void lds_wr16(uint32_t addr, const t4_u32x4& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 
+// The last MFMAs' results, then the wave's 128x128 bf16 quarter staged through its own
+// 32 KiB of LDS (the operand buffers are free after the barrier) and stored as whole
+// 256-B row segments (16 lanes per row, 4 rows per instruction).
+__device__ __forceinline__ void nt4_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], char* smem, int wave, int lane,
+                                             int wm, int wn, int m0, int n0, int mlo, int nlo) {
+  __syncthreads();
+  char* stage = smem + wave * 32768;
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 tv = acc[i][j];
+      const int row = 16 * i + r;                   // 0..127
+      const int col = 16 * j + 4 * q;               // 0..127, 4 consecutive
+      const int chunk = (col >> 3) ^ (row & 15);    // 16-byte chunk of the 256-B row, swizzled
+      *reinterpret_cast<uint2*>(stage + row * 256 + chunk * 16 + (col & 4) * 2) =
+          make_uint2(pack2(tv[0], tv[1]), pack2(tv[2], tv[3]));
+    }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const bool full = (m0 == mlo) & (n0 == nlo);
+#pragma unroll
+  for (int s = 0; s < 32; ++s) {
+    const int row = 4 * s + (lane >> 4);  // 0..127
+    const int c = lane & 15;              // 16-byte chunk
+    const uint4 val = *reinterpret_cast<const uint4*>(stage + row * 256 + ((c ^ (row & 15)) << 4));
+    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 128 + 8 * c;
+    if (!full && (grow < mlo || gcol < nlo)) continue;
+    *reinterpret_cast<uint4*>(g.C + (int64_t)grow * g.ldc + gcol) = val;
+  }
+}
+
 }  // namespace
 
 // One output tile per workgroup (grid = tiles, XCD-grouped order), tail tiles shifted
@@ -240,36 +273,107 @@ __global__ __launch_bounds__(T4_THREADS, 1) void gemm_nt4_kernel(Nt4Args g) {
 #undef NT4_STEP
 #undef NT4_READ_SET
 
-  // ---- epilogue: the last MFMAs' results, then the wave's 128x128 bf16 quarter staged
-  // through its own 32 KiB of LDS (the operand buffers are free after the barrier) and
-  // stored as whole 256-B row segments (16 lanes per row, 4 rows per instruction).
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // re-fetches past the end
-  __syncthreads();
-  char* stage = smem + wave * 32768;
-  const int r = lane & 15, q = lane >> 4;
+  nt4_epilogue(g, acc, smem, wave, lane, wm, wn, m0, n0, mlo, nlo);
+}
+
+// NT4_STAGED variant: the same wave geometry and MFMA stream, operands in FOUR 32-KiB
+// slots of one 32-deep k-step each (A [256][32] + B [256][32], 64-B rows).  Each k-step
+// opens with a counted wait + barrier (k-step s+1 landed, the slot of s-1 free); the DMA of
+// k-step s+3 (8 pieces per wave) is spread one per 8 MFMAs over k-step s, so the operand
+// stream has no bursts and two k-steps of lead.  64-B rows: physical chunk = chunk ^
+// g((row >> 2) & 3) with g = {0, 2, 3, 1}, conflict-free for ds_read_b128's lane groups.
+constexpr int T4S_SLOT = 2 * T4_BM * 32 * 2;  // 32 KiB
+__device__ __forceinline__ int t4s_g(int b) { return (0x1320 >> (4 * b)) & 3; }  // {0, 2, 3, 1}
+
+__global__ __launch_bounds__(T4_THREADS, 1) void gemm_nt4s_kernel(Nt4Args g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * T4S_SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ns = g.K / 32;  // k-steps, a multiple of 4 (host check)
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int tiles = g.tiles_m * g.tiles_n;
+  int v = blockIdx.x;
+  {
+    const int G = gridDim.x, x = v % 8, q = G / 8, r = G % 8;
+    v = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + v / 8;
+  }
+  if (v >= tiles) return;
+  const int tm = v / g.tiles_n, tn = v % g.tiles_n;
+  const int mlo = tm * T4_BM, nlo = tn * T4_BN;
+  const int m0 = min(mlo, g.M - T4_BM), n0 = min(nlo, g.N - T4_BN);
+
+  // DMA: a piece = 16 rows x 64 B; wave w copies pieces w + 4q (q = 0..3) of A and of B:
+  // rows 64q + 16w + lane/4, physical chunk lane % 4 <- logical chunk (lane % 4) ^ g(row>>2 & 3)
+  // with (row >> 2) & 3 = (lane >> 4) for these rows (64q + 16w is a multiple of 16)
+  const int prow = 16 * wave + (lane >> 2);
+  const int pch = (lane & 3) ^ t4s_g(lane >> 4);
+  const uint32_t voA = (uint32_t)(prow * g.lda * 2 + pch * 16);
+  const uint32_t voB = (uint32_t)(prow * g.ldb * 2 + pch * 16);
+  const char* a_tile = reinterpret_cast<const char*>(g.A + (int64_t)m0 * g.lda);
+  const char* b_tile = reinterpret_cast<const char*>(g.B + (int64_t)n0 * g.ldb);
+  const int64_t a_q = (int64_t)64 * g.lda * 2, b_q = (int64_t)64 * g.ldb * 2;
+  auto dma_piece = [&](int ks, int slot, int pc) {  // pc 0..7: A q = pc, B q = pc - 4
+    const int q = pc & 3;
+    const uint32_t dst = lds0 + (uint32_t)(slot * T4S_SLOT + (pc >= 4 ? T4S_SLOT / 2 : 0) + (wave + 4 * q) * 1024);
+    if (pc < 4) dma16(a_tile + q * a_q + (int64_t)ks * 64, voA, dst);
+    else dma16(b_tile + q * b_q + (int64_t)ks * 64, voB, dst);
+  };
+  // fragments: row wm*128 + 16 i + (lane & 15), logical chunk lane >> 4 of the 64-B row
+  const int rphys = ((lane >> 4) ^ t4s_g((lane >> 2) & 3)) << 4;
+  const uint32_t adA = lds0 + (uint32_t)((wm * 128 + (lane & 15)) * 64 + rphys);
+  const uint32_t adB = lds0 + (uint32_t)(T4S_SLOT / 2 + (wn * 128 + (lane & 15)) * 64 + rphys);
+
+  f32x4 acc[8][8];
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+  for (int st = 0; st < 3; ++st)
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc) dma_piece(min(st, ns - 1), st, pc);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // k-step 0
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lds_rd<0>(xb[j], adB + 1024 * j);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) lds_rd<0>(xa[i], adA + 1024 * i);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 tv = acc[i][j];
-      const int row = 16 * i + r;                   // 0..127
-      const int col = 16 * j + 4 * q;               // 0..127, 4 consecutive
-      const int chunk = (col >> 3) ^ (row & 15);    // 16-byte chunk of the 256-B row, swizzled
-      *reinterpret_cast<uint2*>(stage + row * 256 + chunk * 16 + (col & 4) * 2) =
-          make_uint2(pack2(tv[0], tv[1]), pack2(tv[2], tv[3]));
-    }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  const bool full = (m0 == mlo) & (n0 == nlo);
-#pragma unroll
-  for (int s = 0; s < 32; ++s) {
-    const int row = 4 * s + (lane >> 4);  // 0..127
-    const int c = lane & 15;              // 16-byte chunk
-    const uint4 val = *reinterpret_cast<const uint4*>(stage + row * 256 + ((c ^ (row & 15)) << 4));
-    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 128 + 8 * c;
-    if (!full && (grow < mlo || gcol < nlo)) continue;
-    *reinterpret_cast<uint4*>(g.C + (int64_t)grow * g.ldc + gcol) = val;
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // k-step S (slot S & 3) on (CA, CB): wait for k-step S+1 (8 younger pieces may fly),
+  // barrier, 64 MFMAs; reads of k-step S+1 (slot (S+1) & 3) one per 2 MFMAs in the first
+  // half; DMA of k-step S+3 into slot (S+3) & 3 (= the slot of S-1) one per 8 MFMAs.
+#define NT4S_STEP(SL, CA, CB, NA, NB, S)                                                       \
+  {                                                                                            \
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                          \
+    __builtin_amdgcn_s_barrier();                                                              \
+    const int dks_ = min((S) + 3, ns - 1);                                                     \
+    _Pragma("unroll") for (int m = 0; m < 64; ++m) {                                           \
+      const int i_ = m >> 3, j_ = m & 7;                                                       \
+      mfma_acc(acc[i_][j_], CB[j_], CA[i_]);                                                   \
+      if ((m & 1) == 0 && m < 32) {                                                            \
+        const int r_ = m >> 1;                                                                 \
+        constexpr uint32_t nso_ = (uint32_t)((((SL) + 1) & 3) * T4S_SLOT);                     \
+        if (r_ < 8) lds_rd<0>(NB[r_], adB + nso_ + 1024 * r_);                                \
+        else lds_rd<0>(NA[r_ - 8], adA + nso_ + 1024 * (r_ - 8));                             \
+      }                                                                                        \
+      if ((m & 7) == 3) dma_piece(dks_, ((SL) + 3) & 3, m >> 3);                              \
+    }                                                                                          \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                        \
   }
+  for (int s0 = 0; s0 < ns; s0 += 4) {
+    NT4S_STEP(0, xa, xb, ya, yb, s0)
+    NT4S_STEP(1, ya, yb, xa, xb, s0 + 1)
+    NT4S_STEP(2, xa, xb, ya, yb, s0 + 2)
+    NT4S_STEP(3, ya, yb, xa, xb, s0 + 3)
+  }
+#undef NT4S_STEP
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  nt4_epilogue(g, acc, smem, wave, lane, wm, wn, m0, n0, mlo, nlo);
 }
 
 NSA_API hipError_t nsa_gemm_nt4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
@@ -290,6 +394,12 @@ NSA_API hipError_t nsa_gemm_nt4(const void* A, int lda, const void* B, int ldb, 
   a.ldc = ldc;
   a.tiles_m = (M + T4_BM - 1) / T4_BM;
   a.tiles_n = (N + T4_BN - 1) / T4_BN;
-  gemm_nt4_kernel<<<dim3(a.tiles_m * a.tiles_n), T4_THREADS, 0, s>>>(a);
+#ifndef NT4_STAGED
+#define NT4_STAGED 1  // 0: two 64-KiB buffers, one barrier per K-tile (gemm_nt4_kernel)
+#endif
+  if (NT4_STAGED)
+    gemm_nt4s_kernel<<<dim3(a.tiles_m * a.tiles_n), T4_THREADS, 0, s>>>(a);
+  else
+    gemm_nt4_kernel<<<dim3(a.tiles_m * a.tiles_n), T4_THREADS, 0, s>>>(a);
   return hipGetLastError();
 }
