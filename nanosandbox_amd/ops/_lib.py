@@ -90,7 +90,6 @@ _SIGNATURES = {
     "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],
-    "nsa_gemm_nt4": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemm_nt": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                     c_int, c_int, c_int, c_int, c_void_p],
 }

@@ -93,22 +93,6 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0):
     return out
 
 
-def nt4_supported(M, N, K):
-    return M >= 256 and N >= 256 and K >= 128 and K % 128 == 0
-
-
-def nt4(a, b):
-    """C = a @ b^T on the 4-wave software-pipelined kernel (csrc/kernels/gemm_nt4.hip)."""
-    M, K = a.shape
-    N = b.shape[0]
-    _check(a, "a")
-    _check(b, "b")
-    out = torch.empty(M, N, device=a.device, dtype=BF16)
-    _lib.call("nsa_gemm_nt4", _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), _lib.ptr(out), out.stride(0), M, N, K,
-              _lib.stream())
-    return out
-
-
 def fwd(x2, w):
     """Y = X · W^T (nn.Linear forward, bf16)."""
     return nt(x2, w)

@@ -44,7 +44,6 @@ def main():
     ap.add_argument("--alt", default="", help="NAME=PATH,... stand-alone NT builds (scripts/build_nt_variants.sh)")
     ap.add_argument("--oldlib", default="", help="PATH of a build of the round-2 gemm.hip: times its 4-wave "
                     "kernel (variant 11) in the NT layout as 'w4'")
-    ap.add_argument("--alt4", default="", help="NAME=PATH,... stand-alone gemm_nt4 builds (build_nt4_variants.sh)")
     ap.add_argument("--gms", default="", help="extra tile-group sizes to time, e.g. 1,4,8")
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
     a = ap.parse_args()
@@ -56,23 +55,6 @@ def main():
         L.nsa_gemm_nt.argtypes = _lib._SIGNATURES["nsa_gemm_nt"]
         L.nsa_gemm_nt.restype = ctypes.c_int
         alts[nm] = L
-
-    alts4 = {}
-    for spec in [t for t in a.alt4.split(",") if t]:
-        nm, path = spec.split("=", 1)
-        L = ctypes.CDLL(os.path.abspath(path))
-        L.nsa_gemm_nt4.argtypes = _lib._SIGNATURES["nsa_gemm_nt4"]
-        L.nsa_gemm_nt4.restype = ctypes.c_int
-        alts4[nm] = L
-
-    def alt_nt4(L, x, w):
-        Mx, Kx = x.shape
-        Nx = w.shape[0]
-        out = torch.empty(Mx, Nx, device=x.device, dtype=torch.bfloat16)
-        err = L.nsa_gemm_nt4(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
-                             Mx, Nx, Kx, _lib.stream())
-        assert err == 0, err
-        return out
 
     old = None
     if a.oldlib:
@@ -132,15 +114,6 @@ def main():
         del ref
         cands = {"hipblaslt": lambda: x @ w.t(), "nt": lambda: gemm.nt(x, w),
                  "nt_nopost": lambda: gemm.nt(x, w, probe=2)}
-        if gemm.nt4_supported(M, N, K):
-            cands["nt4"] = lambda: gemm.nt4(x, w)
-            e4 = ((gemm.nt4(x, w)[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
-            t4 = ((gemm.nt4(x, w)[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
-            print(json.dumps({"check": f"{name}/nt4", "rel_err": e4, "tail_maxabs": t4}), flush=True)
-        for nm, L in alts4.items():
-            cands[f"nt4_{nm}"] = lambda L=L: alt_nt4(L, x, w)
-            e = ((alt_nt4(L, x, w)[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
-            print(json.dumps({"check": f"{name}/nt4_{nm}", "rel_err": e}), flush=True)
         if old is not None:
             cands["w4"] = lambda: old_nt(x, w)
             e = ((old_nt(x, w)[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
