@@ -55,6 +55,9 @@ static_assert(SMEM <= 163840, "LDS budget");
 #ifndef NSA_NT_DEF
 #define NSA_NT_DEF 4  // epilogue rounds (of 4) deferred into the next tile's first K-tile
 #endif
+#ifndef NSA_NT_VMW
+#define NSA_NT_VMW 8  // steady-state DMA wait: vmcnt(VMW) keeps VMW / 2 half-tiles in flight (A/B probe)
+#endif
 #ifndef NSA_NT_RPP
 #define NSA_NT_RPP 4  // deferred rounds stored per phase
 #endif
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
   if (c2.valid) {
     issue_half(c2, BAL ? 1 : 0);
     issue_half(c2, BAL ? 0 : 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    vm_wait_imm<NSA_NT_VMW>();
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -485,10 +488,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_nt_kernel(NtArgs g) {
       }                                                                                        \
       if (cc_.valid) {                                                                         \
         if ((KT == 1 || (KT == 2 && RPP * P < DEF)) && pend) {                                 \
-          vm_wait_imm<8 + (KT == 1 ? (4 - DEF) * SR + SR * (DEF < RPP * (P + 1) ? DEF : RPP * (P + 1)) \
+          vm_wait_imm<NSA_NT_VMW + (KT == 1 ? (4 - DEF) * SR + SR * (DEF < RPP * (P + 1) ? DEF : RPP * (P + 1)) \
                                    : SR * (DEF > RPP * P ? DEF - RPP * P : 0))>();              \
         } else {                                                                               \
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                    \
+          vm_wait_imm<NSA_NT_VMW>();                                                          \
         }                                                                                      \
       } else {                                                                                 \
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
