@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--real-data", default="",
                     help="dataset name or directory with train.bin/val.bin (nanoGPT bench.py real_data); "
                          "default: synthetic uniform tokens")
+    ap.add_argument("--rccl-sweep", default="4,16,64,256",
+                    help="all-reduce sizes (MiB) timed once before the timed steps when WORLD_SIZE > 1 "
+                         "(bus bandwidth by bucket size, printed to stderr); '' disables")
     ap.add_argument("--profile", action="store_true",
                     help="nanoGPT bench.py profile mode: torch.profiler over the timed steps "
                          "(schedule wait 1 / warmup 1 / active rest), TensorBoard trace under ./bench_log")
@@ -128,6 +131,9 @@ def main():
         from nanosandbox_amd.ops import gemm_tune
         for k, v in sorted(gemm_tune.table().items()):
             print(f"gemm backend {k}: {v}")
+        if world > 1 and args.rccl_sweep:
+            from nanosandbox_amd.parallel import allreduce_sweep
+            allreduce_sweep(tr.info, [int(v) for v in args.rccl_sweep.split(",") if v])
         torch.cuda.synchronize()
         if dist.is_initialized():
             dist.barrier()

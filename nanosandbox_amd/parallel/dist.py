@@ -182,6 +182,38 @@ def report_transport(info: "DistInfo", nbytes: int = 64 << 20, iters: int = 5, v
     return rep
 
 
+def allreduce_sweep(info: "DistInfo", sizes_mib=(4, 16, 64, 256), iters: int = 3, verbose: bool = True) -> list:
+    """All-reduce bus bandwidth by message size (the gradient bucket size trade-off of
+    docs/rccl.md: per-call latency vs per-link bandwidth over xGMI).  Rank 0 prints one
+    ``rccl sweep:`` JSON line; every rank returns the rows."""
+    import json
+    import time
+    if not info.ddp or not dist.is_initialized():
+        return []
+    be = dist.get_backend()
+    dev = torch.device(info.device) if be == "nccl" else torch.device("cpu")
+    n = info.world_size
+    rows = []
+    for mib in sizes_mib:
+        x = torch.ones((int(mib) << 20) // 4, dtype=torch.float32, device=dev)
+        dist.all_reduce(x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / iters
+        rows.append({"MiB": mib, "ms": round(dt * 1e3, 3),
+                     "busbw_GBps": round(2 * (n - 1) / n * x.numel() * 4 / dt / 1e9, 1)})
+        del x
+    if info.rank == 0 and verbose:
+        print("rccl sweep: " + json.dumps({"backend": be, "world": n, "rows": rows}), flush=True)
+    return rows
+
+
 def _attempt_store(rank: int, world: int):
     """The rendezvous store for an elastic restart, namespaced by the attempt.
 

@@ -166,3 +166,34 @@ def test_rccl_env_presets(monkeypatch):
     for k in dist.XGMI_ENV:
         assert os.environ[k] == dist.XGMI_ENV[k]
     assert dist.rccl_env_defaults("xgmi") == {}  # idempotent
+
+
+def _sweep_worker(rank, world, port, out_dir):
+    import json
+    import os
+
+    import torch.distributed as dist
+
+    from nanosandbox_amd.parallel import allreduce_sweep
+    from nanosandbox_amd.parallel.dist import init_distributed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    info = init_distributed("gloo", "cpu")
+    rows = allreduce_sweep(info, (1, 2), iters=1, verbose=False)
+    with open(os.path.join(out_dir, f"sweep{rank}.json"), "w") as f:
+        json.dump(rows, f)
+    dist.destroy_process_group()
+
+
+def test_allreduce_sweep_rows(tmp_path):
+    """bench.py's pre-timing bucket-size sweep (world > 1): one row per size, positive bus
+    bandwidth, on every rank."""
+    import json
+
+    port = _free_port()
+    mp.spawn(_sweep_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        rows = json.load(open(tmp_path / f"sweep{r}.json"))
+        assert [x["MiB"] for x in rows] == [1, 2]
+        assert all(x["busbw_GBps"] > 0 and x["ms"] > 0 for x in rows)
