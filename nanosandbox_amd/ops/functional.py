@@ -358,6 +358,8 @@ class LayerNormFn(torch.autograd.Function):
             ds, dh = grads
         else:
             ds, dh = None, grads[0]
+        if dh is None and ds is None:  # no output reached the loss (grads are not materialised)
+            return None, None, None, None, None, None
         x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
         b = b_or_mean if ctx.has_bias else None
         C = x2.shape[-1]
