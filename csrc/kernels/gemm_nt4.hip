@@ -1,0 +1,478 @@
+// Persistent four-wave bf16 "NT" GEMM for gfx950: C[M,N] = A[M,K] · B[N,K]^T (both operands
+// K-contiguous, fp32 accumulate), with the same epilogues as gemm_nt.hip (bf16 store,
+// u + gelu(u) for the c_fc forward, acc * gelu'(U) for the mlp.c_proj input grad).
+//
+// Why a second NT kernel: the 8-wave kernel (gemm_nt.hip, 128x64 per wave) reads
+// 24 fragments (24 KiB) per wave per 64-deep K-tile for 64 MFMAs; with 8 waves that is
+// 192 KiB of ds_read_b128 plus 64 KiB of LDS-DMA writes per CU per K-tile, against
+// 2048 MFMA cycles per SIMD — the LDS array runs near its 256 B/clk (PMC:
+// SQ_LDS_CMD_FIFO_FULL 60M at the lm_head dX shape, profiles/r3_gemm_pmc.md).  Here a wave
+// owns 128x128 (8x8 accumulators of v_mfma_f32_16x16x32_bf16 = 256 AGPRs) and reads 32
+// fragments per 128 MFMAs: 128 KiB of reads per CU per K-tile, a third less.
+//
+// Schedule of one 64-deep K-tile (two 32-deep k-steps, 128 MFMAs per wave, one wave per
+// SIMD; the numbers are MFMA slots n = 0..127, k-step 0 = n < 64):
+//   n  0-14  read the A fragments of k-step 1 (8, current buffer)
+//   n 20/21  lgkmcnt(0), barrier 1: every wave is done with the buffer's A image
+//   n 22-50  LDS-DMA of K-tile t+2's A image into this buffer (8 pieces, one per 4 MFMAs),
+//            B fragments of k-step 1 read between them (n 23-37)
+//   n 56/57  lgkmcnt(0), barrier 2: the buffer's B image is free too
+//   n 58-74  LDS-DMA of K-tile t+2's B image, pieces 0-4
+//   n 90/91  vmcnt(13) + barrier 3: K-tile t+1 (issued one K-tile ago) has landed
+//   n 92-122 read K-tile t+1's k-step-0 fragments (16, other buffer); B pieces 5-7
+//   n 127    lgkmcnt(0) (form (ii): the wait names every fragment it covers)
+// so DMA has one whole K-tile (~2048 MFMA cycles) to land, two 64-KiB buffers suffice, and
+// no MFMA ever waits on LDS.  LDS-DMA is buffer_load_dwordx4 ... lds with the tile row
+// base in the buffer resource (advanced 128 B per K-tile), the piece's row offset in an
+// SGPR soffset and one per-lane VGPR offset (XOR swizzle of the 16-B chunk in the source
+// address, cdna_hip_programming.md rule 21): no VALU work per DMA.
+//
+// B rows are staged in a permuted order (image row q holds output column pi(q)) so that a
+// lane's accumulators of fragments 2p and 2p+1 cover 8 CONSECUTIVE output columns: the
+// epilogue writes 16 B per lane straight from the accumulators, no LDS round trip.
+//
+// Persistent: grid = #CUs, tiles walked in the XCD-grouped order of gemm_nt.hip; the DMA
+// cursor runs straight on into the next tile, so the next tile's first two K-tiles load
+// while this tile's epilogue stores.  Tail tiles are shifted back inside the matrix and
+// store only their not-yet-covered rows / columns: M, N >= 256, N % 8 == 0, K % 64 == 0.
+#include <utility>
+
+#include "common.h"
+
+namespace {
+
+constexpr int Q_BM = 256, Q_BN = 256, Q_BK = 64;
+constexpr int Q_THR = 256;
+constexpr int Q_IMG = Q_BM * Q_BK * 2;  // 32 KiB: one operand's [256][64] bf16 K-tile image
+constexpr int Q_BUF = 2 * Q_IMG;        // A image, then B image
+constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
+
+#ifndef NSA_NT4_SCHED
+#define NSA_NT4_SCHED 0  // 0: three barriers per K-tile (header); 1: two barriers, evenly spread DMA
+#endif
+#ifndef NSA_NT4_DS
+#define NSA_NT4_DS 6  // SCHED 1: MFMAs between LDS-DMA pieces
+#endif
+#ifndef NSA_NT4_VMS
+#define NSA_NT4_VMS 98  // SCHED 1: slot of the wait for the previous K-tile's pieces
+#endif
+#ifndef NSA_NT4_RS
+#define NSA_NT4_RS 1  // SCHED 1: MFMAs between the next K-tile's fragment reads
+#endif
+
+enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2 };
+
+typedef int q_i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t q_u32x4 __attribute__((ext_vector_type(4)));
+
+struct Nt4Args {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  bf16_t* C2;
+  const bf16_t* U;
+  int M, N, K;
+  int lda, ldb, ldc;
+  int tiles_m, tiles_n, tiles;
+  int gm;
+};
+
+template <int I>
+using QI = std::integral_constant<int, I>;
+template <class F, int... Is>
+__device__ __forceinline__ void q_for(F&& f, std::integer_sequence<int, Is...>) {
+  (f(QI<Is>{}), ...);
+}
+
+__device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+// first k-step of an output tile: the accumulator starts from 0 (no zeroing pass)
+__device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+}
+template <int OFF>
+__device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
+}
+// wait for every outstanding LDS read; the fragments it covers are named so the compiler
+// cannot touch them before the data has landed (cdna_hip_programming.md "What hipcc does not do")
+__device__ __forceinline__ void q_wait8(bf16x8 (&f)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]));
+}
+__device__ __forceinline__ void q_wait16(bf16x8 (&f)[8], bf16x8 (&h)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
+                 "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]), "+v"(h[7]));
+}
+__device__ __forceinline__ void q_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void q_vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc.base + soff + voff land at lds + 16 l
+__device__ __forceinline__ void q_dma(uint32_t lds, uint32_t voff, q_i32x4 rsrc, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(voff),
+               "s"(rsrc), "s"(soff)
+               : "memory");
+}
+
+__device__ __forceinline__ void q_tile_coords(const Nt4Args& g, int seq, int& m0, int& n0, int& mlo, int& nlo) {
+  const int per = g.gm * g.tiles_n;
+  const int grp = seq / per;
+  const int first = grp * g.gm;
+  const int gm = min(g.gm, g.tiles_m - first);
+  const int in = seq - grp * per;
+  mlo = (first + in % gm) * Q_BM;
+  nlo = (in / gm) * Q_BN;
+  m0 = min(mlo, g.M - Q_BM);
+  n0 = min(nlo, g.N - Q_BN);
+}
+
+// raw buffer resource over [base, base + bytes): gfx9 word 3 = 0x00020000 (32-bit data format)
+__device__ __forceinline__ q_i32x4 q_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  q_i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32) & 0xffff);
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// DMA cursor: the K-tile whose pieces the current K-tile's slots issue (two ahead)
+struct QCur {
+  q_i32x4 ra, rb;
+  int seq, k;
+  bool valid;
+};
+
+__device__ __forceinline__ void q_cur_tile(const Nt4Args& g, QCur& c, int seq) {
+  c.seq = seq;
+  c.k = 0;
+  c.valid = seq < g.tiles;
+  if (c.valid) {
+    int m0, n0, mlo, nlo;
+    q_tile_coords(g, seq, m0, n0, mlo, nlo);
+    c.ra = q_rsrc(g.A + (int64_t)m0 * g.lda, (uint32_t)(Q_BM * g.lda * 2));
+    c.rb = q_rsrc(g.B + (int64_t)n0 * g.ldb, (uint32_t)(Q_BN * g.ldb * 2));
+  } else {
+    // past the last tile the slots still issue their pieces (no branches in the K-tile
+    // body, vmcnt counts stay fixed): an empty range makes every load out of bounds, so
+    // nothing is fetched and the never-read buffer receives zeros
+    c.ra = q_rsrc(g.A, 0);
+    c.rb = q_rsrc(g.B, 0);
+  }
+}
+__device__ __forceinline__ void q_add_base(q_i32x4& r, int bytes) {
+  uint64_t b = ((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x;
+  b += (uint64_t)bytes;
+  r.x = (int)(uint32_t)b;
+  r.y = (int)(uint32_t)(b >> 32);
+  r.z -= bytes;
+}
+__device__ __forceinline__ void q_cur_next(const Nt4Args& g, QCur& c, int nk, int G) {
+  if (!c.valid) return;
+  if (++c.k == nk) {
+    q_cur_tile(g, c, c.seq + G);
+  } else {
+    q_add_base(c.ra, 2 * Q_BK);
+    q_add_base(c.rb, 2 * Q_BK);
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(q_u32x4{a, b, c, d}, reinterpret_cast<q_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+  }
+}
+
+// Epilogue straight from the accumulators: lane l holds row 16 i + (l & 15) of the wave's
+// 128 rows and, over fragments 2p / 2p+1, the 8 consecutive columns 32 p + 8 (l >> 4) + 0..7.
+template <int EPI, bool NT>
+__device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
+                                           int lane) {
+  int m0, n0, mlo, nlo;
+  q_tile_coords(g, seq, m0, n0, mlo, nlo);
+  const bool full = (m0 == mlo) & (n0 == nlo);
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wm * 128 + 16 * i + r;
+    q_u32x4 uv[4];
+    if constexpr (EPI == Q_EPI_DGELU) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int col = n0 + wn * 128 + 32 * p + 8 * q;
+        uv[p] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)row * g.ldc + col));
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int col = n0 + wn * 128 + 32 * p + 8 * q;
+      if (!full && (row < mlo || col < nlo)) continue;
+      const f32x4 x = acc[i][2 * p], y = acc[i][2 * p + 1];
+      uint32_t w[4] = {pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]), pack2(y[2], y[3])};
+      if constexpr (EPI == Q_EPI_DGELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t u = uv[p][e];
+          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
+          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
+          w[e] = pack2(a0, a1);
+        }
+      }
+      const int64_t off = (int64_t)row * g.ldc + col;
+      q_st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
+      if constexpr (EPI == Q_EPI_GELU) {
+        uint32_t gg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
+        q_st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// PROBE (timing only, wrong results): 1 = no DMA after the prologue, 4 = no epilogue stores
+template <int EPI, bool NT, int PROBE>
+__global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
+  __shared__ __attribute__((aligned(16))) char smem[Q_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int G = gridDim.x;
+  const int nk = g.K / Q_BK;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // XCD-aware virtual block id: blocks b, b+8, ... share an XCD and get consecutive ids
+  int v = blockIdx.x;
+  {
+    const int x = v % 8, qq = G / 8, rr = G % 8;
+    v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + v / 8;
+  }
+  if (v >= g.tiles) return;
+
+  // ---- DMA geometry.  Wave w copies pieces P = 8 w + p (p = 0..7) of each image: image rows
+  // 8 P + i, i = lane >> 3, physical 16-B chunk lane & 7, which holds logical chunk
+  // (lane & 7) ^ s(row), s(r) = (r >> 1) & 7 = (4 (p & 1) + (i >> 1)) & 7.
+  // A: image row = tile row.  B: image row q holds tile column pi(q) (see the header):
+  // for a piece, pi = 64 w + 32 (p >> 2) + 16 (p & 1) + 4 ((p >> 1) & 1) + 8 (i >> 2) + (i & 3).
+  const int li = lane >> 3, lc = lane & 7;
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t ch = (uint32_t)((lc ^ ((4 * h + (li >> 1)) & 7)) << 4);
+    voA[h] = (uint32_t)(li * g.lda * 2) + ch;
+    voB[h] = (uint32_t)((8 * (li >> 2) + (li & 3)) * g.ldb * 2) + ch;
+  }
+  uint32_t soA[8], soB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    soA[p] = (uint32_t)__builtin_amdgcn_readfirstlane((64 * wave + 8 * p) * g.lda * 2);
+    soB[p] = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (64 * wave + 32 * (p >> 2) + 16 * (p & 1) + 4 * ((p >> 1) & 1)) * g.ldb * 2);
+  }
+  const uint32_t dmaA0 = lds0 + (uint32_t)(wave * 8 * 1024);          // + buffer + p * 1 KiB
+  const uint32_t dmaB0 = lds0 + (uint32_t)(Q_IMG + wave * 8 * 1024);
+
+  // ---- fragment read bases (buffer 0): A rows wm*128 + 16 i + (lane & 15), B image rows
+  // wn*128 + 16 j + (lane & 15), logical chunk 4 kk + (lane >> 4)
+  const int sw = ((lane & 15) >> 1) & 7;
+  uint32_t rA[2], rB[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const uint32_t ch = (uint32_t)(((4 * kk + (lane >> 4)) ^ sw) << 4);
+    rA[kk] = lds0 + (uint32_t)((wm * 128 + (lane & 15)) * 128) + ch;
+    rB[kk] = lds0 + (uint32_t)(Q_IMG + (wn * 128 + (lane & 15)) * 128) + ch;
+  }
+
+  auto issue_a = [&](const QCur& c, uint32_t buf, int p) {
+    q_dma(dmaA0 + buf + (uint32_t)(p * 1024), voA[p & 1], c.ra, soA[p]);
+  };
+  auto issue_b = [&](const QCur& c, uint32_t buf, int p) {
+    q_dma(dmaB0 + buf + (uint32_t)(p * 1024), voB[p & 1], c.rb, soB[p]);
+  };
+
+  // ---- prologue: K-tiles 0 and 1 of this workgroup's sequence into buffers 0 / 1
+  QCur c;
+  q_cur_tile(g, c, v);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) issue_a(c, 0, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) issue_b(c, 0, p);
+  q_cur_next(g, c, nk, G);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) issue_a(c, Q_BUF, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) issue_b(c, Q_BUF, p);
+  q_vmwait<16>();
+  q_cur_next(g, c, nk, G);  // c = the K-tile the first loop iteration's slots issue (two ahead)
+  q_barrier();
+
+  f32x4 acc[8][8];
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  q_for([&](auto I) {
+    constexpr int n = decltype(I)::value;
+    q_rd<n * 2048>(a0[n], rA[0]);
+    q_rd<n * 2048>(b0[n], rB[0]);
+  }, std::make_integer_sequence<int, 8>{});
+  q_wait16(a0, b0);
+
+  uint32_t buf = 0;  // LDS buffer of the K-tile being multiplied (byte offset 0 / Q_BUF)
+  int seq = v;
+  // one 64-deep K-tile; FIRST: the tile's first, whose k-step 0 starts the accumulators at 0
+  auto ktile = [&](auto FIRST_) {
+    constexpr bool FIRST = decltype(FIRST_)::value;
+    constexpr bool dv = PROBE != 1;
+    const uint32_t nb = buf ^ (uint32_t)Q_BUF;
+    q_for([&](auto I) {
+      constexpr int n = decltype(I)::value;
+      constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
+      if constexpr (kk == 0) {
+        if constexpr (FIRST) q_mfma0(acc[i][j], b0[j], a0[i]);
+        else q_mfma(acc[i][j], b0[j], a0[i]);
+      } else {
+        q_mfma(acc[i][j], b1[j], a1[i]);
+      }
+#if NSA_NT4_SCHED == 0
+      // k-step 1 A fragments (this buffer)
+      if constexpr (n < 16 && (n & 1) == 0) q_rd<(n >> 1) * 2048>(a1[n >> 1], rA[1] + buf);
+      if constexpr (n == 20) q_wait8(a1);
+      if constexpr (n == 21) q_barrier();
+      // K-tile t+2's A image into this buffer, k-step 1 B fragments between the pieces
+      if constexpr (n >= 22 && n <= 50 && ((n - 22) & 3) == 0) {
+        if constexpr (dv) issue_a(c, buf, (n - 22) >> 2);
+      }
+      if constexpr (n >= 23 && n <= 37 && ((n - 23) & 1) == 0) q_rd<(n - 23) / 2 * 2048>(b1[(n - 23) / 2], rB[1] + buf);
+      if constexpr (n == 56) q_wait8(b1);
+      if constexpr (n == 57) q_barrier();
+      if constexpr (n >= 58 && n <= 74 && ((n - 58) & 3) == 0) {
+        if constexpr (dv) issue_b(c, buf, (n - 58) >> 2);
+      }
+      // K-tile t+1 has landed (its 16 pieces are older than this K-tile's 13)
+      if constexpr (n == 90) {
+        q_vmwait<dv ? 13 : 0>();
+      }
+      if constexpr (n == 91) q_barrier();
+      // its k-step 0 fragments (other buffer): B 0..7, then A 0..7
+      if constexpr (n >= 92 && n <= 122 && (n & 1) == 0) {
+        constexpr int s = (n - 92) >> 1;
+        if constexpr (s < 8) q_rd<s * 2048>(b0[s], rB[0] + nb);
+        else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
+      }
+      if constexpr (n == 97 || n == 105 || n == 113) {
+        if constexpr (dv) issue_b(c, buf, 5 + (n - 97) / 8);
+      }
+#else
+      // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
+      // K-tile t+2 spread one per DS MFMAs, then K-tile t+1's k-step-0 fragments
+      if constexpr (n <= 30 && (n & 1) == 0) {
+        constexpr int s = n >> 1;
+        if constexpr (s < 8) q_rd<s * 2048>(a1[s], rA[1] + buf);
+        else q_rd<(s - 8) * 2048>(b1[s - 8], rB[1] + buf);
+      }
+      if constexpr (n == 32) q_wait16(a1, b1);
+      if constexpr (n == 33) q_barrier();
+      constexpr int D0 = 34, DS = NSA_NT4_DS, VMS = NSA_NT4_VMS;
+      if constexpr (n >= D0 && (n - D0) % DS == 0 && (n - D0) / DS < 16) {
+        constexpr int pc = (n - D0) / DS;
+        if constexpr (dv) {
+          if constexpr (pc < 8) issue_a(c, buf, pc);
+          else issue_b(c, buf, pc - 8);
+        }
+      }
+      constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
+      if constexpr (n == VMS) q_vmwait<dv ? issued : 0>();
+      if constexpr (n == VMS + 1) q_barrier();
+      if constexpr (n >= VMS + 2 && n < VMS + 2 + 16 * NSA_NT4_RS && (n - VMS - 2) % NSA_NT4_RS == 0) {
+        constexpr int s = (n - VMS - 2) / NSA_NT4_RS;
+        if constexpr (s < 8) q_rd<s * 2048>(b0[s], rB[0] + nb);
+        else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
+      }
+#endif
+      if constexpr (n == 127) q_wait16(a0, b0);
+    }, std::make_integer_sequence<int, 128>{});
+    buf = nb;
+    q_cur_next(g, c, nk, G);
+  };
+  while (true) {
+    ktile(std::true_type{});
+    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{});
+    // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (PROBE != 4) {
+      q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" ::"a"(acc[i][j]));
+    }
+    seq += G;
+    if (seq >= g.tiles) break;
+  }
+  q_vmwait<0>();
+}
+
+// Same contract as nsa_gemm_nt (epi: 0 bf16, 1 u + gelu(u) into C / C2, 2 acc * gelu'(U);
+// bits 8-11 timing probe (1 no DMA, 4 no stores); bits 12-13 store policy: 0 nontemporal above the Infinity Cache, 1 always, 2 never;
+// bits 16-23 row-blocks per tile group, 0 = automatic).  grid = persistent workgroups.
+NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                                const void* U, int M, int N, int K, int grid, hipStream_t s) {
+  const int epi_full = epi;
+  const int stp = (epi >> 12) & 0x3;
+  const int probe = (epi >> 8) & 0xf;
+  epi &= 0xff;
+  if (M < Q_BM || N < Q_BN || K < Q_BK || K % Q_BK != 0 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K ||
+      ldb < K || ldc < N || grid < 1)
+    return hipErrorInvalidValue;
+  if ((int64_t)Q_BM * lda * 2 >= (1ll << 31) || (int64_t)Q_BN * ldb * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+  if ((epi == Q_EPI_GELU && !C2) || (epi == Q_EPI_DGELU && !U)) return hipErrorInvalidValue;
+  Nt4Args a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.C2 = (bf16_t*)C2;
+  a.U = (const bf16_t*)U;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.tiles_m = (M + Q_BM - 1) / Q_BM;
+  a.tiles_n = (N + Q_BN - 1) / Q_BN;
+  a.tiles = a.tiles_m * a.tiles_n;
+  const int gmsel = (epi_full >> 16) & 0xff;
+  a.gm = gmsel ? gmsel : (a.tiles_n <= 16 ? 1 : 8);
+  const int64_t out_bytes = (int64_t)M * N * 2 * (epi == Q_EPI_GELU ? 2 : 1);
+  const bool nt = stp == 1 || (stp == 0 && out_bytes >= NSA_NT_MIN_BYTES);
+  const dim3 gr(grid < a.tiles ? grid : a.tiles);
+#define NT4_LAUNCH(E)                                                        \
+  if (probe == 1) gemm_nt4_kernel<E, true, 1><<<gr, Q_THR, 0, s>>>(a);       \
+  else if (probe == 4) gemm_nt4_kernel<E, true, 4><<<gr, Q_THR, 0, s>>>(a);  \
+  else if (nt) gemm_nt4_kernel<E, true, 0><<<gr, Q_THR, 0, s>>>(a);          \
+  else gemm_nt4_kernel<E, false, 0><<<gr, Q_THR, 0, s>>>(a);
+  switch (epi) {
+    case Q_EPI_BF16: NT4_LAUNCH(Q_EPI_BF16) break;
+    case Q_EPI_GELU: NT4_LAUNCH(Q_EPI_GELU) break;
+    case Q_EPI_DGELU: NT4_LAUNCH(Q_EPI_DGELU) break;
+    default: return hipErrorInvalidValue;
+  }
+#undef NT4_LAUNCH
+  return hipGetLastError();
+}

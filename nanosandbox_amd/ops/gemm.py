@@ -66,14 +66,15 @@ def nt_supported(M, N, K) -> bool:
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 
-def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None, gm=0):
+def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None, gm=0, w4=False):
     var = NT_VAR if var is None else var
-    _lib.call("nsa_gemm_nt", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
+    _lib.call("nsa_gemm_nt4" if w4 else "nsa_gemm_nt", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
               C.stride(0), _lib.ptr(C2), _lib.ptr(U), M, N, K, grid or num_cus(A.device), _lib.stream())
 
 
-def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0):
-    """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the persistent kernel.
+def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0, w4=False):
+    """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the persistent kernel
+    (``w4``: the four-wave kernel of gemm_nt4.hip, else the eight-wave gemm_nt.hip).
 
     epi NT_EPI_GELU returns (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u)."""
     M, K = a.shape
@@ -83,13 +84,13 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0):
     out = torch.empty(M, N, device=a.device, dtype=BF16)
     if epi == NT_EPI_GELU:
         act = torch.empty_like(out)
-        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var, gm=gm)
+        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
         return out, act
     if epi == NT_EPI_DGELU:
         _check(u, "u")
-        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var, gm=gm)
+        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
         return out
-    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var, gm=gm)
+    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
     return out
 
 

@@ -52,9 +52,10 @@ def main():
     for spec in [t for t in a.alt.split(",") if t]:
         nm, path = spec.split("=", 1)
         L = ctypes.CDLL(os.path.abspath(path))
-        L.nsa_gemm_nt.argtypes = _lib._SIGNATURES["nsa_gemm_nt"]
-        L.nsa_gemm_nt.restype = ctypes.c_int
-        alts[nm] = L
+        fn = getattr(L, "nsa_gemm_nt4", None) or L.nsa_gemm_nt
+        fn.argtypes = _lib._SIGNATURES["nsa_gemm_nt"]
+        fn.restype = ctypes.c_int
+        alts[nm] = fn
 
     old = None
     if a.oldlib:
@@ -78,7 +79,7 @@ def main():
         Nx = w.shape[0]
         out = torch.empty(Mx, Nx, device=x.device, dtype=torch.bfloat16)
         act = torch.empty_like(out) if epi == gemm.NT_EPI_GELU else None
-        err = L.nsa_gemm_nt(epi, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+        err = L(epi, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                             None if act is None else act.data_ptr(), None if u is None else u.data_ptr(), Mx, Nx, Kx,
                             gemm.num_cus(), _lib.stream())
         assert err == 0, err
@@ -97,7 +98,10 @@ def main():
         w = uni(n_, k_)
         ref = x.float() @ w.float().t()
         got = gemm.nt(x, w).float()
-        print(json.dumps({"check_odd": [m_, n_, k_], "rel_err": ((got - ref).norm() / ref.norm()).item()}), flush=True)
+        got4 = gemm.nt(x, w, w4=True).float()
+        print(json.dumps({"check_odd": [m_, n_, k_], "rel_err": ((got - ref).norm() / ref.norm()).item(),
+                          "rel_err_w4": ((got4 - ref).norm() / ref.norm()).item(),
+                          "maxabs_w4": (got4 - ref).abs().max().item()}), flush=True)
     for name in a.shapes.split(","):
         N, K = shapes[name]
         fl = 2.0 * M * N * K
@@ -112,8 +116,12 @@ def main():
         tail = ((got[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
         print(json.dumps({"check": name, "rel_err": err, "tail_maxabs": tail}), flush=True)
         del ref
-        cands = {"hipblaslt": lambda: x @ w.t(), "nt": lambda: gemm.nt(x, w),
-                 "nt_nopost": lambda: gemm.nt(x, w, probe=2)}
+        got4 = gemm.nt(x, w, w4=True)
+        err4 = ((got4[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
+        tail4 = ((got4[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
+        print(json.dumps({"check": name + "/w4", "rel_err": err4, "tail_maxabs": tail4}), flush=True)
+        del got4
+        cands = {"hipblaslt": lambda: x @ w.t(), "nt": lambda: gemm.nt(x, w), "nt4": lambda: gemm.nt(x, w, w4=True)}
         if old is not None:
             cands["w4"] = lambda: old_nt(x, w)
             e = ((old_nt(x, w)[rows].float() - x[rows].float() @ w.float().t()).norm() / ref_n).item()
@@ -133,6 +141,7 @@ def main():
         if a.probe:
             for pr, nm in ((1, "nodma"), (4, "nostore")):
                 cands[f"nt_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr)
+                cands[f"nt4_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr, w4=True)
         if a.epi and name in ("c_fc", "mlp.c_proj.dx"):
             if name == "c_fc":
                 u, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
@@ -148,6 +157,10 @@ def main():
                     _lib.call("nsa_gelu_fwd", _lib.ptr(uu), _lib.ptr(gg), uu.numel(), _lib.stream())
                 cands["hipblaslt+gelu"] = split
                 cands["nt_gelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+                cands["nt4_gelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU, w4=True)
+                u4, g4 = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, w4=True)
+                print(json.dumps({"check": name + "/gelu_w4", "maxabs_u": (u4.float() - u.float()).abs().max().item(),
+                                  "maxabs_g": (g4.float() - g.float()).abs().max().item()}), flush=True)
                 cands["nt_gelu_nopost"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU, probe=2)
                 for nm, L in alts.items():
                     cands[f"nt_gelu_{nm}"] = lambda L=L: alt_nt(L, x, w, epi=gemm.NT_EPI_GELU)
@@ -169,6 +182,9 @@ def main():
                     _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
                 cands["hipblaslt+dgelu"] = split2
                 cands["nt_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u)
+                cands["nt4_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, w4=True)
+                e4 = ((gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, w4=True).float() - got.float()).abs().max()).item()
+                print(json.dumps({"check": name + "/dgelu_w4_vs_nt_maxabs", "v": e4}), flush=True)
                 cands["nt_dgelu_nopost"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, probe=2)
                 for nm, L in alts.items():
                     cands[f"nt_dgelu_{nm}"] = lambda L=L: alt_nt(L, x, w, epi=gemm.NT_EPI_DGELU, u=u)
