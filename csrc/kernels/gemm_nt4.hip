@@ -45,22 +45,42 @@ constexpr int Q_BM = 256, Q_BN = 256, Q_BK = 64;
 constexpr int Q_THR = 256;
 constexpr int Q_IMG = Q_BM * Q_BK * 2;  // 32 KiB: one operand's [256][64] bf16 K-tile image
 constexpr int Q_BUF = 2 * Q_IMG;        // A image, then B image
-constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
+constexpr int Q_STG = 8192;            // epilogue staging per wave (32 rows x 128 columns bf16)
+constexpr int Q_SMEM = 2 * Q_BUF + 4 * Q_STG;  // 128 KiB of K-tile buffers + 32 KiB staging = 160 KiB
+static_assert(Q_SMEM <= 163840, "LDS budget");
+#ifndef NSA_NT4_STAG
+#define NSA_NT4_STAG 1  // start-time stagger phases: workgroup v starts (v % STAG) / STAG of a tile late
+#endif
+#ifndef NSA_NT4_EPI_LDS
+#define NSA_NT4_EPI_LDS 0  // 1: whole-row stores re-shaped through LDS; 0: 64-B row pieces from the registers
+#endif
 
 #ifndef NSA_NT4_SCHED
-#define NSA_NT4_SCHED 0  // 0: three barriers per K-tile (header); 1: two barriers, evenly spread DMA
+#define NSA_NT4_SCHED 1  // 0: three barriers per K-tile (header); 1: two barriers, evenly spread DMA
 #endif
 #ifndef NSA_NT4_DS
 #define NSA_NT4_DS 6  // SCHED 1: MFMAs between LDS-DMA pieces
 #endif
 #ifndef NSA_NT4_VMS
-#define NSA_NT4_VMS 98  // SCHED 1: slot of the wait for the previous K-tile's pieces
+#define NSA_NT4_VMS 92  // SCHED 1: slot of the wait for the previous K-tile's pieces
 #endif
 #ifndef NSA_NT4_RS
-#define NSA_NT4_RS 1  // SCHED 1: MFMAs between the next K-tile's fragment reads
+#define NSA_NT4_RS 2  // SCHED 1: MFMAs between the next K-tile's fragment reads
 #endif
 
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2 };
+
+// pieces a K-tile has issued when it waits for the previous K-tile's
+#if NSA_NT4_SCHED == 0
+constexpr int Q_ISS = 13;
+#else
+constexpr int Q_ISS = (NSA_NT4_VMS - 34) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - 34) / NSA_NT4_DS + 1 : 16;
+#endif
+// vector-memory operations of one wave's epilogue of a full tile (stores, and the U loads)
+template <int EPI>
+constexpr int q_epi_vm() {
+  return EPI == Q_EPI_BF16 ? 32 : 64;
+}
 
 typedef int q_i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t q_u32x4 __attribute__((ext_vector_type(4)));
@@ -187,6 +207,17 @@ __device__ __forceinline__ void q_cur_next(const Nt4Args& g, QCur& c, int nk, in
   }
 }
 
+// The wait for the previous K-tile's pieces.  vmcnt counts in issue order, so in the first
+// K-tile after a full tile's epilogue that epilogue's stores (and U loads) are younger than
+// the awaited pieces and may stay outstanding: the count grows by q_epi_vm (capped: when it
+// would exceed the 6-bit field the epilogue has already drained down to the cap).
+template <int ISS, int EPI>
+__device__ __forceinline__ void q_vmw(bool after_epi) {
+  constexpr int W = ISS == 0 ? 0 : (ISS + q_epi_vm<EPI>() < 63 ? ISS + q_epi_vm<EPI>() : 63);
+  if (after_epi) q_vmwait<W>();
+  else q_vmwait<ISS>();
+}
+
 template <bool NT>
 __device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   if constexpr (NT) {
@@ -232,6 +263,73 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
         }
       }
       const int64_t off = (int64_t)row * g.ldc + col;
+      q_st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
+      if constexpr (EPI == Q_EPI_GELU) {
+        uint32_t gg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
+        q_st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
+      }
+    }
+  }
+}
+
+
+// Epilogue through a wave-private 8-KiB LDS slice, in 4 rounds of 32 rows x 128 columns:
+// the accumulators go in as 16-B pieces (lane l: row 16 i2 + (l & 15), chunk 4 p + (l >> 4)),
+// come back as whole-row chunks (lane l: row 4 k + (l & 3), chunk l >> 2), so each store
+// instruction writes 4 rows x 256 contiguous bytes.  Physical chunk = chunk ^ swz(row),
+// swz = 4 (row & 3) + ((row >> 2) & 3): the 8 rows of a ds_write_b128 lane group and the
+// 4 rows x 4 chunks of a ds_read_b128 lane group all land in distinct 16-B bank groups.
+__device__ __forceinline__ int q_swz(int row) { return 4 * (row & 3) + ((row >> 2) & 3); }
+
+template <int EPI, bool NT>
+__device__ __forceinline__ void q_epilogue_lds(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
+                                               int lane, char* stage) {
+  int m0, n0, mlo, nlo;
+  q_tile_coords(g, seq, m0, n0, mlo, nlo);
+  const bool full = (m0 == mlo) & (n0 == nlo);
+  const int r = lane & 15, q = lane >> 4;
+  const int rr = lane & 3, cc = lane >> 2;
+  const int col = n0 + wn * 128 + 8 * cc;
+#pragma unroll
+  for (int rd = 0; rd < 4; ++rd) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int row = 16 * i2 + r;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const f32x4 x = acc[2 * rd + i2][2 * p], y = acc[2 * rd + i2][2 * p + 1];
+        *reinterpret_cast<uint4*>(stage + row * 256 + (((4 * p + q) ^ q_swz(row)) << 4)) =
+            make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]), pack2(y[2], y[3]));
+      }
+    }
+    q_u32x4 uv[8];
+    if constexpr (EPI == Q_EPI_DGELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int grow = m0 + wm * 128 + 32 * rd + 4 * k + rr;
+        uv[k] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)grow * g.ldc + col));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = 4 * k + rr;
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * 256 + ((cc ^ q_swz(row)) << 4));
+      const int grow = m0 + wm * 128 + 32 * rd + row;
+      if (!full && (grow < mlo || col < nlo)) continue;
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (EPI == Q_EPI_DGELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t u = uv[k][e];
+          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
+          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
+          w[e] = pack2(a0, a1);
+        }
+      }
+      const int64_t off = (int64_t)grow * g.ldc + col;
       q_st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
       if constexpr (EPI == Q_EPI_GELU) {
         uint32_t gg[4];
@@ -307,6 +405,12 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     q_dma(dmaB0 + buf + (uint32_t)(p * 1024), voB[p & 1], c.rb, soB[p]);
   };
 
+  if constexpr (NSA_NT4_STAG > 1) {
+    // de-synchronise the epilogues: with every CU storing its 128-KiB tile at the same moment
+    // the stores queue on HBM; started (v % STAG) / STAG of a tile apart they do not
+    const int units = (v % NSA_NT4_STAG) * nk * 32 / NSA_NT4_STAG;  // ~2048 cycles per K-tile, 64 per unit
+    for (int u = 0; u < units; u += 16) __builtin_amdgcn_s_sleep(16);
+  }
   // ---- prologue: K-tiles 0 and 1 of this workgroup's sequence into buffers 0 / 1
   QCur c;
   q_cur_tile(g, c, v);
@@ -334,6 +438,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
 
   uint32_t buf = 0;  // LDS buffer of the K-tile being multiplied (byte offset 0 / Q_BUF)
   int seq = v;
+  bool pend = false;  // the previous tile's epilogue left its vector-memory ops in flight
   // one 64-deep K-tile; FIRST: the tile's first, whose k-step 0 starts the accumulators at 0
   auto ktile = [&](auto FIRST_) {
     constexpr bool FIRST = decltype(FIRST_)::value;
@@ -365,7 +470,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       }
       // K-tile t+1 has landed (its 16 pieces are older than this K-tile's 13)
       if constexpr (n == 90) {
-        q_vmwait<dv ? 13 : 0>();
+        q_vmw<dv ? 13 : 0, EPI>(FIRST && pend);
       }
       if constexpr (n == 91) q_barrier();
       // its k-step 0 fragments (other buffer): B 0..7, then A 0..7
@@ -388,6 +493,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       if constexpr (n == 32) q_wait16(a1, b1);
       if constexpr (n == 33) q_barrier();
       constexpr int D0 = 34, DS = NSA_NT4_DS, VMS = NSA_NT4_VMS;
+      static_assert(D0 + 15 * DS <= 127 && VMS + 2 + 15 * NSA_NT4_RS <= 127, "every piece and read fits the K-tile");
       if constexpr (n >= D0 && (n - D0) % DS == 0 && (n - D0) / DS < 16) {
         constexpr int pc = (n - D0) / DS;
         if constexpr (dv) {
@@ -396,7 +502,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         }
       }
       constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
-      if constexpr (n == VMS) q_vmwait<dv ? issued : 0>();
+      if constexpr (n == VMS) q_vmw<dv ? issued : 0, EPI>(FIRST && pend);
       if constexpr (n == VMS + 1) q_barrier();
       if constexpr (n >= VMS + 2 && n < VMS + 2 + 16 * NSA_NT4_RS && (n - VMS - 2) % NSA_NT4_RS == 0) {
         constexpr int s = (n - VMS - 2) / NSA_NT4_RS;
@@ -415,7 +521,20 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
+      if constexpr (NSA_NT4_EPI_LDS)
+        q_epilogue_lds<EPI, NT>(g, acc, seq, wm, wn, lane, smem + 2 * Q_BUF + wave * Q_STG);
+      else
+        q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
+      int m0, n0, mlo, nlo;
+      q_tile_coords(g, seq, m0, n0, mlo, nlo);
+      if ((m0 == mlo) & (n0 == nlo)) {
+        // every store was issued: the next tile's first wait counts them
+        if constexpr (q_epi_vm<EPI>() + Q_ISS > 63) q_vmwait<63 - Q_ISS>();
+        pend = true;
+      } else {
+        q_vmwait<0>();  // a tail tile skips masked stores: drain instead of counting
+        pend = false;
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)

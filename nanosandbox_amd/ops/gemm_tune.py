@@ -17,7 +17,8 @@ so a fusion is used exactly where it measures faster.
 Candidate names: ``hipblaslt`` / ``hipblaslt_t`` (the library, input grads also on the
 cached weight transpose), ``nt`` (our persistent NT kernel, ``csrc/kernels/gemm_nt.hip``:
 forward and — through the cached K-contiguous weight transpose — input grads),
-``ntgelu`` / ``ntdgelu`` (the same kernel with the GELU / GELU' epilogue), ``nsa<v>``
+``ntgelu`` / ``ntdgelu`` (the same kernel with the GELU / GELU' epilogue), ``nt4`` /
+``nt4gelu`` / ``nt4dgelu`` (the four-wave persistent kernel, ``csrc/kernels/gemm_nt4.hip``), ``nsa<v>``
 (weight grads: split-K kernel variant v of ``csrc/kernels/gemm.hip``).  Weight-gradient
 candidates are timed into a scratch buffer so the real accumulator is touched exactly once.
 Our kernels win ties: a library candidate is picked only when it is more than
@@ -212,12 +213,19 @@ def _fwd_pick(x2, w):
         return "hipblaslt"
     cands = {"hipblaslt": lambda: x2 @ w.t()} if _library_ok(M, N, K) else {}
     cands["nt"] = lambda: _gemm.nt(x2, w)
+    cands["nt4"] = lambda: _gemm.nt(x2, w, w4=True)
     return choose(("fwd", M, N, K), cands)
+
+
+def _native(name, a, b, epi=0, u=None):
+    """Run native candidate ``name`` ("nt*": eight-wave kernel, "nt4*": four-wave kernel)."""
+    return _gemm.nt(a, b, epi=epi, u=u, w4=name.startswith("nt4"))
 
 
 def fwd(x2, w):
     """y = x2 @ w^T (bf16)."""
-    return x2 @ w.t() if _fwd_pick(x2, w) == "hipblaslt" else _gemm.nt(x2, w)
+    name = _fwd_pick(x2, w)
+    return x2 @ w.t() if name == "hipblaslt" else _native(name, x2, w)
 
 
 # Weight generation: bumped whenever the bf16 compute weights are rewritten outside
@@ -273,6 +281,7 @@ def _dgrad_pick(dy2, w):
         return "hipblaslt"
     cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
     cands["nt"] = lambda: _gemm.nt(dy2, _wt(w))
+    cands["nt4"] = lambda: _gemm.nt(dy2, _wt(w), w4=True)
     return choose(("dgrad", M, N, K), cands)
 
 
@@ -286,7 +295,7 @@ def dgrad(dy2, w):
         return dy2 @ w
     if name == "hipblaslt_t":
         return dy2 @ _wt(w).t()
-    return _gemm.nt(dy2, _wt(w))
+    return _native(name, dy2, _wt(w))
 
 
 def _gelu_fwd(u):
@@ -320,9 +329,10 @@ def fwd_gelu(x2, w):
     # the split form counts as a library candidate when its GEMM is the library's, so the
     # fused kernel wins within NATIVE_MARGIN of it (as against a plain library GEMM)
     sname = "split_lib" if _is_library(_fwd_pick(x2, w)) else "split"
-    cands = {sname: split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)}
+    cands = {sname: split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU),
+             "nt4gelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU, w4=True)}
     name = choose(("fwd_gelu", M, N, K), cands)
-    return split() if name.startswith("split") else _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)
+    return split() if name.startswith("split") else _native(name, x2, w, epi=_gemm.NT_EPI_GELU)
 
 
 def dgrad_dgelu(dy2, w, u, between=None):
@@ -346,11 +356,12 @@ def dgrad_dgelu(dy2, w, u, between=None):
         return _gelu_bwd(dg, u)
 
     sname = "split_lib" if _is_library(_dgrad_pick(dy2, w)) else "split"
-    cands = {sname: split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)}
+    cands = {sname: split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u),
+             "nt4dgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, w4=True)}
     name = choose(("dgrad_dgelu", M, N, K), cands)
     if name.startswith("split"):
         return split(between)
-    du = _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)
+    du = _native(name, dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)
     if between is not None:
         between()
     return du

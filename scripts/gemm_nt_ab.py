@@ -132,6 +132,7 @@ def main():
             print(json.dumps({"check": f"{name}/{nm}", "rel_err": e}), flush=True)
         for gm_ in [int(t) for t in a.gms.split(",") if t]:
             cands[f"nt_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_)
+            cands[f"nt4_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_, w4=True)
         for v in [int(t) for t in a.vars.split(",") if t and t != "0"]:
             cands[f"nt_v{v}"] = lambda v=v: gemm.nt(x, w, var=v)
             if v:

@@ -142,3 +142,39 @@ def test_transpose_bf16(kernels, R, C):
     assert torch.equal(t, w.t())
     t2 = gemm_tune._transpose(w * 2, out=t)  # rebuilt in place
     assert t2.data_ptr() == t.data_ptr() and torch.equal(t2, (w * 2).t())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
+                                   (256, 256, 64), (1000, 1288, 640), (8200, 768, 3072), (4096, 768, 4608)])
+def test_nt4_matches_fp32_and_nt(kernels, M, N, K):
+    """Four-wave persistent NT kernel (gemm_nt4.hip) vs fp32 torch, and bitwise against the
+    eight-wave kernel (same accumulation order per output: one K-tile at a time, k-steps in
+    order) for the plain, GELU and GELU' epilogues; ragged M / N exercise the shifted tail
+    tiles and the drained (uncounted) epilogue, 8200 x 768 several tiles per workgroup."""
+    from nanosandbox_amd.ops import gemm
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    y4 = gemm.nt(x, w, w4=True)
+    assert rel(y4, x.float() @ w.float().t()) < 1e-2
+    u4, g4 = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, w4=True)
+    assert torch.equal(u4, y4)
+    assert rel(g4, F.gelu(u4.float())) < 1e-2
+    for st in (1, 2):
+        assert torch.equal(gemm.nt(x, w, var=st, w4=True), y4)
+    u = torch.randn(M, N, device=DEV).to(BF)
+    d4 = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, w4=True)
+    uf = u.float()
+    gp = 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
+    assert rel(d4, y4.float() * gp) < 1e-2
+
+
+def test_nt4_asymmetric_identity(kernels):
+    """A = I with an asymmetric B through the four-wave kernel: a row/column swap or a wrong
+    column permutation of the staged B image shows up exactly (guide §3)."""
+    from nanosandbox_amd.ops import gemm
+    n = 512
+    eye = torch.eye(n, device=DEV).to(BF)
+    b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(251).to(BF)
+    assert torch.equal(gemm.nt(eye, b, w4=True).float(), b.float().t())
+    assert torch.equal(gemm.nt(b, eye, w4=True).float(), b.float())
