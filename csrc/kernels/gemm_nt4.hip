@@ -27,9 +27,11 @@
 // SGPR soffset and one per-lane VGPR offset (XOR swizzle of the 16-B chunk in the source
 // address, cdna_hip_programming.md rule 21): no VALU work per DMA.
 //
-// B rows are staged in a permuted order (image row q holds output column pi(q)) so that a
-// lane's accumulators of fragments 2p and 2p+1 cover 8 CONSECUTIVE output columns: the
-// epilogue writes 16 B per lane straight from the accumulators, no LDS round trip.
+// The MFMA's first operand is the A fragment, so a lane holds rows 4 (l >> 4) + e (e = 0..3)
+// of output column l & 15 of each 16x16 tile.  B rows are staged in a permuted order: image
+// row 16 j + r of a wave's half holds output column 8 r + j, so for one (i, e) a lane's
+// accumulators of the 8 fragments j are 8 CONSECUTIVE columns and one store instruction
+// writes 4 rows x 256 contiguous bytes straight from the accumulators (no LDS round trip).
 //
 // Persistent: grid = #CUs, tiles walked in the XCD-grouped order of gemm_nt.hip; the DMA
 // cursor runs straight on into the next tile, so the next tile's first two K-tiles load
@@ -45,14 +47,9 @@ constexpr int Q_BM = 256, Q_BN = 256, Q_BK = 64;
 constexpr int Q_THR = 256;
 constexpr int Q_IMG = Q_BM * Q_BK * 2;  // 32 KiB: one operand's [256][64] bf16 K-tile image
 constexpr int Q_BUF = 2 * Q_IMG;        // A image, then B image
-constexpr int Q_STG = 8192;            // epilogue staging per wave (32 rows x 128 columns bf16)
-constexpr int Q_SMEM = 2 * Q_BUF + 4 * Q_STG;  // 128 KiB of K-tile buffers + 32 KiB staging = 160 KiB
-static_assert(Q_SMEM <= 163840, "LDS budget");
+constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 #ifndef NSA_NT4_STAG
 #define NSA_NT4_STAG 1  // start-time stagger phases: workgroup v starts (v % STAG) / STAG of a tile late
-#endif
-#ifndef NSA_NT4_EPI_LDS
-#define NSA_NT4_EPI_LDS 0  // 1: whole-row stores re-shaped through LDS; 0: 64-B row pieces from the registers
 #endif
 
 #ifndef NSA_NT4_SCHED
@@ -104,12 +101,12 @@ __device__ __forceinline__ void q_for(F&& f, std::integer_sequence<int, Is...>) 
   (f(QI<Is>{}), ...);
 }
 
-__device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+__device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // first k-step of an output tile: the accumulator starts from 0 (no zeroing pass)
-__device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+__device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
@@ -136,11 +133,22 @@ __device__ __forceinline__ void q_vmwait() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc.base + soff + voff land at lds + 16 l
+// one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc.base + soff + voff + OFF land at
+// M0 + OFF + 16 l.  Pieces go in groups of four consecutive KiB of LDS: the group's first
+// piece (OFF = 0) writes M0, the other three reuse it with the instruction offset (which
+// applies to the LDS and the global address alike; their soff carries -OFF), so a group
+// costs one M0 write instead of four.  Nothing else in the kernel touches M0 between the
+// pieces of a group (checked in the ISA: no other m0 writes).
+template <int OFF>
 __device__ __forceinline__ void q_dma(uint32_t lds, uint32_t voff, q_i32x4 rsrc, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(voff),
-               "s"(rsrc), "s"(soff)
-               : "memory");
+  if constexpr (OFF == 0) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(voff),
+                 "s"(rsrc), "s"(soff)
+                 : "memory");
+  } else {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds" ::"v"(voff), "s"(rsrc), "s"(soff), "n"(OFF)
+                 : "memory");
+  }
 }
 
 __device__ __forceinline__ void q_tile_coords(const Nt4Args& g, int seq, int& m0, int& n0, int& mlo, int& nlo) {
@@ -154,6 +162,8 @@ __device__ __forceinline__ void q_tile_coords(const Nt4Args& g, int seq, int& m0
   m0 = min(mlo, g.M - Q_BM);
   n0 = min(nlo, g.N - Q_BN);
 }
+
+constexpr int Q_GRP = 3072;  // largest instruction offset inside an M0 group of DMA pieces
 
 // raw buffer resource over [base, base + bytes): gfx9 word 3 = 0x00020000 (32-bit data format)
 __device__ __forceinline__ q_i32x4 q_rsrc(const void* base, uint32_t bytes) {
@@ -180,8 +190,10 @@ __device__ __forceinline__ void q_cur_tile(const Nt4Args& g, QCur& c, int seq) {
   if (c.valid) {
     int m0, n0, mlo, nlo;
     q_tile_coords(g, seq, m0, n0, mlo, nlo);
-    c.ra = q_rsrc(g.A + (int64_t)m0 * g.lda, (uint32_t)(Q_BM * g.lda * 2));
-    c.rb = q_rsrc(g.B + (int64_t)n0 * g.ldb, (uint32_t)(Q_BN * g.ldb * 2));
+    // the resource base sits Q_GRP bytes below the tile's first row (every soffset carries
+    // +Q_GRP), so the soffsets of a piece group never go negative
+    c.ra = q_rsrc(reinterpret_cast<const char*>(g.A + (int64_t)m0 * g.lda) - Q_GRP, (uint32_t)(Q_BM * g.lda * 2 + Q_GRP));
+    c.rb = q_rsrc(reinterpret_cast<const char*>(g.B + (int64_t)n0 * g.ldb) - Q_GRP, (uint32_t)(Q_BN * g.ldb * 2 + Q_GRP));
   } else {
     // past the last tile the slots still issue their pieces (no branches in the K-tile
     // body, vmcnt counts stay fixed): an empty range makes every load out of bounds, so
@@ -227,8 +239,9 @@ __device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32
   }
 }
 
-// Epilogue straight from the accumulators: lane l holds row 16 i + (l & 15) of the wave's
-// 128 rows and, over fragments 2p / 2p+1, the 8 consecutive columns 32 p + 8 (l >> 4) + 0..7.
+// Epilogue straight from the accumulators: for fragment row i and element e, lane l holds
+// row 16 i + 4 (l >> 4) + e of the wave's 128 rows, columns 8 (l & 15) + 0..7 (fragments
+// j = 0..7), so the 16 lanes of a quarter-wave write one row's 256 contiguous bytes.
 template <int EPI, bool NT>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
                                            int lane) {
@@ -236,30 +249,35 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
   q_tile_coords(g, seq, m0, n0, mlo, nlo);
   const bool full = (m0 == mlo) & (n0 == nlo);
   const int r = lane & 15, q = lane >> 4;
+  const int col = n0 + wn * 128 + 8 * r;
+  // EPI_DGELU: the U pieces of two fragment rows are in flight at a time
+  q_u32x4 uv[2][4];
+  auto load_u = [&](int i, q_u32x4 (&dst)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = m0 + wm * 128 + 16 * i + 4 * q + e;  // in bounds: tiles lie inside the matrix
+      dst[e] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)row * g.ldc + col));
+    }
+  };
+  if constexpr (EPI == Q_EPI_DGELU) {
+    load_u(0, uv[0]);
+    load_u(1, uv[1]);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wm * 128 + 16 * i + r;
-    q_u32x4 uv[4];
-    if constexpr (EPI == Q_EPI_DGELU) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int col = n0 + wn * 128 + 32 * p + 8 * q;
-        uv[p] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)row * g.ldc + col));
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int col = n0 + wn * 128 + 32 * p + 8 * q;
+    for (int e = 0; e < 4; ++e) {
+      const int row = m0 + wm * 128 + 16 * i + 4 * q + e;
       if (!full && (row < mlo || col < nlo)) continue;
-      const f32x4 x = acc[i][2 * p], y = acc[i][2 * p + 1];
-      uint32_t w[4] = {pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]), pack2(y[2], y[3])};
+      uint32_t w[4] = {pack2(acc[i][0][e], acc[i][1][e]), pack2(acc[i][2][e], acc[i][3][e]),
+                       pack2(acc[i][4][e], acc[i][5][e]), pack2(acc[i][6][e], acc[i][7][e])};
       if constexpr (EPI == Q_EPI_DGELU) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t u = uv[p][e];
-          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
-          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
-          w[e] = pack2(a0, a1);
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t u = uv[i & 1][e][h];
+          const float a0 = __uint_as_float(w[h] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
+          const float a1 = __uint_as_float(w[h] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
+          w[h] = pack2(a0, a1);
         }
       }
       const int64_t off = (int64_t)row * g.ldc + col;
@@ -267,84 +285,21 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
       if constexpr (EPI == Q_EPI_GELU) {
         uint32_t gg[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
+        for (int h = 0; h < 4; ++h)
+          gg[h] = pack2(nsa_gelu(__uint_as_float(w[h] << 16)), nsa_gelu(__uint_as_float(w[h] & 0xffff0000u)));
         q_st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
       }
     }
-  }
-}
-
-
-// Epilogue through a wave-private 8-KiB LDS slice, in 4 rounds of 32 rows x 128 columns:
-// the accumulators go in as 16-B pieces (lane l: row 16 i2 + (l & 15), chunk 4 p + (l >> 4)),
-// come back as whole-row chunks (lane l: row 4 k + (l & 3), chunk l >> 2), so each store
-// instruction writes 4 rows x 256 contiguous bytes.  Physical chunk = chunk ^ swz(row),
-// swz = 4 (row & 3) + ((row >> 2) & 3): the 8 rows of a ds_write_b128 lane group and the
-// 4 rows x 4 chunks of a ds_read_b128 lane group all land in distinct 16-B bank groups.
-__device__ __forceinline__ int q_swz(int row) { return 4 * (row & 3) + ((row >> 2) & 3); }
-
-template <int EPI, bool NT>
-__device__ __forceinline__ void q_epilogue_lds(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
-                                               int lane, char* stage) {
-  int m0, n0, mlo, nlo;
-  q_tile_coords(g, seq, m0, n0, mlo, nlo);
-  const bool full = (m0 == mlo) & (n0 == nlo);
-  const int r = lane & 15, q = lane >> 4;
-  const int rr = lane & 3, cc = lane >> 2;
-  const int col = n0 + wn * 128 + 8 * cc;
-#pragma unroll
-  for (int rd = 0; rd < 4; ++rd) {
-#pragma unroll
-    for (int i2 = 0; i2 < 2; ++i2) {
-      const int row = 16 * i2 + r;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const f32x4 x = acc[2 * rd + i2][2 * p], y = acc[2 * rd + i2][2 * p + 1];
-        *reinterpret_cast<uint4*>(stage + row * 256 + (((4 * p + q) ^ q_swz(row)) << 4)) =
-            make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]), pack2(y[2], y[3]));
-      }
-    }
-    q_u32x4 uv[8];
     if constexpr (EPI == Q_EPI_DGELU) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int grow = m0 + wm * 128 + 32 * rd + 4 * k + rr;
-        uv[k] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)grow * g.ldc + col));
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int row = 4 * k + rr;
-      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * 256 + ((cc ^ q_swz(row)) << 4));
-      const int grow = m0 + wm * 128 + 32 * rd + row;
-      if (!full && (grow < mlo || col < nlo)) continue;
-      uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      if constexpr (EPI == Q_EPI_DGELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t u = uv[k][e];
-          const float a0 = __uint_as_float(w[e] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
-          const float a1 = __uint_as_float(w[e] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
-          w[e] = pack2(a0, a1);
-        }
-      }
-      const int64_t off = (int64_t)grow * g.ldc + col;
-      q_st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
-      if constexpr (EPI == Q_EPI_GELU) {
-        uint32_t gg[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          gg[e] = pack2(nsa_gelu(__uint_as_float(w[e] << 16)), nsa_gelu(__uint_as_float(w[e] & 0xffff0000u)));
-        q_st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
-      }
+      if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
     }
   }
 }
 
 }  // namespace
 
-// PROBE (timing only, wrong results): 1 = no DMA after the prologue, 4 = no epilogue stores
+// PROBE (timing only, wrong results): 1 = no DMA after the prologue, 2 = no wait for the
+// previous K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue stores
 template <int EPI, bool NT, int PROBE>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   __shared__ __attribute__((aligned(16))) char smem[Q_SMEM];
@@ -367,22 +322,25 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   // ---- DMA geometry.  Wave w copies pieces P = 8 w + p (p = 0..7) of each image: image rows
   // 8 P + i, i = lane >> 3, physical 16-B chunk lane & 7, which holds logical chunk
   // (lane & 7) ^ s(row), s(r) = (r >> 1) & 7 = (4 (p & 1) + (i >> 1)) & 7.
-  // A: image row = tile row.  B: image row q holds tile column pi(q) (see the header):
-  // for a piece, pi = 64 w + 32 (p >> 2) + 16 (p & 1) + 4 ((p >> 1) & 1) + 8 (i >> 2) + (i & 3).
+  // A: image row = tile row.  B: image row q = 128 h + 16 j + r holds tile column
+  // 128 h + 8 r + j (see the header): for a piece, 128 (w >> 1) + 64 (p & 1) + 4 (w & 1)
+  // + (p >> 1) + 8 i.
   const int li = lane >> 3, lc = lane & 7;
   uint32_t voA[2], voB[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const uint32_t ch = (uint32_t)((lc ^ ((4 * h + (li >> 1)) & 7)) << 4);
     voA[h] = (uint32_t)(li * g.lda * 2) + ch;
-    voB[h] = (uint32_t)((8 * (li >> 2) + (li & 3)) * g.ldb * 2) + ch;
+    voB[h] = (uint32_t)(8 * li * g.ldb * 2) + ch;
   }
+  // per-piece row offsets, less the instruction offset of the piece in its M0 group, plus the
+  // Q_GRP the resource base was lowered by (so never negative)
   uint32_t soA[8], soB[8];
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
-    soA[p] = (uint32_t)__builtin_amdgcn_readfirstlane((64 * wave + 8 * p) * g.lda * 2);
+    soA[p] = (uint32_t)__builtin_amdgcn_readfirstlane((64 * wave + 8 * p) * g.lda * 2 + Q_GRP - (p & 3) * 1024);
     soB[p] = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (64 * wave + 32 * (p >> 2) + 16 * (p & 1) + 4 * ((p >> 1) & 1)) * g.ldb * 2);
+        (128 * (wave >> 1) + 64 * (p & 1) + 4 * (wave & 1) + (p >> 1)) * g.ldb * 2 + Q_GRP - (p & 3) * 1024);
   }
   const uint32_t dmaA0 = lds0 + (uint32_t)(wave * 8 * 1024);          // + buffer + p * 1 KiB
   const uint32_t dmaB0 = lds0 + (uint32_t)(Q_IMG + wave * 8 * 1024);
@@ -398,11 +356,14 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     rB[kk] = lds0 + (uint32_t)(Q_IMG + (wn * 128 + (lane & 15)) * 128) + ch;
   }
 
-  auto issue_a = [&](const QCur& c, uint32_t buf, int p) {
-    q_dma(dmaA0 + buf + (uint32_t)(p * 1024), voA[p & 1], c.ra, soA[p]);
+  // piece P of K-tile cursor c into buffer buf (the pieces of an M0 group are issued in order)
+  auto issue_a = [&](const QCur& c, uint32_t buf, auto P) {
+    constexpr int p = decltype(P)::value;
+    q_dma<(p & 3) * 1024>(dmaA0 + buf + (uint32_t)((p & 4) * 1024), voA[p & 1], c.ra, soA[p]);
   };
-  auto issue_b = [&](const QCur& c, uint32_t buf, int p) {
-    q_dma(dmaB0 + buf + (uint32_t)(p * 1024), voB[p & 1], c.rb, soB[p]);
+  auto issue_b = [&](const QCur& c, uint32_t buf, auto P) {
+    constexpr int p = decltype(P)::value;
+    q_dma<(p & 3) * 1024>(dmaB0 + buf + (uint32_t)((p & 4) * 1024), voB[p & 1], c.rb, soB[p]);
   };
 
   if constexpr (NSA_NT4_STAG > 1) {
@@ -414,15 +375,11 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   // ---- prologue: K-tiles 0 and 1 of this workgroup's sequence into buffers 0 / 1
   QCur c;
   q_cur_tile(g, c, v);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) issue_a(c, 0, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) issue_b(c, 0, p);
+  q_for([&](auto P) { issue_a(c, 0, P); }, std::make_integer_sequence<int, 8>{});
+  q_for([&](auto P) { issue_b(c, 0, P); }, std::make_integer_sequence<int, 8>{});
   q_cur_next(g, c, nk, G);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) issue_a(c, Q_BUF, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) issue_b(c, Q_BUF, p);
+  q_for([&](auto P) { issue_a(c, Q_BUF, P); }, std::make_integer_sequence<int, 8>{});
+  q_for([&](auto P) { issue_b(c, Q_BUF, P); }, std::make_integer_sequence<int, 8>{});
   q_vmwait<16>();
   q_cur_next(g, c, nk, G);  // c = the K-tile the first loop iteration's slots issue (two ahead)
   q_barrier();
@@ -448,10 +405,10 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       constexpr int n = decltype(I)::value;
       constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
       if constexpr (kk == 0) {
-        if constexpr (FIRST) q_mfma0(acc[i][j], b0[j], a0[i]);
-        else q_mfma(acc[i][j], b0[j], a0[i]);
+        if constexpr (FIRST) q_mfma0(acc[i][j], a0[i], b0[j]);
+        else q_mfma(acc[i][j], a0[i], b0[j]);
       } else {
-        q_mfma(acc[i][j], b1[j], a1[i]);
+        q_mfma(acc[i][j], a1[i], b1[j]);
       }
 #if NSA_NT4_SCHED == 0
       // k-step 1 A fragments (this buffer)
@@ -460,13 +417,13 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       if constexpr (n == 21) q_barrier();
       // K-tile t+2's A image into this buffer, k-step 1 B fragments between the pieces
       if constexpr (n >= 22 && n <= 50 && ((n - 22) & 3) == 0) {
-        if constexpr (dv) issue_a(c, buf, (n - 22) >> 2);
+        if constexpr (dv) issue_a(c, buf, QI<((n - 22) >> 2)>{});
       }
       if constexpr (n >= 23 && n <= 37 && ((n - 23) & 1) == 0) q_rd<(n - 23) / 2 * 2048>(b1[(n - 23) / 2], rB[1] + buf);
       if constexpr (n == 56) q_wait8(b1);
       if constexpr (n == 57) q_barrier();
       if constexpr (n >= 58 && n <= 74 && ((n - 58) & 3) == 0) {
-        if constexpr (dv) issue_b(c, buf, (n - 58) >> 2);
+        if constexpr (dv) issue_b(c, buf, QI<((n - 58) >> 2)>{});
       }
       // K-tile t+1 has landed (its 16 pieces are older than this K-tile's 13)
       if constexpr (n == 90) {
@@ -480,7 +437,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
       }
       if constexpr (n == 97 || n == 105 || n == 113) {
-        if constexpr (dv) issue_b(c, buf, 5 + (n - 97) / 8);
+        if constexpr (dv) issue_b(c, buf, QI<(5 + (n - 97) / 8)>{});
       }
 #else
       // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
@@ -491,19 +448,19 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         else q_rd<(s - 8) * 2048>(b1[s - 8], rB[1] + buf);
       }
       if constexpr (n == 32) q_wait16(a1, b1);
-      if constexpr (n == 33) q_barrier();
+      if constexpr (n == 33 && PROBE != 3) q_barrier();
       constexpr int D0 = 34, DS = NSA_NT4_DS, VMS = NSA_NT4_VMS;
       static_assert(D0 + 15 * DS <= 127 && VMS + 2 + 15 * NSA_NT4_RS <= 127, "every piece and read fits the K-tile");
       if constexpr (n >= D0 && (n - D0) % DS == 0 && (n - D0) / DS < 16) {
         constexpr int pc = (n - D0) / DS;
         if constexpr (dv) {
-          if constexpr (pc < 8) issue_a(c, buf, pc);
-          else issue_b(c, buf, pc - 8);
+          if constexpr (pc < 8) issue_a(c, buf, QI<pc>{});
+          else issue_b(c, buf, QI<pc - 8>{});
         }
       }
       constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
-      if constexpr (n == VMS) q_vmw<dv ? issued : 0, EPI>(FIRST && pend);
-      if constexpr (n == VMS + 1) q_barrier();
+      if constexpr (n == VMS && PROBE != 2) q_vmw<dv ? issued : 0, EPI>(FIRST && pend);
+      if constexpr (n == VMS + 1 && PROBE != 3) q_barrier();
       if constexpr (n >= VMS + 2 && n < VMS + 2 + 16 * NSA_NT4_RS && (n - VMS - 2) % NSA_NT4_RS == 0) {
         constexpr int s = (n - VMS - 2) / NSA_NT4_RS;
         if constexpr (s < 8) q_rd<s * 2048>(b0[s], rB[0] + nb);
@@ -521,10 +478,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      if constexpr (NSA_NT4_EPI_LDS)
-        q_epilogue_lds<EPI, NT>(g, acc, seq, wm, wn, lane, smem + 2 * Q_BUF + wave * Q_STG);
-      else
-        q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
+      q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -559,7 +513,8 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   if (M < Q_BM || N < Q_BN || K < Q_BK || K % Q_BK != 0 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K ||
       ldb < K || ldc < N || grid < 1)
     return hipErrorInvalidValue;
-  if ((int64_t)Q_BM * lda * 2 >= (1ll << 31) || (int64_t)Q_BN * ldb * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+  if ((int64_t)Q_BM * lda * 2 + Q_GRP >= (1ll << 31) || (int64_t)Q_BN * ldb * 2 + Q_GRP >= (1ll << 31))
+    return hipErrorInvalidValue;
   if ((epi == Q_EPI_GELU && !C2) || (epi == Q_EPI_DGELU && !U)) return hipErrorInvalidValue;
   Nt4Args a{};
   a.A = (const bf16_t*)A;
@@ -583,6 +538,8 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
 #define NT4_LAUNCH(E)                                                        \
   if (probe == 1) gemm_nt4_kernel<E, true, 1><<<gr, Q_THR, 0, s>>>(a);       \
+  else if (probe == 2) gemm_nt4_kernel<E, true, 2><<<gr, Q_THR, 0, s>>>(a);  \
+  else if (probe == 3) gemm_nt4_kernel<E, true, 3><<<gr, Q_THR, 0, s>>>(a);  \
   else if (probe == 4) gemm_nt4_kernel<E, true, 4><<<gr, Q_THR, 0, s>>>(a);  \
   else if (nt) gemm_nt4_kernel<E, true, 0><<<gr, Q_THR, 0, s>>>(a);          \
   else gemm_nt4_kernel<E, false, 0><<<gr, Q_THR, 0, s>>>(a);

@@ -63,6 +63,11 @@ def nt_supported(M, N, K) -> bool:
     return M >= 256 and N >= 256 and K >= BK and K % BK == 0 and N % 8 == 0
 
 
+def nt4_supported(M, N, K) -> bool:
+    """Shape rules of the four-wave kernel (the same as the eight-wave kernel's)."""
+    return nt_supported(M, N, K)
+
+
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 

@@ -213,7 +213,8 @@ def _fwd_pick(x2, w):
         return "hipblaslt"
     cands = {"hipblaslt": lambda: x2 @ w.t()} if _library_ok(M, N, K) else {}
     cands["nt"] = lambda: _gemm.nt(x2, w)
-    cands["nt4"] = lambda: _gemm.nt(x2, w, w4=True)
+    if _gemm.nt4_supported(M, N, K):
+        cands["nt4"] = lambda: _gemm.nt(x2, w, w4=True)
     return choose(("fwd", M, N, K), cands)
 
 
@@ -281,7 +282,8 @@ def _dgrad_pick(dy2, w):
         return "hipblaslt"
     cands = {"hipblaslt": lambda: dy2 @ w, "hipblaslt_t": lambda: dy2 @ _wt(w).t()} if _library_ok(M, K, N) else {}
     cands["nt"] = lambda: _gemm.nt(dy2, _wt(w))
-    cands["nt4"] = lambda: _gemm.nt(dy2, _wt(w), w4=True)
+    if _gemm.nt4_supported(M, K, N):
+        cands["nt4"] = lambda: _gemm.nt(dy2, _wt(w), w4=True)
     return choose(("dgrad", M, N, K), cands)
 
 
@@ -329,8 +331,9 @@ def fwd_gelu(x2, w):
     # the split form counts as a library candidate when its GEMM is the library's, so the
     # fused kernel wins within NATIVE_MARGIN of it (as against a plain library GEMM)
     sname = "split_lib" if _is_library(_fwd_pick(x2, w)) else "split"
-    cands = {sname: split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU),
-             "nt4gelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU, w4=True)}
+    cands = {sname: split, "ntgelu": lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU)}
+    if _gemm.nt4_supported(M, N, K):
+        cands["nt4gelu"] = lambda: _gemm.nt(x2, w, epi=_gemm.NT_EPI_GELU, w4=True)
     name = choose(("fwd_gelu", M, N, K), cands)
     return split() if name.startswith("split") else _native(name, x2, w, epi=_gemm.NT_EPI_GELU)
 
@@ -356,8 +359,9 @@ def dgrad_dgelu(dy2, w, u, between=None):
         return _gelu_bwd(dg, u)
 
     sname = "split_lib" if _is_library(_dgrad_pick(dy2, w)) else "split"
-    cands = {sname: split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u),
-             "nt4dgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, w4=True)}
+    cands = {sname: split, "ntdgelu": lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u)}
+    if _gemm.nt4_supported(M, K, N):
+        cands["nt4dgelu"] = lambda: _gemm.nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, w4=True)
     name = choose(("dgrad_dgelu", M, N, K), cands)
     if name.startswith("split"):
         return split(between)

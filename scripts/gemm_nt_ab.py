@@ -93,7 +93,7 @@ def main():
               "mlp.c_proj.dx": (3072, 768), "lm_head.dx": (768, 50304)}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     print(json.dumps({"device": torch.cuda.get_device_name(), "cus": gemm.num_cus()}), flush=True)
-    for (m_, n_, k_) in ((1000, 520, 192), (256, 256, 64), (777, 1288, 640), (4096, 50304, 128)):
+    for (m_, n_, k_) in ((1000, 520, 320), (256, 256, 256), (777, 1288, 640), (4096, 50304, 256)):
         x = uni(m_, k_)
         w = uni(n_, k_)
         ref = x.float() @ w.float().t()
@@ -142,6 +142,7 @@ def main():
         if a.probe:
             for pr, nm in ((1, "nodma"), (4, "nostore")):
                 cands[f"nt_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr)
+            for pr, nm in ((1, "nodma"), (2, "novmwait"), (3, "nobarrier"), (4, "nostore")):
                 cands[f"nt4_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr, w4=True)
         if a.epi and name in ("c_fc", "mlp.c_proj.dx"):
             if name == "c_fc":
