@@ -61,6 +61,9 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 #ifndef NSA_NT4_VMS
 #define NSA_NT4_VMS 92  // SCHED 1: slot of the wait for the previous K-tile's pieces
 #endif
+#ifndef NSA_NT4_ER
+#define NSA_NT4_ER 1  // SCHED 1: MFMAs between the k-step-1 fragment reads at the K-tile head
+#endif
 #ifndef NSA_NT4_RS
 #define NSA_NT4_RS 2  // SCHED 1: MFMAs between the next K-tile's fragment reads
 #endif
@@ -71,7 +74,8 @@ enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2 };
 #if NSA_NT4_SCHED == 0
 constexpr int Q_ISS = 13;
 #else
-constexpr int Q_ISS = (NSA_NT4_VMS - 34) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - 34) / NSA_NT4_DS + 1 : 16;
+constexpr int Q_D0 = 15 * NSA_NT4_ER + 4;  // slot of the first piece
+constexpr int Q_ISS = (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 : 16;
 #endif
 // vector-memory operations of one wave's epilogue of a full tile (stores, and the U loads)
 template <int EPI>
@@ -442,14 +446,15 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
 #else
       // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
       // K-tile t+2 spread one per DS MFMAs, then K-tile t+1's k-step-0 fragments
-      if constexpr (n <= 30 && (n & 1) == 0) {
-        constexpr int s = n >> 1;
+      constexpr int ER = NSA_NT4_ER;  // MFMAs between the k-step-1 fragment reads
+      if constexpr (n <= 15 * ER && n % ER == 0) {
+        constexpr int s = n / ER;
         if constexpr (s < 8) q_rd<s * 2048>(a1[s], rA[1] + buf);
         else q_rd<(s - 8) * 2048>(b1[s - 8], rB[1] + buf);
       }
-      if constexpr (n == 32) q_wait16(a1, b1);
-      if constexpr (n == 33 && PROBE != 3) q_barrier();
-      constexpr int D0 = 34, DS = NSA_NT4_DS, VMS = NSA_NT4_VMS;
+      if constexpr (n == 15 * ER + 2) q_wait16(a1, b1);
+      if constexpr (n == 15 * ER + 3 && PROBE != 3) q_barrier();
+      constexpr int D0 = 15 * ER + 4, DS = NSA_NT4_DS, VMS = NSA_NT4_VMS;
       static_assert(D0 + 15 * DS <= 127 && VMS + 2 + 15 * NSA_NT4_RS <= 127, "every piece and read fits the K-tile");
       if constexpr (n >= D0 && (n - D0) % DS == 0 && (n - D0) / DS < 16) {
         constexpr int pc = (n - D0) / DS;
