@@ -1,0 +1,343 @@
+// Four-wave bf16 weight-gradient GEMM for gfx950 (dW = dY^T · X), the
+// main loop of gemm_nt4.hip on operands stored token-major:
+//
+//   C[M,N] (+)= A[K,M]^T · B[K,N]   A = dY [tokens][out] (lda), B = X [tokens][in] (ldb),
+//                                   C fp32 [out][in] (the flat gradient), K = tokens,
+//                                   split over blockIdx.z (split z owns K-tiles
+//                                   [z n / S, (z+1) n / S), any split count)
+//
+// Per workgroup one 256x256 output tile, 4 waves of 128x128 (8x8 accumulators of
+// v_mfma_f32_16x16x32_bf16 in AGPRs, tied asm operands).  A K-tile is 64 tokens: two images
+// [64][256] bf16 (512-B rows) staged by LDS-DMA (buffer_load_dwordx4 ... lds, one M0 write
+// per group of four 1-KiB pieces, piece = 2 token rows) into two buffers; the MFMA fragments
+// (16 rows/columns x 32 tokens) are read transposed with ds_read_b64_tr_b16, two per
+// fragment.  Image chunk swizzle: 16-B chunk c of row r at c ^ 2 g(r), g = (r & 3) |
+// ((r >> 3) & 1) << 2 (the eight rows of a transposed read's lane groups in eight distinct
+// 32-B bank groups; the same image as gemm.hip's rimg).  Schedule per K-tile (MFMA slots):
+//   n 0-31   the k-step-1 fragments (32 transposed reads, this buffer)
+//   n 33/34  wait, barrier (this buffer is free)
+//   n 35-125 LDS-DMA of K-tile t+2 into this buffer, one piece per 6 MFMAs
+//   n 92/93  vmcnt, barrier (K-tile t+1 has landed)
+//   n 94-125 K-tile t+1's k-step-0 fragments (32 reads, other buffer)
+// MFMA operands are swapped (B fragment first) so a lane holds 4 consecutive output columns
+// of a row: the epilogue re-shapes 64-row halves through LDS into whole 256-B rows, one fp32
+// atomic (or plain store for the deterministic partials) per lane per row and half.
+#include <utility>
+
+#include "common.h"
+
+namespace {
+
+constexpr int W_BM = 256, W_BN = 256, W_BK = 64;
+constexpr int W_THR = 256;
+constexpr int W_IMG = W_BK * 256 * 2;  // 32 KiB: [64 tokens][256] bf16
+constexpr int W_SMEM = 4 * W_IMG;      // A0 A1 B0 B1
+constexpr int W_GRP = 3072;            // largest instruction offset inside an M0 group of pieces
+
+enum : int { W_EPI_ATOMIC = 1, W_EPI_STORE = 4 };
+
+typedef int w_i32x4 __attribute__((ext_vector_type(4)));
+
+struct Wg4Args {
+  const bf16_t* A;
+  const bf16_t* B;
+  float* C;
+  int M, N, K;
+  int lda, ldb, ldc;
+  int tiles_m, tiles_n, splits;
+};
+
+template <int I>
+struct WI {
+  static constexpr int value = I;
+};
+template <class F, int... Is>
+__device__ __forceinline__ void w_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(WI<Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void w_for(F&& f) {
+  w_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ void w_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+__device__ __forceinline__ void w_mfma0(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+}
+__device__ __forceinline__ void w_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void w_vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void w_dma(uint32_t lds, uint32_t voff, w_i32x4 rsrc, uint32_t soff) {
+  if constexpr (OFF == 0) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(voff),
+                 "s"(rsrc), "s"(soff)
+                 : "memory");
+  } else {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds" ::"v"(voff), "s"(rsrc), "s"(soff), "n"(OFF)
+                 : "memory");
+  }
+}
+__device__ __forceinline__ w_i32x4 w_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  w_i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32) & 0xffff);
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void w_add_base(w_i32x4& r, uint32_t bytes) {
+  uint64_t b = ((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x;
+  b += bytes;
+  r.x = (int)(uint32_t)b;
+  r.y = (int)(uint32_t)(b >> 32);
+}
+// transposed fragment half: lane l gets 4 consecutive tokens of column (l & 15)
+__device__ __forceinline__ s16x4 w_tr(uint32_t addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(uintptr_t)addr);
+}
+__device__ __forceinline__ bf16x8 w_cat(s16x4 a, s16x4 b) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ int w_g(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+}  // namespace
+
+template <int EPI>
+__global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
+  __shared__ __attribute__((aligned(16))) char smem[W_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+
+  // tile: blocks b, b+8, ... share an XCD; consecutive blocks of an XCD walk neighbouring
+  // tiles (row-major over the tile grid), the split index is blockIdx.z
+  const int tiles = g.tiles_m * g.tiles_n;
+  int v = blockIdx.x;
+  {
+    const int G = gridDim.x, x = v % 8, qq = G / 8, rr = G % 8;
+    v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + v / 8;
+  }
+  if (v >= tiles) return;
+  const int tm = v / g.tiles_n, tn = v % g.tiles_n;
+  const int mlo = tm * W_BM, nlo = tn * W_BN;
+  const int m0 = min(mlo, g.M - W_BM), n0 = min(nlo, g.N - W_BN);
+  const int nkt = g.K / W_BK, z = blockIdx.z;
+  const int kt0 = (int)((int64_t)z * nkt / g.splits), kt1 = (int)((int64_t)(z + 1) * nkt / g.splits);
+  const int nk = kt1 - kt0;
+
+  // ---- DMA geometry: wave w copies pieces P = 8 w + p of each image = token rows
+  // 16 w + 2 p + h (h = lane >> 5), physical chunk lane & 31 holding logical chunk
+  // (lane & 31) ^ 2 g(row); g depends on (p & 1, p >> 2, h) only.
+  const int h = lane >> 5, lc = lane & 31;
+  uint32_t voA[4], voB[4];
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    const int p = (pp & 1) | ((pp >> 1) << 2);  // representative piece of the class
+    const int row = 2 * p + h;
+    const uint32_t ch = (uint32_t)((lc ^ (2 * w_g(row))) << 4);
+    voA[pp] = (uint32_t)(h * g.lda * 2) + ch;
+    voB[pp] = (uint32_t)(h * g.ldb * 2) + ch;
+  }
+  uint32_t soA[8], soB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    soA[p] = (uint32_t)__builtin_amdgcn_readfirstlane((16 * wave + 2 * p) * g.lda * 2 + W_GRP - (p & 3) * 1024);
+    soB[p] = (uint32_t)__builtin_amdgcn_readfirstlane((16 * wave + 2 * p) * g.ldb * 2 + W_GRP - (p & 3) * 1024);
+  }
+  // LDS: A buffers at 0 / W_IMG, B buffers at 2 W_IMG / 3 W_IMG (buffer = XOR W_IMG)
+  const uint32_t dmaA = lds0 + (uint32_t)(wave * 8 * 1024);
+  const uint32_t dmaB = lds0 + (uint32_t)(2 * W_IMG + wave * 8 * 1024);
+
+  // buffer resources: token row kt0 * 64 of the tile's columns, lowered by W_GRP
+  const uint32_t stepA = (uint32_t)(W_BK * g.lda * 2), stepB = (uint32_t)(W_BK * g.ldb * 2);
+  w_i32x4 ra = w_rsrc(reinterpret_cast<const char*>(g.A + (int64_t)kt0 * W_BK * g.lda + m0) - W_GRP, 0xffffffffu);
+  w_i32x4 rb = w_rsrc(reinterpret_cast<const char*>(g.B + (int64_t)kt0 * W_BK * g.ldb + n0) - W_GRP, 0xffffffffu);
+  int kd = 0;  // K-tile index (within the split) of the cursor
+  auto cur_next = [&]() {
+    if (++kd >= nk) {
+      ra.z = 0;  // past the split's last K-tile: empty range, every piece loads nothing
+      rb.z = 0;
+    } else {
+      w_add_base(ra, stepA);
+      w_add_base(rb, stepB);
+    }
+  };
+  auto issue_a = [&](uint32_t buf, auto P) {
+    constexpr int p = decltype(P)::value;
+    w_dma<(p & 3) * 1024>(dmaA + buf + (uint32_t)((p & 4) * 1024), voA[(p & 1) | ((p >> 2) << 1)], ra, soA[p]);
+  };
+  auto issue_b = [&](uint32_t buf, auto P) {
+    constexpr int p = decltype(P)::value;
+    w_dma<(p & 3) * 1024>(dmaB + buf + (uint32_t)((p & 4) * 1024), voB[(p & 1) | ((p >> 2) << 1)], rb, soB[p]);
+  };
+
+  // ---- fragment read addresses (buffer 0, k-step 0, first half): fragment f covers columns
+  // 16 f of the wave's 128; lane (q, p) = (l & 15) >> 2, l & 3 reads token row
+  // 8 (l >> 4) + q, columns 16 f + 4 p: chunk 2 f' + (p >> 1) with f' the image column block.
+  // k-step 1 = +32 rows (16 KiB), second half = +4 rows (2 KiB): g is unchanged by both.
+  const int ig = lane & 15, fq = ig >> 2, fp = ig & 3;
+  const int krow = 8 * (lane >> 4) + fq;
+  const int gk = w_g(krow);
+  uint32_t rdA[8], rdB[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    const int fa = wm * 8 + f, fb = wn * 8 + f;  // 16-column blocks of the 256-wide image
+    rdA[f] = lds0 + (uint32_t)(krow * 512 + (((2 * fa + (fp >> 1)) ^ (2 * gk)) << 4) + (fp & 1) * 8);
+    rdB[f] = lds0 + (uint32_t)(2 * W_IMG + krow * 512 + (((2 * fb + (fp >> 1)) ^ (2 * gk)) << 4) + (fp & 1) * 8);
+  }
+
+  // ---- prologue: K-tiles 0 and 1 into buffers 0 / 1
+  w_for<8>([&](auto P) { issue_a(0, P); });
+  w_for<8>([&](auto P) { issue_b(0, P); });
+  cur_next();
+  w_for<8>([&](auto P) { issue_a(W_IMG, P); });
+  w_for<8>([&](auto P) { issue_b(W_IMG, P); });
+  w_vmwait<16>();
+  cur_next();
+  w_barrier();
+
+  f32x4 acc[8][8];
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a0[f] = w_cat(w_tr(rdA[f]), w_tr(rdA[f] + 2048));
+    b0[f] = w_cat(w_tr(rdB[f]), w_tr(rdB[f] + 2048));
+  }
+
+  uint32_t buf = 0;
+  auto ktile = [&](auto FIRST_) {
+    constexpr bool FIRST = decltype(FIRST_)::value;
+    w_for<128>([&](auto I) {
+      constexpr int n = decltype(I)::value;
+      constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
+      if constexpr (kk == 0) {
+        if constexpr (FIRST) w_mfma0(acc[i][j], b0[j], a0[i]);
+        else w_mfma(acc[i][j], b0[j], a0[i]);
+      } else {
+        w_mfma(acc[i][j], b1[j], a1[i]);
+      }
+      // k-step 1 fragments of this buffer, one transposed read per MFMA
+      if constexpr (n < 32) {
+        constexpr int f = (n >> 1) & 7, hf = n & 1;
+        if constexpr (n < 16) {
+          if constexpr (hf == 0) a1[f] = w_cat(w_tr(rdA[f] + 16384), w_tr(rdA[f] + 16384 + 2048));
+        } else {
+          if constexpr (hf == 0) b1[f] = w_cat(w_tr(rdB[f] + 16384), w_tr(rdB[f] + 16384 + 2048));
+        }
+      }
+      if constexpr (n == 33) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this buffer's reads done
+      if constexpr (n == 34) w_barrier();
+      constexpr int D0 = 35, DS = 6;
+      if constexpr (n >= D0 && (n - D0) % DS == 0 && (n - D0) / DS < 16) {
+        constexpr int pc = (n - D0) / DS;
+        if constexpr (pc < 8) issue_a(buf, WI<pc>{});
+        else issue_b(buf, WI<pc - 8>{});
+      }
+      if constexpr (n == 62) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+          rdA[f] ^= (uint32_t)W_IMG;
+          rdB[f] ^= (uint32_t)W_IMG;
+        }
+      }
+      if constexpr (n == 92) w_vmwait<(92 - D0) / DS + 1>();
+      if constexpr (n == 93) w_barrier();
+      if constexpr (n >= 94 && n < 126 && ((n - 94) & 1) == 0) {
+        constexpr int f = ((n - 94) >> 1) & 7;
+        if constexpr (n < 110) b0[f] = w_cat(w_tr(rdB[f]), w_tr(rdB[f] + 2048));
+        else a0[f] = w_cat(w_tr(rdA[f]), w_tr(rdA[f] + 2048));
+      }
+    });
+    buf ^= (uint32_t)W_IMG;
+    cur_next();
+  };
+  ktile(WI<1>{});
+  for (int kt = 1; kt < nk; ++kt) ktile(WI<0>{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  w_barrier();  // every wave is done with the K-tile buffers: the epilogue reuses them
+
+  // ---- epilogue: two halves of 64 rows per wave through a wave-private 32-KiB slice
+  // [64][128] fp32 (512-B rows, 16-B unit u of row r at u ^ (r & 7)); lane l holds row
+  // 16 i + (l & 15), columns 16 j + 4 (l >> 4) + 0..3
+  char* ep = smem + wave * 32768;
+  const int er = lane & 15, eq = lane >> 4;
+  float* Cz = g.C;
+  if constexpr (EPI == W_EPI_STORE) Cz += (int64_t)z * g.M * g.ldc;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = 4 * half + ii;
+      const int row = 16 * ii + er;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = 4 * j + eq;
+        *reinterpret_cast<f32x4*>(ep + row * 512 + ((u ^ (row & 7)) << 4)) = acc[i][j];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int col0 = n0 + wn * 128;
+#pragma unroll 4
+    for (int rr = 0; rr < 64; ++rr) {
+      const int grow = m0 + wm * 128 + 64 * half + rr;
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int c = 64 * c2 + lane;
+        const float val = *reinterpret_cast<const float*>(ep + rr * 512 + ((((c >> 2) ^ (rr & 7))) << 4) + (c & 3) * 4);
+        if (grow >= mlo && col0 + c >= nlo) {
+          if constexpr (EPI == W_EPI_STORE)
+            Cz[(int64_t)grow * g.ldc + col0 + c] = val;
+          else
+            atomicAdd(Cz + (int64_t)grow * g.ldc + col0 + c, val);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// C (fp32) [M, N] (+)= A^T B, A stored [K][M], B stored [K][N]; K split over `splits`.
+// epi: 1 = fp32 atomic add into C, 4 = split z stores its partial into C + z*M*ldc.
+// M, N >= 256, M % 8 == N % 8 == 0, K % 64 == 0, splits <= K / 64.
+NSA_API hipError_t nsa_gemm_wgrad4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M,
+                                   int N, int K, int splits, hipStream_t s) {
+  if ((epi != W_EPI_ATOMIC && epi != W_EPI_STORE) || M < W_BM || N < W_BN || M % 8 || N % 8 || K % W_BK ||
+      splits < 1 || splits > K / W_BK || lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N)
+    return hipErrorInvalidValue;
+  if ((int64_t)W_BK * lda * 2 + W_GRP >= (1ll << 31) || (int64_t)W_BK * ldb * 2 + W_GRP >= (1ll << 31))
+    return hipErrorInvalidValue;
+  Wg4Args a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (float*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.tiles_m = (M + W_BM - 1) / W_BM;
+  a.tiles_n = (N + W_BN - 1) / W_BN;
+  a.splits = splits;
+  const dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
+  if (epi == W_EPI_ATOMIC) wgrad4_kernel<W_EPI_ATOMIC><<<grid, W_THR, 0, s>>>(a);
+  else wgrad4_kernel<W_EPI_STORE><<<grid, W_THR, 0, s>>>(a);
+  return hipGetLastError();
+}

@@ -38,8 +38,16 @@ def supported(M, N, K) -> bool:
     return M % 8 == 0 and N % 8 == 0 and K % BK == 0 and M >= 8 and N >= 8
 
 
+WGRAD4 = 10  # variant id of the four-wave weight-grad kernel (csrc/kernels/gemm_wg4.hip)
+
+
 def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, variant=None):
-    epi = epi | ((VARIANT if variant is None else variant) << 8)
+    v = VARIANT if variant is None else variant
+    if v == WGRAD4 and M >= TILE and N >= TILE:
+        _lib.call("nsa_gemm_wgrad4", epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, M, N, K, splits,
+                  _lib.stream())
+        return
+    epi = epi | ((7 if v == WGRAD4 else v) << 8)
     _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, None, None,
               M, N, K, splits, _lib.stream())
 

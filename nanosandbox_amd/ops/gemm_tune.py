@@ -82,7 +82,7 @@ DETERMINISTIC = False
 NATIVE_MARGIN = float(os.environ.get("NSA_NATIVE_MARGIN", "0.03"))
 # weight-grad split counts that fill whole CU rounds as tuner candidates (NSA_WGRAD_FULL_ROUNDS=0: off)
 WGRAD_FULL_ROUNDS = os.environ.get("NSA_WGRAD_FULL_ROUNDS", "1") != "0"
-WGRAD_VARIANTS = (1, 7, 9)   # weight-grad (fp32 atomic epilogue) candidates: ring, ring64, phase
+WGRAD_VARIANTS = (1, 7, 9, 10)   # weight-grad (fp32 atomic epilogue) candidates: ring, ring64, phase, four-wave
 
 
 def _time_all(candidates: dict, rounds=3, reps=3):

@@ -56,7 +56,7 @@ def test_nt_input_grad_and_dgelu_epilogue(kernels, M, N, K):
                                           (2048, 768, 3072, 4), (1024, 50304, 768, 1),
                                           (1024, 768, 768, 3), (4096, 2304, 768, 28),  # uneven K splits
                                           (1024, 768, 768, 16)])  # one K-tile per split
-@pytest.mark.parametrize("variant", [1, 7, 9])
+@pytest.mark.parametrize("variant", [1, 7, 9, 10])
 def test_wgrad_acc(kernels, T, N, K, splits, variant):
     from nanosandbox_amd.ops import gemm
     if K % 8:
@@ -76,7 +76,7 @@ def test_wgrad_acc(kernels, T, N, K, splits, variant):
     assert torch.equal(g1, g2)
 
 
-@pytest.mark.parametrize("variant", [1, 7, 9])
+@pytest.mark.parametrize("variant", [1, 7, 9, 10])
 def test_asymmetric_identity(kernels, variant):
     """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
     from nanosandbox_amd.ops import gemm
