@@ -112,17 +112,32 @@ __device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& a, const bf16x8
 __device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
+#ifndef NSA_NT4_CRD
+#define NSA_NT4_CRD 0  // 1: fragment reads as compiler-visible LDS loads (hipcc places the lgkmcnt waits)
+#endif
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
+  if constexpr (NSA_NT4_CRD) {
+    d = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>((uintptr_t)(addr + OFF));
+  } else {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
+  }
 }
 // wait for every outstanding LDS read; the fragments it covers are named so the compiler
 // cannot touch them before the data has landed (cdna_hip_programming.md "What hipcc does not do")
 __device__ __forceinline__ void q_wait8(bf16x8 (&f)[8]) {
+  if constexpr (NSA_NT4_CRD) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return;
+  }
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]));
 }
 __device__ __forceinline__ void q_wait16(bf16x8 (&f)[8], bf16x8 (&h)[8]) {
+  if constexpr (NSA_NT4_CRD) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return;
+  }
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
                  "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]), "+v"(h[7]));
@@ -472,7 +487,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
       }
 #endif
-      if constexpr (n == 127) q_wait16(a0, b0);
+      if constexpr (n == 127 && !NSA_NT4_CRD) q_wait16(a0, b0);
     }, std::make_integer_sequence<int, 128>{});
     buf = nb;
     q_cur_next(g, c, nk, G);
