@@ -164,19 +164,34 @@ __device__ __forceinline__ bf16x8 tr_frag_w(const char* tile, int r0, int r1, in
 // neither sinks it towards a later use nor counts it in its own vmcnt bookkeeping).
 // glds16s: wave-uniform 64-bit base in SGPRs + a 32-bit per-lane byte offset (one VGPR
 // per address instead of two).
+// NSA_FA_M0KEEP=0 (default): M0 is written, not saved and restored — nothing else in these
+// kernels reads M0 (checked in the ISA: every m0 access is one of these statements), and
+// the save / restore pair cost two SALU per piece.
+#ifndef NSA_FA_M0KEEP
+#define NSA_FA_M0KEEP 0
+#endif
 __device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds_dst)
-               : "memory");
+  if constexpr (NSA_FA_M0KEEP) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds_dst)
+                 : "memory");
+  } else {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_dst)
+                 : "memory");
+  }
 }
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
+  if constexpr (NSA_FA_M0KEEP) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+  } else {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_dst) : "memory");
+  }
 }
 
 // =============================================================================
