@@ -11,21 +11,22 @@
 // fragments per 128 MFMAs: 128 KiB of reads per CU per K-tile, a third less.
 //
 // Schedule of one 64-deep K-tile (two 32-deep k-steps, 128 MFMAs per wave, one wave per
-// SIMD; the numbers are MFMA slots n = 0..127, k-step 0 = n < 64):
-//   n  0-14  read the A fragments of k-step 1 (8, current buffer)
-//   n 20/21  lgkmcnt(0), barrier 1: every wave is done with the buffer's A image
-//   n 22-50  LDS-DMA of K-tile t+2's A image into this buffer (8 pieces, one per 4 MFMAs),
-//            B fragments of k-step 1 read between them (n 23-37)
-//   n 56/57  lgkmcnt(0), barrier 2: the buffer's B image is free too
-//   n 58-74  LDS-DMA of K-tile t+2's B image, pieces 0-4
-//   n 90/91  vmcnt(13) + barrier 3: K-tile t+1 (issued one K-tile ago) has landed
-//   n 92-122 read K-tile t+1's k-step-0 fragments (16, other buffer); B pieces 5-7
-//   n 127    lgkmcnt(0) (form (ii): the wait names every fragment it covers)
-// so DMA has one whole K-tile (~2048 MFMA cycles) to land, two 64-KiB buffers suffice, and
-// no MFMA ever waits on LDS.  LDS-DMA is buffer_load_dwordx4 ... lds with the tile row
-// base in the buffer resource (advanced 128 B per K-tile), the piece's row offset in an
-// SGPR soffset and one per-lane VGPR offset (XOR swizzle of the 16-B chunk in the source
-// address, cdna_hip_programming.md rule 21): no VALU work per DMA.
+// SIMD; the numbers are MFMA slots n = 0..127, k-step 0 = n < 64; ER / DS / VMS / RS below):
+//   n  0-15   read the 16 k-step-1 fragments of this buffer, one per MFMA
+//   n 17/18   lgkmcnt(0) (the wait names every fragment), barrier: the buffer is free
+//   n 19-109  LDS-DMA of K-tile t+2 into this buffer, one 1-KiB piece per 6 MFMAs
+//   n 92/93   vmcnt(10) + barrier: K-tile t+1 (issued one K-tile ago) has landed
+//   n 94-124  read K-tile t+1's 16 k-step-0 fragments (other buffer), one per 2 MFMAs
+//   n 127     lgkmcnt(0)
+// so DMA has about one K-tile (~2048 MFMA cycles) to land, two 64-KiB buffers suffice, and
+// no MFMA waits on LDS.  LDS-DMA is buffer_load_dwordx4 ... lds with the tile row base in
+// the buffer resource (advanced 128 B per K-tile), the piece's row offset in an SGPR
+// soffset and one per-lane VGPR offset (XOR swizzle of the 16-B chunk in the source
+// address, cdna_hip_programming.md rule 21); four pieces share one M0 write through the
+// instruction offset: no VALU and one SALU per piece.  (Shaped after hipBLASLt's gfx950
+// MT256x256x64 solution for these layouts, read with llvm-objdump; measured alternatives
+// — three barriers per K-tile, M0 per piece, denser DMA, compiler-placed LDS waits, an
+// LDS-re-shaped epilogue, start-time staggering — are in docs/performance.md.)
 //
 // The MFMA's first operand is the A fragment, so a lane holds rows 4 (l >> 4) + e (e = 0..3)
 // of output column l & 15 of each 16x16 tile.  B rows are staged in a permuted order: image
@@ -48,35 +49,25 @@ constexpr int Q_THR = 256;
 constexpr int Q_IMG = Q_BM * Q_BK * 2;  // 32 KiB: one operand's [256][64] bf16 K-tile image
 constexpr int Q_BUF = 2 * Q_IMG;        // A image, then B image
 constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
-#ifndef NSA_NT4_STAG
-#define NSA_NT4_STAG 1  // start-time stagger phases: workgroup v starts (v % STAG) / STAG of a tile late
-#endif
 
-#ifndef NSA_NT4_SCHED
-#define NSA_NT4_SCHED 1  // 0: three barriers per K-tile (header); 1: two barriers, evenly spread DMA
-#endif
 #ifndef NSA_NT4_DS
-#define NSA_NT4_DS 6  // SCHED 1: MFMAs between LDS-DMA pieces
+#define NSA_NT4_DS 6  // MFMAs between LDS-DMA pieces
 #endif
 #ifndef NSA_NT4_VMS
-#define NSA_NT4_VMS 92  // SCHED 1: slot of the wait for the previous K-tile's pieces
+#define NSA_NT4_VMS 92  // slot of the wait for the previous K-tile's pieces
 #endif
 #ifndef NSA_NT4_ER
-#define NSA_NT4_ER 1  // SCHED 1: MFMAs between the k-step-1 fragment reads at the K-tile head
+#define NSA_NT4_ER 1  // MFMAs between the k-step-1 fragment reads at the K-tile head
 #endif
 #ifndef NSA_NT4_RS
-#define NSA_NT4_RS 2  // SCHED 1: MFMAs between the next K-tile's fragment reads
+#define NSA_NT4_RS 2  // MFMAs between the next K-tile's fragment reads
 #endif
 
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2 };
 
 // pieces a K-tile has issued when it waits for the previous K-tile's
-#if NSA_NT4_SCHED == 0
-constexpr int Q_ISS = 13;
-#else
 constexpr int Q_D0 = 15 * NSA_NT4_ER + 4;  // slot of the first piece
 constexpr int Q_ISS = (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 : 16;
-#endif
 // vector-memory operations of one wave's epilogue of a full tile (stores, and the U loads)
 template <int EPI>
 constexpr int q_epi_vm() {
@@ -112,32 +103,13 @@ __device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& a, const bf16x8
 __device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
-#ifndef NSA_NT4_CRD
-#define NSA_NT4_CRD 0  // 1: fragment reads as compiler-visible LDS loads (hipcc places the lgkmcnt waits)
-#endif
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
-  if constexpr (NSA_NT4_CRD) {
-    d = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>((uintptr_t)(addr + OFF));
-  } else {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
-  }
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(OFF));
 }
 // wait for every outstanding LDS read; the fragments it covers are named so the compiler
 // cannot touch them before the data has landed (cdna_hip_programming.md "What hipcc does not do")
-__device__ __forceinline__ void q_wait8(bf16x8 (&f)[8]) {
-  if constexpr (NSA_NT4_CRD) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    return;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]));
-}
 __device__ __forceinline__ void q_wait16(bf16x8 (&f)[8], bf16x8 (&h)[8]) {
-  if constexpr (NSA_NT4_CRD) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    return;
-  }
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]),
                  "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]), "+v"(h[5]), "+v"(h[6]), "+v"(h[7]));
@@ -385,12 +357,6 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     q_dma<(p & 3) * 1024>(dmaB0 + buf + (uint32_t)((p & 4) * 1024), voB[p & 1], c.rb, soB[p]);
   };
 
-  if constexpr (NSA_NT4_STAG > 1) {
-    // de-synchronise the epilogues: with every CU storing its 128-KiB tile at the same moment
-    // the stores queue on HBM; started (v % STAG) / STAG of a tile apart they do not
-    const int units = (v % NSA_NT4_STAG) * nk * 32 / NSA_NT4_STAG;  // ~2048 cycles per K-tile, 64 per unit
-    for (int u = 0; u < units; u += 16) __builtin_amdgcn_s_sleep(16);
-  }
   // ---- prologue: K-tiles 0 and 1 of this workgroup's sequence into buffers 0 / 1
   QCur c;
   q_cur_tile(g, c, v);
@@ -429,36 +395,6 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       } else {
         q_mfma(acc[i][j], a1[i], b1[j]);
       }
-#if NSA_NT4_SCHED == 0
-      // k-step 1 A fragments (this buffer)
-      if constexpr (n < 16 && (n & 1) == 0) q_rd<(n >> 1) * 2048>(a1[n >> 1], rA[1] + buf);
-      if constexpr (n == 20) q_wait8(a1);
-      if constexpr (n == 21) q_barrier();
-      // K-tile t+2's A image into this buffer, k-step 1 B fragments between the pieces
-      if constexpr (n >= 22 && n <= 50 && ((n - 22) & 3) == 0) {
-        if constexpr (dv) issue_a(c, buf, QI<((n - 22) >> 2)>{});
-      }
-      if constexpr (n >= 23 && n <= 37 && ((n - 23) & 1) == 0) q_rd<(n - 23) / 2 * 2048>(b1[(n - 23) / 2], rB[1] + buf);
-      if constexpr (n == 56) q_wait8(b1);
-      if constexpr (n == 57) q_barrier();
-      if constexpr (n >= 58 && n <= 74 && ((n - 58) & 3) == 0) {
-        if constexpr (dv) issue_b(c, buf, QI<((n - 58) >> 2)>{});
-      }
-      // K-tile t+1 has landed (its 16 pieces are older than this K-tile's 13)
-      if constexpr (n == 90) {
-        q_vmw<dv ? 13 : 0, EPI>(FIRST && pend);
-      }
-      if constexpr (n == 91) q_barrier();
-      // its k-step 0 fragments (other buffer): B 0..7, then A 0..7
-      if constexpr (n >= 92 && n <= 122 && (n & 1) == 0) {
-        constexpr int s = (n - 92) >> 1;
-        if constexpr (s < 8) q_rd<s * 2048>(b0[s], rB[0] + nb);
-        else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
-      }
-      if constexpr (n == 97 || n == 105 || n == 113) {
-        if constexpr (dv) issue_b(c, buf, QI<(5 + (n - 97) / 8)>{});
-      }
-#else
       // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
       // K-tile t+2 spread one per DS MFMAs, then K-tile t+1's k-step-0 fragments
       constexpr int ER = NSA_NT4_ER;  // MFMAs between the k-step-1 fragment reads
@@ -486,8 +422,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         if constexpr (s < 8) q_rd<s * 2048>(b0[s], rB[0] + nb);
         else q_rd<(s - 8) * 2048>(a0[s - 8], rA[0] + nb);
       }
-#endif
-      if constexpr (n == 127 && !NSA_NT4_CRD) q_wait16(a0, b0);
+      if constexpr (n == 127) q_wait16(a0, b0);
     }, std::make_integer_sequence<int, 128>{});
     buf = nb;
     q_cur_next(g, c, nk, G);
