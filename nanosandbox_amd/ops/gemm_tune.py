@@ -134,7 +134,8 @@ def choose(key, candidates: dict, fixed: str | None = None) -> str:
             # no timing race: a fixed rule, identical in every run: the native
             # candidate (or the caller's ``fixed`` pick), else the first one
             best = fixed if fixed in candidates else next(
-                (n for n in candidates if n.startswith("nt") or n.startswith("det")), next(iter(candidates)))
+                (n for n in candidates if n.startswith("nt4")),
+                next((n for n in candidates if n.startswith("nt") or n.startswith("det")), next(iter(candidates))))
         else:
             best = _pick_timed(candidates)
         best = _agree(best)
