@@ -3,7 +3,7 @@
 //
 //   C[M,N] (+)= A[K,M]^T · B[K,N]   A = dY [tokens][out] (lda), B = X [tokens][in] (ldb),
 //                                   C fp32 [out][in] (the flat gradient), K = tokens,
-//                                   split over blockIdx.z (split z owns K-tiles
+//                                   split S ways (split z owns K-tiles
 //                                   [z n / S, (z+1) n / S), any split count)
 //
 // Per workgroup one 256x256 output tile, 4 waves of 128x128 (8x8 accumulators of
@@ -124,19 +124,22 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
 
-  // tile: blocks b, b+8, ... share an XCD; consecutive blocks of an XCD walk neighbouring
-  // tiles (row-major over the tile grid), the split index is blockIdx.z
+  // work item u = (split z, tile v), one block each on a 1-D grid.  Blocks b, b+8, ... share
+  // an XCD; the remap gives an XCD consecutive items u, i.e. every tile of one or a few
+  // splits, so the token slices of dY and X that those tiles share are read from HBM once
+  // and then hit in that XCD's L2 (the 768 x 768 dW, 9 tiles x 28 splits: 3x less HBM).
   const int tiles = g.tiles_m * g.tiles_n;
-  int v = blockIdx.x;
+  int u = blockIdx.x;
   {
-    const int G = gridDim.x, x = v % 8, qq = G / 8, rr = G % 8;
-    v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + v / 8;
+    const int G = gridDim.x, x = u % 8, qq = G / 8, rr = G % 8;
+    u = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + u / 8;
   }
-  if (v >= tiles) return;
+  if (u >= tiles * g.splits) return;
+  const int v = u % tiles, z = u / tiles;
   const int tm = v / g.tiles_n, tn = v % g.tiles_n;
   const int mlo = tm * W_BM, nlo = tn * W_BN;
   const int m0 = min(mlo, g.M - W_BM), n0 = min(nlo, g.N - W_BN);
-  const int nkt = g.K / W_BK, z = blockIdx.z;
+  const int nkt = g.K / W_BK;
   const int kt0 = (int)((int64_t)z * nkt / g.splits), kt1 = (int)((int64_t)(z + 1) * nkt / g.splits);
   const int nk = kt1 - kt0;
 
@@ -293,8 +296,12 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const int col0 = n0 + wn * 128;
+    // the K-splits of one tile add into the same rows: each split walks them from its own
+    // starting row, so concurrent atomics of different splits hit different lines
+    const int rot = (z * 23) & 63;
 #pragma unroll 4
-    for (int rr = 0; rr < 64; ++rr) {
+    for (int r2 = 0; r2 < 64; ++r2) {
+      const int rr = (r2 + rot) & 63;
       const int grow = m0 + wm * 128 + 64 * half + rr;
 #pragma unroll
       for (int c2 = 0; c2 < 2; ++c2) {
@@ -336,7 +343,7 @@ NSA_API hipError_t nsa_gemm_wgrad4(int epi, const void* A, int lda, const void* 
   a.tiles_m = (M + W_BM - 1) / W_BM;
   a.tiles_n = (N + W_BN - 1) / W_BN;
   a.splits = splits;
-  const dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
+  const dim3 grid(a.tiles_m * a.tiles_n * splits);
   if (epi == W_EPI_ATOMIC) wgrad4_kernel<W_EPI_ATOMIC><<<grid, W_THR, 0, s>>>(a);
   else wgrad4_kernel<W_EPI_STORE><<<grid, W_THR, 0, s>>>(a);
   return hipGetLastError();
