@@ -142,6 +142,19 @@ __device__ __forceinline__ void q_dma(uint32_t lds, uint32_t voff, q_i32x4 rsrc,
   }
 }
 
+#ifndef NSA_NT4_GLDS
+#define NSA_NT4_GLDS 1  // 1: global_load_lds_dwordx4 (SGPR base + per-piece VGPR offset) instead of buffer_load ... lds
+#endif
+template <int OFF>
+__device__ __forceinline__ void q_dmag(uint32_t lds, uint32_t voff, const void* sbase) {
+  if constexpr (OFF == 0) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(voff), "s"(sbase)
+                 : "memory");
+  } else {
+    asm volatile("global_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(voff), "s"(sbase), "n"(OFF) : "memory");
+  }
+}
+
 __device__ __forceinline__ void q_tile_coords(const Nt4Args& g, int seq, int& m0, int& n0, int& mlo, int& nlo) {
   const int per = g.gm * g.tiles_n;
   const int grp = seq / per;
@@ -189,8 +202,9 @@ __device__ __forceinline__ void q_cur_tile(const Nt4Args& g, QCur& c, int seq) {
     // past the last tile the slots still issue their pieces (no branches in the K-tile
     // body, vmcnt counts stay fixed): an empty range makes every load out of bounds, so
     // nothing is fetched and the never-read buffer receives zeros
-    c.ra = q_rsrc(g.A, 0);
-    c.rb = q_rsrc(g.B, 0);
+    // (GLDS: no range check, so the base stays a real tile-0 address, lowered like the rest)
+    c.ra = q_rsrc(reinterpret_cast<const char*>(g.A) - Q_GRP, 0);
+    c.rb = q_rsrc(reinterpret_cast<const char*>(g.B) - Q_GRP, 0);
   }
 }
 __device__ __forceinline__ void q_add_base(q_i32x4& r, int bytes) {
@@ -348,13 +362,31 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   }
 
   // piece P of K-tile cursor c into buffer buf (the pieces of an M0 group are issued in order)
+  // GLDS: per-piece VGPR offsets (row offset folded in), the tile base as an SGPR pair
+  uint32_t vpA[NSA_NT4_GLDS ? 8 : 1], vpB[NSA_NT4_GLDS ? 8 : 1];
+  if constexpr (NSA_NT4_GLDS) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      vpA[p] = voA[p & 1] + soA[p];
+      vpB[p] = voB[p & 1] + soB[p];
+    }
+  }
+  auto sbase = [](const q_i32x4& r) {
+    return reinterpret_cast<const void*>(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x);
+  };
   auto issue_a = [&](const QCur& c, uint32_t buf, auto P) {
     constexpr int p = decltype(P)::value;
-    q_dma<(p & 3) * 1024>(dmaA0 + buf + (uint32_t)((p & 4) * 1024), voA[p & 1], c.ra, soA[p]);
+    if constexpr (NSA_NT4_GLDS)
+      q_dmag<(p & 3) * 1024>(dmaA0 + buf + (uint32_t)((p & 4) * 1024), vpA[p], sbase(c.ra));
+    else
+      q_dma<(p & 3) * 1024>(dmaA0 + buf + (uint32_t)((p & 4) * 1024), voA[p & 1], c.ra, soA[p]);
   };
   auto issue_b = [&](const QCur& c, uint32_t buf, auto P) {
     constexpr int p = decltype(P)::value;
-    q_dma<(p & 3) * 1024>(dmaB0 + buf + (uint32_t)((p & 4) * 1024), voB[p & 1], c.rb, soB[p]);
+    if constexpr (NSA_NT4_GLDS)
+      q_dmag<(p & 3) * 1024>(dmaB0 + buf + (uint32_t)((p & 4) * 1024), vpB[p], sbase(c.rb));
+    else
+      q_dma<(p & 3) * 1024>(dmaB0 + buf + (uint32_t)((p & 4) * 1024), voB[p & 1], c.rb, soB[p]);
   };
 
   // ---- prologue: K-tiles 0 and 1 of this workgroup's sequence into buffers 0 / 1
