@@ -87,6 +87,18 @@ __device__ __forceinline__ void w_dma(uint32_t lds, uint32_t voff, w_i32x4 rsrc,
                  : "memory");
   }
 }
+#ifndef NSA_WG4_GLDS
+#define NSA_WG4_GLDS 0  // 1: global_load_lds_dwordx4 with an SGPR base + per-piece VGPR offsets (measured 1-3 % slower here)
+#endif
+template <int OFF>
+__device__ __forceinline__ void w_dmag(uint32_t lds, uint32_t voff, const void* sbase) {
+  if constexpr (OFF == 0) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(voff), "s"(sbase)
+                 : "memory");
+  } else {
+    asm volatile("global_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(voff), "s"(sbase), "n"(OFF) : "memory");
+  }
+}
 __device__ __forceinline__ w_i32x4 w_rsrc(const void* base, uint32_t bytes) {
   const uint64_t b = (uint64_t)(uintptr_t)base;
   w_i32x4 r;
@@ -173,20 +185,39 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
   int kd = 0;  // K-tile index (within the split) of the cursor
   auto cur_next = [&]() {
     if (++kd >= nk) {
-      ra.z = 0;  // past the split's last K-tile: empty range, every piece loads nothing
+      // past the split's last K-tile: buffer_load gets an empty range (loads nothing); the
+      // global_load_lds form re-reads the split's last K-tile into a buffer nobody reads
+      ra.z = 0;
       rb.z = 0;
     } else {
       w_add_base(ra, stepA);
       w_add_base(rb, stepB);
     }
   };
+  uint32_t vpA[NSA_WG4_GLDS ? 8 : 1], vpB[NSA_WG4_GLDS ? 8 : 1];
+  if constexpr (NSA_WG4_GLDS) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      vpA[p] = voA[(p & 1) | ((p >> 2) << 1)] + soA[p];
+      vpB[p] = voB[(p & 1) | ((p >> 2) << 1)] + soB[p];
+    }
+  }
+  auto sbase = [](const w_i32x4& r) {
+    return reinterpret_cast<const void*>(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x);
+  };
   auto issue_a = [&](uint32_t buf, auto P) {
     constexpr int p = decltype(P)::value;
-    w_dma<(p & 3) * 1024>(dmaA + buf + (uint32_t)((p & 4) * 1024), voA[(p & 1) | ((p >> 2) << 1)], ra, soA[p]);
+    if constexpr (NSA_WG4_GLDS)
+      w_dmag<(p & 3) * 1024>(dmaA + buf + (uint32_t)((p & 4) * 1024), vpA[p], sbase(ra));
+    else
+      w_dma<(p & 3) * 1024>(dmaA + buf + (uint32_t)((p & 4) * 1024), voA[(p & 1) | ((p >> 2) << 1)], ra, soA[p]);
   };
   auto issue_b = [&](uint32_t buf, auto P) {
     constexpr int p = decltype(P)::value;
-    w_dma<(p & 3) * 1024>(dmaB + buf + (uint32_t)((p & 4) * 1024), voB[(p & 1) | ((p >> 2) << 1)], rb, soB[p]);
+    if constexpr (NSA_WG4_GLDS)
+      w_dmag<(p & 3) * 1024>(dmaB + buf + (uint32_t)((p & 4) * 1024), vpB[p], sbase(rb));
+    else
+      w_dma<(p & 3) * 1024>(dmaB + buf + (uint32_t)((p & 4) * 1024), voB[(p & 1) | ((p >> 2) << 1)], rb, soB[p]);
   };
 
   // ---- fragment read addresses (buffer 0, k-step 0, first half): fragment f covers columns
