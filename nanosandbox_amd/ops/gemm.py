@@ -107,14 +107,16 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0, w4=Fal
     return out
 
 
+# the fixed-kernel entry points below use the four-wave kernel (faster on every GPT-2 shape,
+# docs/performance.md); the tuner (ops/gemm_tune.py) still races both against hipBLASLt
 def fwd(x2, w):
     """Y = X · W^T (nn.Linear forward, bf16)."""
-    return nt(x2, w)
+    return nt(x2, w, w4=True)
 
 
 def fwd_gelu(x2, w):
     """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
-    return nt(x2, w, epi=NT_EPI_GELU)
+    return nt(x2, w, epi=NT_EPI_GELU, w4=True)
 
 
 def dgrad(dy2, w, u=None, wt=None):
@@ -122,8 +124,8 @@ def dgrad(dy2, w, u=None, wt=None):
     with ``u`` also multiplied by gelu'(u)."""
     wt = w.t().contiguous() if wt is None else wt
     if u is None:
-        return nt(dy2, wt)
-    return nt(dy2, wt, epi=NT_EPI_DGELU, u=u)
+        return nt(dy2, wt, w4=True)
+    return nt(dy2, wt, epi=NT_EPI_DGELU, u=u, w4=True)
 
 
 def wgrad_splits(n_out, n_in, tokens, cus=256):

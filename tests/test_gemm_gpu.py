@@ -17,8 +17,10 @@ def rel(a, b):
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
                                    (256, 256, 3072), (1000, 1288, 640), (4096, 768, 4608)])
 def test_nt_forward_and_gelu_epilogue(kernels, M, N, K):
-    """Persistent NT kernel (gemm_nt.hip) vs fp32 torch: plain, GELU epilogue, ragged M/N
-    (tail tiles shifted back inside the matrix), several tiles per workgroup."""
+    """Persistent NT kernels vs fp32 torch (gemm.fwd / fwd_gelu run the four-wave kernel):
+    plain, GELU epilogue, ragged M/N (tail tiles shifted back inside the matrix), several
+    tiles per workgroup; the eight-wave kernel (gemm_nt.hip) with either store policy gives
+    bitwise the same output (same accumulation order)."""
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV).to(BF)
