@@ -235,6 +235,13 @@ __device__ __forceinline__ void q_vmw(bool after_epi) {
   else q_vmwait<ISS>();
 }
 
+// two f32 -> one dword of two bf16 (one v_cvt_pk_bf16_f32, RNE)
+typedef __bf16 q_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float q_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t q_pk(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((q_f32x2){a, b}, q_bf16x2));
+}
+
 template <bool NT>
 __device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   if constexpr (NT) {
@@ -247,7 +254,7 @@ __device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32
 // Epilogue straight from the accumulators: for fragment row i and element e, lane l holds
 // row 16 i + 4 (l >> 4) + e of the wave's 128 rows, columns 8 (l & 15) + 0..7 (fragments
 // j = 0..7), so the 16 lanes of a quarter-wave write one row's 256 contiguous bytes.
-template <int EPI, bool NT>
+template <int EPI, bool NT, bool NOSTORE = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
                                            int lane) {
   int m0, n0, mlo, nlo;
@@ -268,35 +275,44 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
     load_u(0, uv[0]);
     load_u(1, uv[1]);
   }
+  // one base pointer per lane; a store's row offset (16 i + e) rows is wave-uniform
+  const int row0 = m0 + wm * 128 + 4 * q;
+  bf16_t* const cb = g.C + (int64_t)row0 * g.ldc + col;
+  bf16_t* const cb2 = EPI == Q_EPI_GELU ? g.C2 + (int64_t)row0 * g.ldc + col : nullptr;
+  {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = m0 + wm * 128 + 16 * i + 4 * q + e;
-      if (!full && (row < mlo || col < nlo)) continue;
-      uint32_t w[4] = {pack2(acc[i][0][e], acc[i][1][e]), pack2(acc[i][2][e], acc[i][3][e]),
-                       pack2(acc[i][4][e], acc[i][5][e]), pack2(acc[i][6][e], acc[i][7][e])};
-      if constexpr (EPI == Q_EPI_DGELU) {
+      for (int e = 0; e < 4; ++e) {
+        if (!full && (row0 + 16 * i + e < mlo || col < nlo)) continue;
+        uint32_t w[4] = {q_pk(acc[i][0][e], acc[i][1][e]), q_pk(acc[i][2][e], acc[i][3][e]),
+                         q_pk(acc[i][4][e], acc[i][5][e]), q_pk(acc[i][6][e], acc[i][7][e])};
+        if constexpr (EPI == Q_EPI_DGELU) {
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const uint32_t u = uv[i & 1][e][h];
-          const float a0 = __uint_as_float(w[h] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
-          const float a1 = __uint_as_float(w[h] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
-          w[h] = pack2(a0, a1);
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t u = uv[i & 1][e][h];
+            const float a0 = __uint_as_float(w[h] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
+            const float a1 = __uint_as_float(w[h] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
+            w[h] = q_pk(a0, a1);
+          }
+        }
+        const int64_t off = (int64_t)(16 * i + e) * g.ldc;
+        if constexpr (NOSTORE) {
+          asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        } else {
+          q_st16<NT>(cb + off, w[0], w[1], w[2], w[3]);
+        }
+        if constexpr (EPI == Q_EPI_GELU) {
+          uint32_t gg[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            gg[h] = q_pk(nsa_gelu(__uint_as_float(w[h] << 16)), nsa_gelu(__uint_as_float(w[h] & 0xffff0000u)));
+          q_st16<NT>(cb2 + off, gg[0], gg[1], gg[2], gg[3]);
         }
       }
-      const int64_t off = (int64_t)row * g.ldc + col;
-      q_st16<NT>(g.C + off, w[0], w[1], w[2], w[3]);
-      if constexpr (EPI == Q_EPI_GELU) {
-        uint32_t gg[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-          gg[h] = pack2(nsa_gelu(__uint_as_float(w[h] << 16)), nsa_gelu(__uint_as_float(w[h] & 0xffff0000u)));
-        q_st16<NT>(g.C2 + off, gg[0], gg[1], gg[2], gg[3]);
+      if constexpr (EPI == Q_EPI_DGELU) {
+        if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
       }
-    }
-    if constexpr (EPI == Q_EPI_DGELU) {
-      if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
     }
   }
 }
@@ -304,7 +320,8 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 }  // namespace
 
 // PROBE (timing only, wrong results): 1 = no DMA after the prologue, 2 = no wait for the
-// previous K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue stores
+// previous K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue at all,
+// 5 = epilogue arithmetic without its stores
 template <int EPI, bool NT, int PROBE>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   __shared__ __attribute__((aligned(16))) char smem[Q_SMEM];
@@ -465,7 +482,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT>(g, acc, seq, wm, wn, lane);
+      q_epilogue<EPI, NT, PROBE == 5>(g, acc, seq, wm, wn, lane);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -528,6 +545,7 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   else if (probe == 2) gemm_nt4_kernel<E, true, 2><<<gr, Q_THR, 0, s>>>(a);  \
   else if (probe == 3) gemm_nt4_kernel<E, true, 3><<<gr, Q_THR, 0, s>>>(a);  \
   else if (probe == 4) gemm_nt4_kernel<E, true, 4><<<gr, Q_THR, 0, s>>>(a);  \
+  else if (probe == 5) gemm_nt4_kernel<E, true, 5><<<gr, Q_THR, 0, s>>>(a);  \
   else if (nt) gemm_nt4_kernel<E, true, 0><<<gr, Q_THR, 0, s>>>(a);          \
   else gemm_nt4_kernel<E, false, 0><<<gr, Q_THR, 0, s>>>(a);
   switch (epi) {

@@ -142,7 +142,7 @@ def main():
         if a.probe:
             for pr, nm in ((1, "nodma"), (4, "nostore")):
                 cands[f"nt_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr)
-            for pr, nm in ((1, "nodma"), (2, "novmwait"), (3, "nobarrier"), (4, "nostore")):
+            for pr, nm in ((1, "nodma"), (2, "novmwait"), (3, "nobarrier"), (4, "noepi"), (5, "nostore")):
                 cands[f"nt4_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr, w4=True)
         if a.epi and name in ("c_fc", "mlp.c_proj.dx"):
             if name == "c_fc":
