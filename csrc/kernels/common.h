@@ -163,6 +163,35 @@ __device__ __forceinline__ float nsa_gelu_grad(float x) {
   return c + x * p;
 }
 
+// The same GELU on two values at once: the non-transcendental arithmetic as packed-f32
+// VALU (v_pk_fma_f32 / v_pk_mul_f32, two lanes' worth per instruction), v_rcp_f32 and
+// v_exp_f32 per element.  For the GEMM epilogues, where one wave per SIMD runs the GELU of
+// a 256 x 256 tile with no MFMA beside it.
+typedef float nsa_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void nsa_gelu_cdf_pdf2(nsa_f32x2 x, nsa_f32x2& cdf, nsa_f32x2& pdf) {
+  const nsa_f32x2 z = nsa_f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const nsa_f32x2 d = 1.0f + 0.3275911f * z;
+  const nsa_f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const nsa_f32x2 poly =
+      t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const nsa_f32x2 y = z * z * -1.4426950408889634f;  // exp(-z^2) = 2^(-z^2 log2 e)
+  const nsa_f32x2 e = {__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+  const nsa_f32x2 erf_abs = 1.0f - poly * e;
+  const nsa_f32x2 erf_z = {__builtin_copysignf(erf_abs.x, x.x), __builtin_copysignf(erf_abs.y, x.y)};
+  cdf = 0.5f + 0.5f * erf_z;
+  pdf = e * 0.39894228040143268f;
+}
+__device__ __forceinline__ nsa_f32x2 nsa_gelu2(nsa_f32x2 x) {
+  nsa_f32x2 c, p;
+  nsa_gelu_cdf_pdf2(x, c, p);
+  return x * c;
+}
+__device__ __forceinline__ nsa_f32x2 nsa_gelu_grad2(nsa_f32x2 x) {
+  nsa_f32x2 c, p;
+  nsa_gelu_cdf_pdf2(x, c, p);
+  return c + x * p;
+}
+
 // Nontemporal streams only pay for tensors larger than the 256 MB Infinity Cache: a smaller
 // one can stay cache-resident for its next reader (shakespeare_char config, 25 MB LayerNorm
 // rows: 4.78 ms/iter with nontemporal streams everywhere, 4.72-4.76 gated).  Streams of at

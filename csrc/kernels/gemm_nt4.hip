@@ -291,9 +291,9 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             const uint32_t u = uv[i & 1][e][h];
-            const float a0 = __uint_as_float(w[h] << 16) * nsa_gelu_grad(__uint_as_float(u << 16));
-            const float a1 = __uint_as_float(w[h] & 0xffff0000u) * nsa_gelu_grad(__uint_as_float(u & 0xffff0000u));
-            w[h] = q_pk(a0, a1);
+            const nsa_f32x2 a = nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)} *
+                                nsa_gelu_grad2(nsa_f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)});
+            w[h] = q_pk(a.x, a.y);
           }
         }
         const int64_t off = (int64_t)(16 * i + e) * g.ldc;
@@ -305,8 +305,10 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
         if constexpr (EPI == Q_EPI_GELU) {
           uint32_t gg[4];
 #pragma unroll
-          for (int h = 0; h < 4; ++h)
-            gg[h] = q_pk(nsa_gelu(__uint_as_float(w[h] << 16)), nsa_gelu(__uint_as_float(w[h] & 0xffff0000u)));
+          for (int h = 0; h < 4; ++h) {
+            const nsa_f32x2 gv = nsa_gelu2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)});
+            gg[h] = q_pk(gv.x, gv.y);
+          }
           q_st16<NT>(cb2 + off, gg[0], gg[1], gg[2], gg[3]);
         }
       }
