@@ -83,6 +83,10 @@ NATIVE_MARGIN = float(os.environ.get("NSA_NATIVE_MARGIN", "0.03"))
 # weight-grad split counts that fill whole CU rounds as tuner candidates (NSA_WGRAD_FULL_ROUNDS=0: off)
 WGRAD_FULL_ROUNDS = os.environ.get("NSA_WGRAD_FULL_ROUNDS", "1") != "0"
 WGRAD_VARIANTS = (1, 7, 9, 10)   # weight-grad (fp32 atomic epilogue) candidates: ring, ring64, phase, four-wave
+# four-wave weight grads with stored split partials + an ordered reduce pass as candidates
+# beside the atomic epilogue (NSA_WGRAD_STORE=1: on; off by default -- the tuner picks them
+# for c_attn / c_fc dW by 2-3 %, but the step time does not move, docs/performance.md)
+WGRAD_STORE_CANDS = os.environ.get("NSA_WGRAD_STORE", "0") != "0"
 
 
 def _time_all(candidates: dict, rounds=3, reps=3):
@@ -436,10 +440,19 @@ def wgrad_acc(dy2, x2, g32):
     for sb in sorted(x for x in extra if 1 <= x <= max(1, T // _gemm.BK) and x != sdef):
         cands.update({f"nsa{v}/s{sb}": cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v))
                       for v in WGRAD_VARIANTS})
+    # the four-wave kernel with its splits' partials stored (plain stores) and added in one
+    # ordered pass instead of fp32 atomics: every work item of a many-split shape (the
+    # 768 x 768 dW: 9 tiles x 28 splits) ends in the same instant, where the atomics queue
+    if WGRAD_STORE_CANDS and WGRAD_VARIANTS[-1] == _gemm.WGRAD4:
+        v = _gemm.WGRAD4
+        for sb in sorted(x for x in extra | {sdef} if 2 <= x <= max(1, T // _gemm.BK)):
+            cands[f"det{v}/s{sb}"] = cand(lambda a, b, c, v=v, sb=sb: _gemm.wgrad_acc(a, b, c, splits=sb, variant=v,
+                                                                                     deterministic=True))
     name = choose(("wgrad", T, N, K), cands)
     if name == "hipblaslt":
         _hip_wgrad(dy2, x2, g32)
     elif name == "hipblaslt_bf16":
         _hip_wgrad_bf16(dy2, x2, g32)
     else:
-        _gemm.wgrad_acc(dy2, x2, g32, splits=_splits(name), variant=_variant(name))
+        _gemm.wgrad_acc(dy2, x2, g32, splits=_splits(name), variant=_variant(name),
+                        deterministic=name.startswith("det"))
