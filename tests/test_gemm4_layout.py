@@ -158,3 +158,22 @@ def test_wg4_epilogue_reshape_conflict_free():
             c = 64 * c2 + lane
             addrs.append(rr * 512 + (((c >> 2) ^ (rr & 7)) << 4) + (c & 3) * 4)
         assert worst_degree(addrs, HALVES, 4, nbanks=32) == 1
+
+
+# -------------------------------------------------------- persistent tile walk (nt4)
+def nt4_tile_coords(seq, tiles_m, tiles_n, gm):
+    """q_tile_coords: groups of gm row blocks x every column, column-major inside a group."""
+    per = gm * tiles_n
+    grp = seq // per
+    first = grp * gm
+    g = min(gm, tiles_m - first)
+    inn = seq - grp * per
+    return first + inn % g, inn // g
+
+
+def test_nt4_tile_walk_is_a_bijection():
+    # the default group sizes (4 for N <= 1024, 1 up to 4096, 8 beyond) and partial last groups
+    for tiles_m, tiles_n in ((480, 3), (480, 9), (480, 12), (480, 197), (7, 3), (13, 5), (1, 1), (9, 197)):
+        for gm in (1, 2, 4, 8, 16):
+            seen = {nt4_tile_coords(s, tiles_m, tiles_n, gm) for s in range(tiles_m * tiles_n)}
+            assert seen == {(m, n) for m in range(tiles_m) for n in range(tiles_n)}, (tiles_m, tiles_n, gm)
