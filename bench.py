@@ -51,6 +51,17 @@ def batch_plan(world: int, micro_batch: int = 0) -> tuple[int, int]:
     return micro_batch, per_rank_seqs // micro_batch * world
 
 
+def rccl_summary(report, sweep) -> dict | None:
+    """The JSON record's RCCL block (None on one GPU)."""
+    if not report and not sweep:
+        return None
+    report = report or {}
+    return {"backend": report.get("backend"), "preset": report.get("preset"),
+            "transport_by_rank": {str(k): v for k, v in (report.get("transport") or {}).items()},
+            "allreduce_64MiB_ms": report.get("allreduce_ms"), "allreduce_64MiB_busbw_GBps": report.get("busbw_GBps"),
+            "sweep": list(sweep or [])}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,7 +72,10 @@ def main():
                          "batch (480/N sequences) that is <= 120 (uses MI355X's 288 GB instead of "
                          "nanoGPT's A100-sized 12; the 491,520-token global batch is unchanged)")
     ap.add_argument("--block-size", type=int, default=1024)
-    ap.add_argument("--model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl"])
+    ap.add_argument("--model", default="gpt2", choices=["gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl", "tiny"],
+                    help="tiny (2 x 64): plumbing tests of the multi-rank path only, not a benchmark")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo rehearsal of the N > 1 path (tests/test_bench_plan.py), not a benchmark")
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--grad-ckpt", action="store_true")
@@ -92,8 +106,14 @@ def main():
     from nanosandbox_amd.train import Trainer
 
     dims = {"gpt2": (12, 12, 768), "gpt2-medium": (24, 16, 1024), "gpt2-large": (36, 20, 1280),
-            "gpt2-xl": (48, 25, 1600)}[args.model]
-    if args.micro_batch <= 0 and not args.grad_ckpt:
+            "gpt2-xl": (48, 25, 1600), "tiny": (2, 2, 64)}[args.model]
+    cuda = args.device == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    if args.micro_batch <= 0 and not args.grad_ckpt and cuda:
         # HBM-sized micro-batch: the largest divisor of the per-rank batch whose activations
         # stay resident next to the model state (utils/memory.py); 120 for GPT-2 124M / 350M
         from nanosandbox_amd.utils.memory import choose_micro_batch
@@ -115,7 +135,8 @@ def main():
             dataset = args.real_data
     cfg.update(dataset=dataset, data_dir=data_dir, batch_size=args.micro_batch, block_size=args.block_size,
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
-               dropout=0.0, bias=False, compile=False, device="cuda", dtype="bfloat16", backend="nccl",
+               dropout=0.0, bias=False, compile=False, device=args.device, dtype="bfloat16",
+               backend="nccl" if cuda else "gloo",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
                fp32_residual=not args.bf16_residual, deterministic=args.deterministic,
                out_dir="/tmp/nsa_bench_out", metrics_jsonl=False, learning_rate=6e-4, warmup_iters=0,
@@ -128,13 +149,15 @@ def main():
         X, Y = tr.batches.get_batch("train")
         for _ in range(args.warmup):
             loss, _, X, Y = tr.train_step(X, Y)
-        from nanosandbox_amd.ops import gemm_tune
-        for k, v in sorted(gemm_tune.table().items()):
-            print(f"gemm backend {k}: {v}")
+        from nanosandbox_amd.ops import gemm_dispatch
+        gemm_kernels = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": v for k, v in sorted(gemm_dispatch.kernels_used().items())}
+        for k, v in gemm_kernels.items():
+            print(f"gemm {k}: {v}")
+        sweep = []
         if world > 1 and args.rccl_sweep:
             from nanosandbox_amd.parallel import allreduce_sweep
-            allreduce_sweep(tr.info, [int(v) for v in args.rccl_sweep.split(",") if v])
-        torch.cuda.synchronize()
+            sweep = allreduce_sweep(tr.info, [int(v) for v in args.rccl_sweep.split(",") if v])
+        sync()
         if dist.is_initialized():
             dist.barrier()
         prof = None
@@ -147,16 +170,16 @@ def main():
                            on_trace_ready=tensorboard_trace_handler("./bench_log"), record_shapes=True,
                            profile_memory=False, with_stack=False)
             prof.start()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss, _, X, Y = tr.train_step(X, Y)
             if prof is not None:
                 prof.step()
-        torch.cuda.synchronize()
+        sync()
         if dist.is_initialized():
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         dt = time.perf_counter() - t0
         dt_t = torch.tensor([dt], device=tr.device, dtype=torch.float64)
         if dist.is_initialized():
@@ -186,7 +209,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": (f"real ({dataset}); random-init weights" if args.real_data else
                      "synthetic (uniform random tokens, vocab 50304); random-init weights"),
             "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,
@@ -196,9 +219,15 @@ def main():
                        "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
                        "residual_dtype": "bf16" if args.bf16_residual else "fp32",
                        "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt)},
-            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1),
+            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1) if cuda else None,
             "mfu_vs_2.5PF": round(mfu, 4),
             "loss": round(lossf, 4),
+            # every GEMM shape of the step and the kernel that ran it (fixed rule,
+            # ops/gemm_dispatch.py): a vendor-library pick would read "torch"
+            "gemm_kernels": gemm_kernels,
+            # N > 1: RCCL's transport per rank (from its INIT log) + the 64 MiB all-reduce, and
+            # the bus bandwidth by message size (docs/rccl.md bucket sizing)
+            "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep),
         }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -356,6 +356,7 @@ constexpr int SMP_MAXC = 52;  // logits per thread kept in registers (V <= 53248
 template <bool VEC4>
 __global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* __restrict__ logits, int V, int ld,
                                                                   float scale_log2, int top_k, uint64_t salt,
+                                                                  const uint64_t* __restrict__ salt_dev,
                                                                   const int64_t* __restrict__ pos,
                                                                   int64_t* __restrict__ tok, int64_t* __restrict__ gen,
                                                                   int gen_ld) {
@@ -408,7 +409,10 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_topk_kernel(const float* _
   SMP_TICK(1);
   const float m = key_val(kmax);
   const int p = (int)*pos;
-  const uint32_t hsh = nsa_hash(nsa_seed(salt), (uint64_t)b * 0x9E3779B97F4A7C15ull + (uint64_t)p);
+  // the device salt (when given) is read at run time, so a captured sampling graph draws a
+  // fresh stream whenever the caller rewrites it (one per generate call)
+  const uint64_t sl = salt ^ (salt_dev ? *salt_dev : 0ull);
+  const uint32_t hsh = nsa_hash(nsa_seed(sl), (uint64_t)b * 0x9E3779B97F4A7C15ull + (uint64_t)p);
   const float unif = (float)(hsh >> 8) * (1.0f / 16777216.0f);
 
   if (top_k > 0 && top_k < V && top_k <= SMP_THREADS) {
@@ -978,19 +982,21 @@ NSA_API hipError_t nsa_decode_attn(const void* qkv, void* kc, void* vc, const vo
 }
 
 // Top-k / temperature sampling of logits [B, V] (fp32, row stride ld) on the device:
-// writes tok[b] and gen[b * gen_ld + *pos].  top_k <= 0 keeps every logit.
+// writes tok[b] and gen[b * gen_ld + *pos].  top_k <= 0 keeps every logit.  The uniform is a
+// counter hash of (salt ^ *salt_dev, row, position); salt_dev may be NULL.
 NSA_API hipError_t nsa_sample_topk(const void* logits, int B, int V, int ld, float temperature, int top_k,
-                                   uint64_t salt, const void* pos, void* tok, void* gen, int gen_ld, hipStream_t s) {
+                                   uint64_t salt, const void* salt_dev, const void* pos, void* tok, void* gen,
+                                   int gen_ld, hipStream_t s) {
   if (B < 1 || V < 1 || V > SMP_THREADS * SMP_MAXC || !(temperature > 0.0f)) return hipErrorInvalidValue;
   const bool vec4 = V % 4 == 0 && ld % 4 == 0 && ((uintptr_t)logits & 15) == 0;
   if (vec4)
     sample_topk_kernel<true><<<B, SMP_THREADS, 0, s>>>((const float*)logits, V, ld, 1.4426950408889634f / temperature,
-                                                       top_k, salt, (const int64_t*)pos, (int64_t*)tok, (int64_t*)gen,
-                                                       gen_ld);
+                                                       top_k, salt, (const uint64_t*)salt_dev, (const int64_t*)pos,
+                                                       (int64_t*)tok, (int64_t*)gen, gen_ld);
   else
     sample_topk_kernel<false><<<B, SMP_THREADS, 0, s>>>((const float*)logits, V, ld, 1.4426950408889634f / temperature,
-                                                        top_k, salt, (const int64_t*)pos, (int64_t*)tok, (int64_t*)gen,
-                                                        gen_ld);
+                                                        top_k, salt, (const uint64_t*)salt_dev, (const int64_t*)pos,
+                                                        (int64_t*)tok, (int64_t*)gen, gen_ld);
   return hipGetLastError();
 }
 

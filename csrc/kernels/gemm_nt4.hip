@@ -63,15 +63,16 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 #define NSA_NT4_RS 2  // MFMAs between the next K-tile's fragment reads
 #endif
 
-enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2 };
+enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XDX = 4 };
 
 // pieces a K-tile has issued when it waits for the previous K-tile's
 constexpr int Q_D0 = 15 * NSA_NT4_ER + 4;  // slot of the first piece
 constexpr int Q_ISS = (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 : 16;
-// vector-memory operations of one wave's epilogue of a full tile (stores, and the U loads)
+// vector-memory operations one wave's epilogue of a full tile can leave outstanding (an
+// upper bound: its stores, plus loads the compiler has not yet waited for)
 template <int EPI>
 constexpr int q_epi_vm() {
-  return EPI == Q_EPI_BF16 ? 32 : 64;
+  return EPI == Q_EPI_BF16 ? 32 : EPI == Q_EPI_XENT ? 48 : 64;
 }
 
 typedef int q_i32x4 __attribute__((ext_vector_type(4)));
@@ -82,7 +83,12 @@ struct Nt4Args {
   const bf16_t* B;
   bf16_t* C;
   bf16_t* C2;
-  const bf16_t* U;
+  const bf16_t* U;     // DGELU: the pre-activation u
+  const bf16_t* bias;  // BIAS: bias[N] added before the store (and before GELU)
+  // fused cross-entropy (see nsa_gemm_nt4_xent / _xdx below)
+  const float* rowf;   // XENT: per-row shift c (the target logit); XDX: per-row pairs {g / S, g or 0}
+  float* part;         // XENT: per-(column half-tile, row) partial sums of exp(logit - c)
+  int nvalid;
   int M, N, K;
   int lda, ldb, ldc;
   int tiles_m, tiles_n, tiles;
@@ -251,10 +257,26 @@ __device__ __forceinline__ void q_st16(bf16_t* p, uint32_t a, uint32_t b, uint32
   }
 }
 
+// sum over the 16 lanes of a DPP row (lanes 16 q .. 16 q + 15); every lane gets the total
+__device__ __forceinline__ float q_rowsum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 // Epilogue straight from the accumulators: for fragment row i and element e, lane l holds
 // row 16 i + 4 (l >> 4) + e of the wave's 128 rows, columns 8 (l & 15) + 0..7 (fragments
 // j = 0..7), so the 16 lanes of a quarter-wave write one row's 256 contiguous bytes.
-template <int EPI, bool NT, bool NOSTORE = false>
+//
+// Fused cross-entropy (nanoGPT F.cross_entropy over the tied lm_head):
+//  XENT (logits GEMM): E = exp(acc - c_row) in bf16 instead of the logits (columns >= nvalid,
+//       the vocabulary padding, give 0), and the row sums of the fp32 E over the wave's 128
+//       columns into part[2 tile_n + wn][row] (plain stores, one writer per slot: no atomics);
+//  XDX  (dX = dlogits · W): out = g (acc / S_row - W[t_row]) in fp32 before the one rounding,
+//       i.e. (softmax - onehot) · W without a dlogits tensor (ignored rows: 1/S = 0, no W row).
+template <int EPI, bool NT, bool BIAS, bool NOSTORE = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
                                            int lane) {
   int m0, n0, mlo, nlo;
@@ -262,12 +284,15 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
   const bool full = (m0 == mlo) & (n0 == nlo);
   const int r = lane & 15, q = lane >> 4;
   const int col = n0 + wn * 128 + 8 * r;
+  const int row0 = m0 + wm * 128 + 4 * q;
+  float bv[8];
+  if constexpr (BIAS) load8(g.bias + col, bv);
   // EPI_DGELU: the U pieces of two fragment rows are in flight at a time
   q_u32x4 uv[2][4];
   auto load_u = [&](int i, q_u32x4 (&dst)[4]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = m0 + wm * 128 + 16 * i + 4 * q + e;  // in bounds: tiles lie inside the matrix
+      const int row = row0 + 16 * i + e;  // in bounds: tiles lie inside the matrix
       dst[e] = __builtin_nontemporal_load(reinterpret_cast<const q_u32x4*>(g.U + (int64_t)row * g.ldc + col));
     }
   };
@@ -275,18 +300,81 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
     load_u(0, uv[0]);
     load_u(1, uv[1]);
   }
+  // EPI_XENT: the shift c of the lane's 32 rows (log2 units), the vocabulary-padding edge
+  constexpr float kLog2e = 1.4426950408889634f;
+  f32x4 crow[8];
+  if constexpr (EPI == Q_EPI_XENT) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) crow[i] = *reinterpret_cast<const f32x4*>(g.rowf + row0 + 16 * i) * kLog2e;
+  }
+  const bool edge = EPI == Q_EPI_XENT && n0 + wn * 128 + 128 > g.nvalid;
+  const int tn = nlo / Q_BN;  // column tile index
+  // EPI_XDX: per fragment row the 4 rows' coefficient pairs {g / S, g or 0}, two rows ahead
+  // (with the gathered W rows, which ride in U like the GELU' epilogue's pre-activations)
+  f32x4 xc[2][2];
+  auto load_c = [&](int i, f32x4 (&dst)[2]) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(g.rowf + 2 * (row0 + 16 * i));
+    dst[0] = p[0];
+    dst[1] = p[1];
+  };
+  if constexpr (EPI == Q_EPI_XDX) {
+    load_u(0, uv[0]);
+    load_u(1, uv[1]);
+    load_c(0, xc[0]);
+    load_c(1, xc[1]);
+  }
   // one base pointer per lane; a store's row offset (16 i + e) rows is wave-uniform
-  const int row0 = m0 + wm * 128 + 4 * q;
   bf16_t* const cb = g.C + (int64_t)row0 * g.ldc + col;
   bf16_t* const cb2 = EPI == Q_EPI_GELU ? g.C2 + (int64_t)row0 * g.ldc + col : nullptr;
   {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      float rs[4];  // XENT: the 4 rows' partial sums
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if (!full && (row0 + 16 * i + e < mlo || col < nlo)) continue;
-        uint32_t w[4] = {q_pk(acc[i][0][e], acc[i][1][e]), q_pk(acc[i][2][e], acc[i][3][e]),
-                         q_pk(acc[i][4][e], acc[i][5][e]), q_pk(acc[i][6][e], acc[i][7][e])};
+        const bool skip = !full && (row0 + 16 * i + e < mlo || col < nlo);
+        const int64_t off = (int64_t)(16 * i + e) * g.ldc;
+        if constexpr (EPI == Q_EPI_XENT) {
+          // no early exit here: every lane takes part in the row reduction
+          const float c = crow[i][e];
+          uint32_t w[4];
+          float s = 0.0f;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][2 * h][e], kLog2e, -c));
+            float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][2 * h + 1][e], kLog2e, -c));
+            if (edge) {
+              e0 = col + 2 * h < g.nvalid ? e0 : 0.0f;
+              e1 = col + 2 * h + 1 < g.nvalid ? e1 : 0.0f;
+            }
+            w[h] = q_pk(e0, e1);
+            s += e0 + e1;
+          }
+          rs[e] = q_rowsum16(col < nlo ? 0.0f : s);
+          if (!skip) {
+            if constexpr (NOSTORE) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+            else q_st16<NT>(cb + off, w[0], w[1], w[2], w[3]);
+          }
+          continue;
+        }
+        if (skip) continue;
+        uint32_t w[4];
+        if constexpr (EPI == Q_EPI_XDX) {
+          const float sc = xc[i & 1][e >> 1][2 * (e & 1)];
+          const float gw = xc[i & 1][e >> 1][2 * (e & 1) + 1];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t wr = uv[i & 1][e][h];
+            w[h] = q_pk(__builtin_fmaf(sc, acc[i][2 * h][e], -gw * __uint_as_float(wr << 16)),
+                        __builtin_fmaf(sc, acc[i][2 * h + 1][e], -gw * __uint_as_float(wr & 0xffff0000u)));
+          }
+        } else if constexpr (BIAS) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) w[h] = q_pk(acc[i][2 * h][e] + bv[2 * h], acc[i][2 * h + 1][e] + bv[2 * h + 1]);
+        } else {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) w[h] = q_pk(acc[i][2 * h][e], acc[i][2 * h + 1][e]);
+        }
         if constexpr (EPI == Q_EPI_DGELU) {
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
@@ -296,7 +384,6 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
             w[h] = q_pk(a.x, a.y);
           }
         }
-        const int64_t off = (int64_t)(16 * i + e) * g.ldc;
         if constexpr (NOSTORE) {
           asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
         } else {
@@ -312,8 +399,17 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           q_st16<NT>(cb2 + off, gg[0], gg[1], gg[2], gg[3]);
         }
       }
-      if constexpr (EPI == Q_EPI_DGELU) {
+      if constexpr (EPI == Q_EPI_XENT) {
+        // lanes r = 0..3 of each row group write the 4 rows' sums (one slot per wave column half)
+        const int row = row0 + 16 * i + r;
+        const float v = r == 0 ? rs[0] : r == 1 ? rs[1] : r == 2 ? rs[2] : rs[3];
+        if (r < 4 && row >= mlo && !NOSTORE) g.part[(int64_t)(2 * tn + wn) * g.M + row] = v;
+      }
+      if constexpr (EPI == Q_EPI_DGELU || EPI == Q_EPI_XDX) {
         if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
+      }
+      if constexpr (EPI == Q_EPI_XDX) {
+        if (i + 2 < 8) load_c(i + 2, xc[i & 1]);
       }
     }
   }
@@ -321,10 +417,11 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 
 }  // namespace
 
-// PROBE (timing only, wrong results): 1 = no DMA after the prologue, 2 = no wait for the
-// previous K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue at all,
-// 5 = epilogue arithmetic without its stores
-template <int EPI, bool NT, int PROBE>
+// PROBE (timing only, wrong results; compiled in only with -DNSA_PROBES, i.e. a
+// build_variant library): 1 = no DMA after the prologue, 2 = no wait for the previous
+// K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue at all, 5 = epilogue
+// arithmetic without its stores
+template <int EPI, bool NT, int PROBE, bool BIAS = false>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   __shared__ __attribute__((aligned(16))) char smem[Q_SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -484,7 +581,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT, PROBE == 5>(g, acc, seq, wm, wn, lane);
+      q_epilogue<EPI, NT, BIAS, PROBE == 5>(g, acc, seq, wm, wn, lane);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -507,57 +604,143 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   q_vmwait<0>();
 }
 
-// Same contract as nsa_gemm_nt (epi: 0 bf16, 1 u + gelu(u) into C / C2, 2 acc * gelu'(U);
-// bits 8-11 timing probe (1 no DMA, 4 no stores); bits 12-13 store policy: 0 nontemporal above the Infinity Cache, 1 always, 2 never;
-// bits 16-23 row-blocks per tile group, 0 = automatic).  grid = persistent workgroups.
+namespace {
+
+hipError_t nt4_check(const Nt4Args& a, int grid) {
+  if (a.M < Q_BM || a.N < Q_BN || a.K < Q_BK || a.K % Q_BK != 0 || a.N % 8 || a.lda % 8 || a.ldb % 8 || a.ldc % 8 ||
+      a.lda < a.K || a.ldb < a.K || a.ldc < a.N || grid < 1)
+    return hipErrorInvalidValue;
+  if ((int64_t)Q_BM * a.lda * 2 + Q_GRP >= (1ll << 31) || (int64_t)Q_BN * a.ldb * 2 + Q_GRP >= (1ll << 31))
+    return hipErrorInvalidValue;
+  return hipSuccess;
+}
+
+void nt4_geometry(Nt4Args& a, int gmsel) {
+  a.tiles_m = (a.M + Q_BM - 1) / Q_BM;
+  a.tiles_n = (a.N + Q_BN - 1) / Q_BN;
+  a.tiles = a.tiles_m * a.tiles_n;
+  // tile groups (q_cur_tile): 4 row blocks x every column for the N <= 1024 outputs (c_attn /
+  // c_fc dX, attn.c_proj, mlp.c_proj: 0.2-2.3 % faster than 1), rows for N <= 4096, 8 beyond
+  a.gm = gmsel ? gmsel : (a.tiles_n <= 4 ? 4 : a.tiles_n <= 16 ? 1 : 8);
+}
+
+template <int E, bool B>
+void nt4_launch(const Nt4Args& a, dim3 gr, bool nt, int probe, hipStream_t s) {
+#ifdef NSA_PROBES
+  switch (probe) {
+    case 1: gemm_nt4_kernel<E, true, 1, B><<<gr, Q_THR, 0, s>>>(a); return;
+    case 2: gemm_nt4_kernel<E, true, 2, B><<<gr, Q_THR, 0, s>>>(a); return;
+    case 3: gemm_nt4_kernel<E, true, 3, B><<<gr, Q_THR, 0, s>>>(a); return;
+    case 4: gemm_nt4_kernel<E, true, 4, B><<<gr, Q_THR, 0, s>>>(a); return;
+    case 5: gemm_nt4_kernel<E, true, 5, B><<<gr, Q_THR, 0, s>>>(a); return;
+    default: break;
+  }
+#else
+  (void)probe;
+#endif
+  if (nt) gemm_nt4_kernel<E, true, 0, B><<<gr, Q_THR, 0, s>>>(a);
+  else gemm_nt4_kernel<E, false, 0, B><<<gr, Q_THR, 0, s>>>(a);
+}
+
+bool nt4_store_nt(int stp, int64_t out_bytes) { return stp == 1 || (stp == 0 && out_bytes >= NSA_NT_MIN_BYTES); }
+
+}  // namespace
+
+// C = A · B^T (bf16) with an optional bias[N] (bf16) added to every row.
+// epi: 0 bf16, 1 u + gelu(u) into C / C2, 2 acc * gelu'(U); bits 8-11 timing probe (-DNSA_PROBES
+// builds only; 1 no DMA, 4 no stores, ...); bits 12-13 store policy: 0 nontemporal above the
+// Infinity Cache, 1 always, 2 never; bits 16-23 row-blocks per tile group, 0 = automatic.
+// grid = persistent workgroups.
 NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
-                                const void* U, int M, int N, int K, int grid, hipStream_t s) {
-  const int epi_full = epi;
+                                const void* U, const void* bias, int M, int N, int K, int grid, hipStream_t s) {
   const int stp = (epi >> 12) & 0x3;
   const int probe = (epi >> 8) & 0xf;
+  const int gmsel = (epi >> 16) & 0xff;
   epi &= 0xff;
-  if (M < Q_BM || N < Q_BN || K < Q_BK || K % Q_BK != 0 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K ||
-      ldb < K || ldc < N || grid < 1)
-    return hipErrorInvalidValue;
-  if ((int64_t)Q_BM * lda * 2 + Q_GRP >= (1ll << 31) || (int64_t)Q_BN * ldb * 2 + Q_GRP >= (1ll << 31))
-    return hipErrorInvalidValue;
-  if ((epi == Q_EPI_GELU && !C2) || (epi == Q_EPI_DGELU && !U)) return hipErrorInvalidValue;
   Nt4Args a{};
   a.A = (const bf16_t*)A;
   a.B = (const bf16_t*)B;
   a.C = (bf16_t*)C;
   a.C2 = (bf16_t*)C2;
   a.U = (const bf16_t*)U;
+  a.bias = (const bf16_t*)bias;
   a.M = M;
   a.N = N;
   a.K = K;
   a.lda = lda;
   a.ldb = ldb;
   a.ldc = ldc;
-  a.tiles_m = (M + Q_BM - 1) / Q_BM;
-  a.tiles_n = (N + Q_BN - 1) / Q_BN;
-  a.tiles = a.tiles_m * a.tiles_n;
-  const int gmsel = (epi_full >> 16) & 0xff;
-  // tile groups (q_cur_tile): 4 row blocks x every column for the N <= 1024 outputs (c_attn /
-  // c_fc dX, attn.c_proj, mlp.c_proj: 0.2-2.3 % faster than 1), rows for N <= 4096, 8 beyond
-  a.gm = gmsel ? gmsel : (a.tiles_n <= 4 ? 4 : a.tiles_n <= 16 ? 1 : 8);
-  const int64_t out_bytes = (int64_t)M * N * 2 * (epi == Q_EPI_GELU ? 2 : 1);
-  const bool nt = stp == 1 || (stp == 0 && out_bytes >= NSA_NT_MIN_BYTES);
+  if (nt4_check(a, grid) != hipSuccess) return hipErrorInvalidValue;
+  if ((epi == Q_EPI_GELU && !C2) || (epi == Q_EPI_DGELU && (!U || bias)) || (bias && (uintptr_t)bias % 16))
+    return hipErrorInvalidValue;
+  nt4_geometry(a, gmsel);
+  const bool nt = nt4_store_nt(stp, (int64_t)M * N * 2 * (epi == Q_EPI_GELU ? 2 : 1));
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
-#define NT4_LAUNCH(E)                                                        \
-  if (probe == 1) gemm_nt4_kernel<E, true, 1><<<gr, Q_THR, 0, s>>>(a);       \
-  else if (probe == 2) gemm_nt4_kernel<E, true, 2><<<gr, Q_THR, 0, s>>>(a);  \
-  else if (probe == 3) gemm_nt4_kernel<E, true, 3><<<gr, Q_THR, 0, s>>>(a);  \
-  else if (probe == 4) gemm_nt4_kernel<E, true, 4><<<gr, Q_THR, 0, s>>>(a);  \
-  else if (probe == 5) gemm_nt4_kernel<E, true, 5><<<gr, Q_THR, 0, s>>>(a);  \
-  else if (nt) gemm_nt4_kernel<E, true, 0><<<gr, Q_THR, 0, s>>>(a);          \
-  else gemm_nt4_kernel<E, false, 0><<<gr, Q_THR, 0, s>>>(a);
   switch (epi) {
-    case Q_EPI_BF16: NT4_LAUNCH(Q_EPI_BF16) break;
-    case Q_EPI_GELU: NT4_LAUNCH(Q_EPI_GELU) break;
-    case Q_EPI_DGELU: NT4_LAUNCH(Q_EPI_DGELU) break;
+    case Q_EPI_BF16:
+      if (bias) nt4_launch<Q_EPI_BF16, true>(a, gr, nt, probe, s);
+      else nt4_launch<Q_EPI_BF16, false>(a, gr, nt, probe, s);
+      break;
+    case Q_EPI_GELU:
+      if (bias) nt4_launch<Q_EPI_GELU, true>(a, gr, nt, probe, s);
+      else nt4_launch<Q_EPI_GELU, false>(a, gr, nt, probe, s);
+      break;
+    case Q_EPI_DGELU: nt4_launch<Q_EPI_DGELU, false>(a, gr, nt, probe, s); break;
     default: return hipErrorInvalidValue;
   }
-#undef NT4_LAUNCH
+  return hipGetLastError();
+}
+
+// Fused cross-entropy, forward: E = exp(A · B^T - c[row]) (bf16, [M, N] at ldc; columns >=
+// nvalid give 0) and part[2 (column tile) + (column half)][row] = the fp32 row sums of E over
+// that half tile (2 * ceil(N / 256) slots of M floats).  c = the target logit of the row
+// (computed before this GEMM), so sum_j E = exp(loss_row) >= ~1: no overflow short of a
+// per-token loss of ~80 nats (nsa_xent_combine flags such rows for an exact recompute).
+NSA_API hipError_t nsa_gemm_nt4_xent(const void* A, int lda, const void* B, int ldb, void* E, int ldc,
+                                     const void* crow, void* part, int M, int N, int nvalid, int K, int grid,
+                                     hipStream_t s) {
+  Nt4Args a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)E;
+  a.rowf = (const float*)crow;
+  a.part = (float*)part;
+  a.nvalid = nvalid;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  if (nt4_check(a, grid) != hipSuccess || nvalid < 1 || nvalid > N || M % 4 || !crow || !part)
+    return hipErrorInvalidValue;
+  nt4_geometry(a, 0);
+  const dim3 gr(grid < a.tiles ? grid : a.tiles);
+  nt4_launch<Q_EPI_XENT, false>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
+  return hipGetLastError();
+}
+
+// Fused cross-entropy, input gradient: C = cs[row] * (A · B^T) - cw[row] * U with A = E [M, K]
+// (the forward's exp), B = W^T [N, K] (K = the padded vocabulary), U [M, N] (ld ldc) = the
+// rows W[target] gathered by nsa_xent_bwd_prep, and rowc [M][2] = {cs, cw} = {g / S, g} (0, 0
+// for an ignored row): g (softmax - onehot) · W with the subtraction in fp32.
+NSA_API hipError_t nsa_gemm_nt4_xdx(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                    const void* U, const void* rowc, int M, int N, int K, int grid, hipStream_t s) {
+  Nt4Args a{};
+  a.A = (const bf16_t*)A;
+  a.B = (const bf16_t*)B;
+  a.C = (bf16_t*)C;
+  a.U = (const bf16_t*)U;
+  a.rowf = (const float*)rowc;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  if (nt4_check(a, grid) != hipSuccess || M % 4 || !U || !rowc) return hipErrorInvalidValue;
+  nt4_geometry(a, 0);
+  const dim3 gr(grid < a.tiles ? grid : a.tiles);
+  nt4_launch<Q_EPI_XDX, false>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
   return hipGetLastError();
 }

@@ -122,7 +122,45 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict_
   if (w == 0 && c < C) atomicAdd(out + c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
+// Bias gradient, first stage: partial[b][c] = sum over row slice b of dy[r][c] (bf16 in, fp32
+// sums).  Block = 4 row lanes x 64 column chunks of 8 (16-byte loads); the 4 row lanes fold
+// in LDS.  The second stage is colsum_kernel (nsa_colsum_accum[_ordered]) into the gradient.
+__global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(const bf16_t* __restrict__ dy, int ld, int rows, int C,
+                                                            int rows_per_block, float* __restrict__ partial) {
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + cx) * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    for (int r = r0 + ry; r < r1; r += 4) {
+      float f[8];
+      load8(dy + (int64_t)r * ld + c, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+  }
+  __shared__ float red[4][64 * 8 + 4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ry][cx * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 8; i += kBlock) {
+    const int cc = blockIdx.x * 64 * 8 + i;
+    if (cc < C) partial[(int64_t)blockIdx.y * C + cc] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 }  // namespace
+
+// partial [nblk][C] (fp32) = column sums of dy [rows][C] (bf16, leading dim ld) over nblk row slices
+NSA_API hipError_t nsa_colsum_bf16_partial(const void* dy, int ld, int rows, int C, void* partial, int nblk,
+                                           hipStream_t s) {
+  if (C % 8 || ld % 8 || nblk < 1) return hipErrorInvalidValue;
+  dim3 grid((C / 8 + 63) / 64, nblk);
+  colsum_bf16_kernel<<<grid, kBlock, 0, s>>>((const bf16_t*)dy, ld, rows, C, (rows + nblk - 1) / nblk,
+                                             (float*)partial);
+  NSA_LAUNCH_CHECK();
+}
 
 NSA_API hipError_t nsa_adamw_step(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask,
                                   int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,

@@ -34,19 +34,22 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
 
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
-                                                     float* __restrict__ row_loss, int V, int write_grad) {
+                                                     float* __restrict__ row_loss, int V, int ld, int write_grad) {
   const int row = blockIdx.x;
-  bf16_t* lr = logits + (int64_t)row * V;
+  bf16_t* lr = logits + (int64_t)row * ld;
   const int64_t tgt = targets[row];
   float m = -INFINITY, s = 0.0f;
   if (VEC) {
-    const int nv = V / 8;
+    const int nv = ld / 8;
     for (int i = threadIdx.x; i < nv; i += kBlock) {
       float f[8];
       load8(lr + i * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = i * 8 + j < V ? f[j] : -INFINITY;
       float bm = f[0];
 #pragma unroll
       for (int j = 1; j < 8; ++j) bm = fmaxf(bm, f[j]);
+      if (bm == -INFINITY) continue;  // a chunk of padding columns only
       float bs = 0.0f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) bs += __expf(f[j] - bm);
@@ -79,14 +82,14 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
   if (!write_grad) return;
   const float invS = 1.0f / S;
   if (VEC) {
-    const int nv = V / 8;
+    const int nv = ld / 8;
     for (int i = threadIdx.x; i < nv; i += kBlock) {
       float f[8];
       load8(lr + i * 8, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = i * 8 + j;
-        float p = valid ? __expf(f[j] - M) * invS : 0.0f;
+        float p = valid && col < V ? __expf(f[j] - M) * invS : 0.0f;
         if (valid && col == tgt) p -= 1.0f;
         f[j] = p;
       }
@@ -140,14 +143,16 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 template <int RB, int RC, int NT = 0>
 __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logits,
                                                      const int64_t* __restrict__ targets,
-                                                     float* __restrict__ row_loss, int V, int write_grad) {
+                                                     float* __restrict__ row_loss, int V, int ld,
+                                                     int write_grad) {
   constexpr int kBlock = RB;
   constexpr int kRegChunks = RC;
   const int row = blockIdx.x;
-  bf16_t* lr = logits + (int64_t)row * V;
+  bf16_t* lr = logits + (int64_t)row * ld;
   const int64_t tgt = targets[row];
   const bool valid = tgt >= 0 && tgt < V;
-  const int nv = V / 8;
+  const int nv = ld / 8;
+  const bool pad = V != ld;  // vocabulary padding columns (>= V) take no part
   __shared__ float red[kBlock / 64];
   // all loads first (clamped index, no branch around a load), then compute
   uint4 r[kRegChunks];
@@ -167,9 +172,13 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
   for (int c = 0; c < kRegChunks; ++c) {
     if ((int)threadIdx.x + c * kBlock < nv) {
       const uint32_t w4[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+      const int col = ((int)threadIdx.x + c * kBlock) * 8;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        m = fmaxf(m, fmaxf(__uint_as_float(w4[q] << 16), __uint_as_float(w4[q] & 0xffff0000u)));
+      for (int q = 0; q < 4; ++q) {
+        const float lo = !pad || col + 2 * q < V ? __uint_as_float(w4[q] << 16) : -INFINITY;
+        const float hi = !pad || col + 2 * q + 1 < V ? __uint_as_float(w4[q] & 0xffff0000u) : -INFINITY;
+        m = fmaxf(m, fmaxf(lo, hi));
+      }
     }
   }
   const float M = block_reduce_max<RB>(m, red);
@@ -178,9 +187,12 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
   for (int c = 0; c < kRegChunks; ++c) {
     if ((int)threadIdx.x + c * kBlock < nv) {
       const uint32_t w4[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+      const int col = ((int)threadIdx.x + c * kBlock) * 8;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        s += __expf(__uint_as_float(w4[q] << 16) - M) + __expf(__uint_as_float(w4[q] & 0xffff0000u) - M);
+      for (int q = 0; q < 4; ++q) {
+        const float e0 = __expf(__uint_as_float(w4[q] << 16) - M), e1 = __expf(__uint_as_float(w4[q] & 0xffff0000u) - M);
+        s += (!pad || col + 2 * q < V ? e0 : 0.0f) + (!pad || col + 2 * q + 1 < V ? e1 : 0.0f);
+      }
     }
   }
   const float S = block_reduce_sum<RB>(s, red);
@@ -195,8 +207,9 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
       float f[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        f[2 * q] = valid ? __expf(__uint_as_float(w4[q] << 16) - M) * invS : 0.0f;
-        f[2 * q + 1] = valid ? __expf(__uint_as_float(w4[q] & 0xffff0000u) - M) * invS : 0.0f;
+        f[2 * q] = valid && (!pad || i * 8 + 2 * q < V) ? __expf(__uint_as_float(w4[q] << 16) - M) * invS : 0.0f;
+        f[2 * q + 1] =
+            valid && (!pad || i * 8 + 2 * q + 1 < V) ? __expf(__uint_as_float(w4[q] & 0xffff0000u) - M) * invS : 0.0f;
       }
       if (valid && (tgt >> 3) == i) f[tgt & 7] -= 1.0f;
       if constexpr (NT & 2) {
@@ -221,30 +234,34 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
 // stores), 1 = 256 x 25, 2 = 512 x 13, 3 / 4 / 5 = 1024 x 7 with nontemporal loads + stores /
 // stores / loads, 6 = 1024 x 7 plain.  Nontemporal loads + stores: 4618 -> 4348 us
 // (5.35 -> 5.69 TB/s, bitwise-identical output); stores alone 4557, loads alone 4641.
-NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int write_grad,
-                                hipStream_t s) {
+// Rows are `ld` apart; columns >= V (vocabulary padding, ld > V) are excluded and get a
+// zero gradient.  Since round 4 this separate pass serves deterministic mode and the shapes
+// the fused path (xent_fused.hip) does not take.
+NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int ld,
+                                int write_grad, hipStream_t s) {
   const int variant = (write_grad >> 8) & 0xff;
   write_grad &= 0xff;
+  if (ld < V) return hipErrorInvalidValue;
   bf16_t* lg = (bf16_t*)logits;
   const int64_t* tg = (const int64_t*)targets;
   float* rl = (float*)row_loss;
-  if (V % 8 == 0 && variant >= 3 && variant <= 5 && V <= 1024 * 8 * 7) {
+  const bool vec = ld % 8 == 0;
+  if (vec && variant >= 3 && variant <= 5 && ld <= 1024 * 8 * 7) {
     // 3: nontemporal loads + stores, 4: nontemporal stores, 5: nontemporal loads
-    if (variant == 3) xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
-    else if (variant == 4) xent_reg_kernel<1024, 7, 2><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
-    else xent_reg_kernel<1024, 7, 1><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
-  } else if (V % 8 == 0 && variant == 1 && V <= 256 * 8 * 25)
-    xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0 && variant == 2 && V <= 512 * 8 * 13)
-    xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0 && (variant == 6 || (int64_t)N * V * 2 < NSA_NT_MIN_BYTES) && V <= 1024 * 8 * 7)
-    xent_reg_kernel<1024, 7, 0><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0 && V <= 1024 * 8 * 7)  // default: nontemporal loads + stores
-    xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, write_grad);
-  else if (V % 8 == 0)
-    xent_kernel<true><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V, write_grad);
+    if (variant == 3) xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    else if (variant == 4) xent_reg_kernel<1024, 7, 2><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    else xent_reg_kernel<1024, 7, 1><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+  } else if (vec && variant == 1 && ld <= 256 * 8 * 25)
+    xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+  else if (vec && variant == 2 && ld <= 512 * 8 * 13)
+    xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+  else if (vec && (variant == 6 || (int64_t)N * ld * 2 < NSA_NT_MIN_BYTES) && ld <= 1024 * 8 * 7)
+    xent_reg_kernel<1024, 7, 0><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+  else if (vec && ld <= 1024 * 8 * 7)  // default: nontemporal loads + stores
+    xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+  else if (vec)
+    xent_kernel<true><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else
-    xent_kernel<false><<<N, kBlock, 0, s>>>((bf16_t*)logits, (const int64_t*)targets, (float*)row_loss, V,
-                                            write_grad);
+    xent_kernel<false><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   return hipGetLastError();
 }

@@ -1,0 +1,226 @@
+// Cross-entropy fused into the tied lm_head GEMMs (SURVEY.md §2.7 K8 + K10; nanoGPT
+// F.cross_entropy(logits, targets, ignore_index=-1) with a mean over the valid rows).
+//
+// The logits [M, V] are never stored.  With c_r = the target logit of row r (computed here
+// first, a gather-dot), the forward GEMM's epilogue (gemm_nt4.hip, EPI_XENT) writes
+// E = exp(logit - c_r) in bf16 plus per-half-tile row sums; then
+//   S_r = sum_v E[r, v] = exp(lse_r - c_r)   ->   loss_r = log S_r,  softmax = E / S_r.
+// Backward, with g = upstream gradient / valid rows:
+//   dX = g (E · W / S - W[t])                  (gemm_nt4 EPI_XDX: fp32 subtraction, one rounding)
+//   dW = E^T · (g x / S) - g sum_{r: t_r = v} x_r   (the four-wave weight-grad GEMM on E, then
+//        nsa_xent_dw_fix: the onehot part as fp32 atomics, with the bf16 rounding of the
+//        target entry's product taken back out, so p_t - 1 keeps fp32 precision).
+// Rows whose S leaves [0.5, 1e30] (a per-token loss beyond ~69 nats, or a target logit far
+// from the GEMM's) are recomputed exactly by nsa_xent_fixup (normally none: the kernel exits).
+#include "common.h"
+
+namespace {
+
+// c_r = x_r · W[t_r] (fp32 from bf16), t32_r = t_r (or -1 when ignored / out of range): one
+// wave per row, 16-byte loads
+__global__ __launch_bounds__(256) void xent_tlogit_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                          const bf16_t* __restrict__ W, int ldw,
+                                                          const int64_t* __restrict__ tgt, float* __restrict__ crow,
+                                                          int* __restrict__ t32, int M, int C, int V) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int64_t t = tgt[row];
+  const bool valid = t >= 0 && t < V;
+  float s = 0.0f;
+  if (valid) {
+    const bf16_t* xr = x + (int64_t)row * ldx;
+    const bf16_t* wr = W + t * ldw;
+    for (int c = lane * 8; c < C; c += 512) {
+      float a[8], b[8];
+      load8(xr + c, a);
+      load8(wr + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = __builtin_fmaf(a[j], b[j], s);
+    }
+    s = wave_sum(s);
+  }
+  if (lane == 0) {
+    crow[row] = s;
+    t32[row] = valid ? (int)t : -1;
+  }
+}
+
+// S_r = sum of the GEMM epilogue's partials; loss_r = log S_r, invS_r = 1 / S_r (0 and 0 for
+// an ignored row); rows outside [0.5, 1e30] go on the fix-up list
+__global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restrict__ part, int slots,
+                                                           const int* __restrict__ t32, float* __restrict__ loss,
+                                                           float* __restrict__ invS, int* __restrict__ nfix,
+                                                           int* __restrict__ fixlist, int M) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= M) return;
+  float S = 0.0f;
+  for (int k = 0; k < slots; ++k) S += part[(int64_t)k * M + row];
+  if (t32[row] < 0) {
+    loss[row] = 0.0f;
+    invS[row] = 0.0f;
+    return;
+  }
+  if (!(S >= 0.5f && S <= 1e30f)) {  // also catches NaN / inf
+    fixlist[atomicAdd(nfix, 1)] = row;
+    loss[row] = 0.0f;
+    invS[row] = 0.0f;
+    return;
+  }
+  loss[row] = __logf(S);
+  invS[row] = 1.0f / S;
+}
+
+// Exact recompute of a flagged row: logits l_v = x_r · W_v (fp32), m = max, E = exp(l - m),
+// S = sum E, loss = m + log S - l_t.  One workgroup per listed row (grid-stride over the
+// device-side count: with no flagged row every workgroup exits at once).
+__global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                         const bf16_t* __restrict__ W, int ldw, bf16_t* __restrict__ E,
+                                                         int lde, const int* __restrict__ t32,
+                                                         const int* __restrict__ nfix, const int* __restrict__ fixlist,
+                                                         float* __restrict__ loss, float* __restrict__ invS, int C,
+                                                         int V, int Vpad) {
+  __shared__ float xs[8192];
+  __shared__ float red[2][4];
+  const int n = *nfix;
+  for (int f = blockIdx.x; f < n; f += gridDim.x) {
+    const int row = fixlist[f];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) xs[c] = bf2f(x[(int64_t)row * ldx + c]);
+    __syncthreads();
+    auto logit = [&](int v) {
+      const bf16_t* wr = W + (int64_t)v * ldw;
+      float s = 0.0f;
+      for (int c = 0; c < C; c += 8) {
+        float b[8];
+        load8(wr + c, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = __builtin_fmaf(xs[c + j], b[j], s);
+      }
+      return s;
+    };
+    float m = -INFINITY;
+    for (int v = threadIdx.x; v < V; v += 256) m = fmaxf(m, logit(v));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float s = 0.0f;
+    for (int v = threadIdx.x; v < Vpad; v += 256) {
+      const float e = v < V ? __expf(logit(v) - m) : 0.0f;
+      E[(int64_t)row * lde + v] = f2bf(e);
+      s += e;
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[1][threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float S = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      loss[row] = m + __logf(S) - logit(t32[row]);
+      invS[row] = 1.0f / S;
+    }
+  }
+}
+
+// Backward prologue, per row: coefficient pair {g / S, g} (0, 0 ignored), the row W[t] gathered
+// for the dX epilogue, and xs = bf16(x g / S) for the weight-gradient GEMM
+__global__ __launch_bounds__(256) void xent_bwd_prep_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                            const bf16_t* __restrict__ W, int ldw,
+                                                            const int* __restrict__ t32, const float* __restrict__ invS,
+                                                            const float* __restrict__ gsc, float* __restrict__ coef,
+                                                            bf16_t* __restrict__ wrows, bf16_t* __restrict__ xs, int M,
+                                                            int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float g = *gsc;
+  const int t = t32[row];
+  const float sc = g * invS[row];
+  if (lane == 0) {
+    coef[2 * row] = sc;
+    coef[2 * row + 1] = t < 0 ? 0.0f : g;
+  }
+  const bf16_t* wr = W + (int64_t)(t < 0 ? 0 : t) * ldw;
+  const bf16_t* xr = x + (int64_t)row * ldx;
+  for (int c = lane * 8; c < C; c += 512) {
+    *reinterpret_cast<uint4*>(wrows + (int64_t)row * C + c) = *reinterpret_cast<const uint4*>(wr + c);
+    float a[8];
+    load8(xr + c, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] *= sc;
+    store8(xs + (int64_t)row * C + c, a);
+  }
+}
+
+// The onehot part of dW, per valid row r with target t:  gW[t] += E[r,t] (s x_r - bf16(s x_r))
+// - g x_r  (s = g / S): subtracts g x_r and takes back the rounding the GEMM's bf16 operand
+// put on the target entry's product.  fp32 atomics, one wave per row.
+__global__ __launch_bounds__(256) void xent_dw_fix_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                          const bf16_t* __restrict__ E, int lde,
+                                                          const int* __restrict__ t32, const float* __restrict__ invS,
+                                                          const float* __restrict__ gsc, float* __restrict__ gW,
+                                                          int ldg, int M, int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int t = t32[row];
+  if (t < 0) return;
+  const float g = *gsc;
+  const float s = g * invS[row];
+  const float et = bf2f(E[(int64_t)row * lde + t]);
+  const bf16_t* xr = x + (int64_t)row * ldx;
+  float* gr = gW + (int64_t)t * ldg;
+  for (int c = lane * 8; c < C; c += 512) {
+    float a[8];
+    load8(xr + c, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float p = s * a[j];
+      const float pr = bf2f(f2bf(p));
+      atomicAdd(gr + c + j, et * (p - pr) - g * a[j]);
+    }
+  }
+}
+
+}  // namespace
+
+NSA_API hipError_t nsa_xent_tlogit(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow,
+                                   void* t32, int M, int C, int V, hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldw % 8) return hipErrorInvalidValue;
+  xent_tlogit_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (const int64_t*)tgt,
+                                                 (float*)crow, (int*)t32, M, C, V);
+  return hipGetLastError();
+}
+
+// nfix must be zeroed by the caller before this launch (it is a stream-ordered counter)
+NSA_API hipError_t nsa_xent_combine(const void* part, int slots, const void* t32, void* loss, void* invS, void* nfix,
+                                    void* fixlist, int M, hipStream_t s) {
+  xent_combine_kernel<<<(M + 255) / 256, 256, 0, s>>>((const float*)part, slots, (const int*)t32, (float*)loss,
+                                                      (float*)invS, (int*)nfix, (int*)fixlist, M);
+  return hipGetLastError();
+}
+
+NSA_API hipError_t nsa_xent_fixup(const void* x, int ldx, const void* W, int ldw, void* E, int lde, const void* t32,
+                                  const void* nfix, const void* fixlist, void* loss, void* invS, int C, int V,
+                                  int Vpad, hipStream_t s) {
+  if (C > 8192 || C % 8 || ldw % 8) return hipErrorInvalidValue;
+  xent_fixup_kernel<<<64, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (bf16_t*)E, lde,
+                                       (const int*)t32, (const int*)nfix, (const int*)fixlist, (float*)loss,
+                                       (float*)invS, C, V, Vpad);
+  return hipGetLastError();
+}
+
+NSA_API hipError_t nsa_xent_bwd_prep(const void* x, int ldx, const void* W, int ldw, const void* t32,
+                                     const void* invS, const void* gsc, void* coef, void* wrows, void* xs, int M,
+                                     int C, hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldw % 8) return hipErrorInvalidValue;
+  xent_bwd_prep_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (const int*)t32,
+                                                   (const float*)invS, (const float*)gsc, (float*)coef,
+                                                   (bf16_t*)wrows, (bf16_t*)xs, M, C);
+  return hipGetLastError();
+}
+
+NSA_API hipError_t nsa_xent_dw_fix(const void* x, int ldx, const void* E, int lde, const void* t32, const void* invS,
+                                   const void* gsc, void* gW, int ldg, int M, int C, hipStream_t s) {
+  if (C % 8 || ldx % 8) return hipErrorInvalidValue;
+  xent_dw_fix_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32,
+                                                 (const float*)invS, (const float*)gsc, (float*)gW, ldg, M, C);
+  return hipGetLastError();
+}

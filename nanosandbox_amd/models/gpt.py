@@ -137,6 +137,11 @@ class GPT(nn.Module):
         self.lm_head = nn.Linear(config.n_embd, config.vocab_size, bias=False)
         # weight tying (https://paperswithcode.com/method/weight-tying)
         self.transformer.wte.weight = self.lm_head.weight
+        # a vocabulary the lm_head GEMM kernel cannot tile exactly (GPT-2's 50257, a char
+        # vocab of 65) runs on zero-padded rows: ask the flat store for the room
+        pad = ops.lm_head_rows(config.vocab_size)
+        if pad != config.vocab_size:
+            self.lm_head.weight._nsa_pad_rows = pad
 
         # init all weights
         self.apply(self._init_weights)
@@ -171,7 +176,9 @@ class GPT(nn.Module):
         fp32 + bf16 residual add promotes to fp32.  bf16 halves the residual bytes
         (opt-in, ``fp32_residual=False``)."""
         self.compute_dtype = dtype
-        self.residual_dtype = residual_dtype if dtype != torch.float32 else torch.float32
+        # bf16 compute runs our kernels; fp16 (GradScaler) and fp32 compute take the torch
+        # reference path of every op (train.py --dtype), with an fp32 residual stream
+        self.residual_dtype = residual_dtype if dtype == torch.bfloat16 else torch.float32
         for m in self.modules():
             if isinstance(m, LayerNorm):
                 m.out_dtype = dtype
@@ -184,7 +191,7 @@ class GPT(nn.Module):
             f"Cannot forward sequence of length {t}, block size is only {self.config.block_size}"
         tr = self.transformer
         x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, self.config.dropout, self.training,
-                          dtype=self.residual_dtype)
+                          dtype=self.residual_dtype, cdtype=self.compute_dtype)
         x = self._trunk(x)
 
         if targets is not None:
@@ -214,7 +221,8 @@ class GPT(nn.Module):
     def forward_logits(self, idx):
         """Full [B, T, V] fp32 logits (evaluation / tests)."""
         tr = self.transformer
-        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.residual_dtype)
+        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.residual_dtype,
+                          cdtype=self.compute_dtype)
         return ops.lm_head_logits(self._trunk(x), self.lm_head.weight)
 
     # ------------------------------------------------------------ surgery/api

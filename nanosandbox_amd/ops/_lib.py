@@ -55,7 +55,7 @@ _SIGNATURES = {
     "nsa_gelu_fwd": [c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_gelu_bwd": [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_dropout": [c_void_p, c_void_p, c_int64, c_float, c_uint64, c_void_p],
-    "nsa_xent_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "nsa_xent_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_scale_rows_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_adamw_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                        c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p],
@@ -69,8 +69,8 @@ _SIGNATURES = {
     "nsa_kv_append": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_decode_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                         c_float, c_int, c_void_p],
-    "nsa_sample_topk": [c_void_p, c_int, c_int, c_int, c_float, c_int, c_uint64, c_void_p, c_void_p, c_void_p, c_int,
-                        c_void_p],
+    "nsa_sample_topk": [c_void_p, c_int, c_int, c_int, c_float, c_int, c_uint64, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_int, c_void_p],
     "nsa_gemv": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_skinny_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_skinny_ln_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p,
@@ -90,12 +90,25 @@ _SIGNATURES = {
     "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],
-    "nsa_gemm_nt": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
-                    c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemm_wgrad4": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_void_p],
-    "nsa_gemm_nt4": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+    "nsa_gemm_nt4": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                      c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_gemm_small": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                       c_int, c_int, c_int, c_void_p],
+    "nsa_gemm_nt4_xent": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                          c_int, c_int, c_void_p],
+    "nsa_gemm_nt4_xdx": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_int, c_void_p],
+    "nsa_xent_tlogit": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "nsa_xent_combine": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "nsa_xent_fixup": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p, c_int, c_int, c_int, c_void_p],
+    "nsa_xent_bwd_prep": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_int, c_int, c_void_p],
+    "nsa_xent_dw_fix": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                        c_void_p],
+    "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
 }
 
 

@@ -1,10 +1,10 @@
 """Autograd functions for every op of the GPT hot path.
 
 Each op has exactly one GPU implementation — our gfx950 HIP kernels from
-``libnsa_kernels.so`` (GEMMs go to hipBLASLt through ``torch.mm``/``addmm``)
-— and a CPU implementation in plain fp32 torch that doubles as the numerics
-reference for the kernel tests.  The choice is by tensor device, not a
-backend switch.
+``libnsa_kernels.so``, GEMMs included (``ops/gemm_dispatch.py`` picks the kernel
+from the shape by a fixed rule; no vendor BLAS on the bf16 path) — and a CPU
+implementation in plain fp32 torch that doubles as the numerics reference for
+the kernel tests.  The choice is by tensor device and dtype, not a backend switch.
 
 Op inventory (nanoGPT ``model.py`` call sites):
 
@@ -13,8 +13,8 @@ op         computes                                     nanoGPT site
 =========  ==========================================  =========================
 K11/K12    ``drop(wte[idx] + wpe[t])``                 ``GPT.forward``
 K3         LayerNorm, eps 1e-5, optional bias           ``LayerNorm.forward``
-K5-K9      ``residual + x @ W^T + b``                   ``nn.Linear`` (+ residual add)
-K4         exact-erf GELU                               ``MLP.forward``
+K5-K9      ``x @ W^T + b`` (bias in the GEMM epilogue)   ``nn.Linear``
+K4         exact-erf GELU (in the c_fc GEMM epilogue)   ``MLP.forward``
 K1/K2      causal flash attention (+dropout)            ``CausalSelfAttention``
 K8+K10     tied lm_head + fused cross-entropy           ``GPT.forward`` loss
 =========  ==========================================  =========================
@@ -22,7 +22,7 @@ K8+K10     tied lm_head + fused cross-entropy           ``GPT.forward`` loss
 Gradient accumulation is fused: if a parameter carries ``main_grad`` (a view
 into the flat fp32 gradient buffer owned by ``optim.flat.FlatParamStore``),
 weight gradients are accumulated straight into it — for Linear weights inside
-the GEMM itself (``addmm`` with an fp32 output, beta=1) — and the parameter's
+the split-K GEMM itself (fp32 atomics into the flat buffer) — and the parameter's
 ``_nsa_grad_hook`` is called so the bucketed reducer can launch an all-reduce
 as soon as a bucket is complete.  Without ``main_grad`` the gradient is
 returned to autograd normally (plain ``.grad`` semantics, used by torch DDP
@@ -41,8 +41,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import gemm as _gemm
-from . import gemm_tune as _tune
-from . import streams as _streams
+from . import gemm_dispatch as _gd
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -77,46 +76,43 @@ def _accumulate(p: torch.Tensor, g: torch.Tensor):
     return None
 
 
-_ADDMM_INPLACE_OK = None
-
-
-def _addmm_f32_inplace_supported() -> bool:
-    """Probe once whether hipBLASLt accepts ``addmm(C, A_bf16, B_bf16, out_dtype=f32, out=C)``."""
-    global _ADDMM_INPLACE_OK
-    if _ADDMM_INPLACE_OK is None:
-        try:
-            a = torch.randn(40, 24, device="cuda", dtype=BF16)
-            b = torch.randn(24, 56, device="cuda", dtype=BF16)
-            c = torch.randn(40, 56, device="cuda", dtype=F32)
-            ref = c + a.float() @ b.float()
-            torch.addmm(c, a, b, out_dtype=F32, out=c)
-            _ADDMM_INPLACE_OK = bool(torch.allclose(c, ref, atol=1e-1, rtol=1e-2))
-        except Exception:  # pragma: no cover - depends on the ROCm build
-            _ADDMM_INPLACE_OK = False
-    return _ADDMM_INPLACE_OK
-
-
 def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     """dW = dy2^T @ x2 accumulated in fp32 (into ``p.main_grad`` when present).
 
-    On MI355X the accumulate runs in the GEMM itself — our split-K MFMA kernel
-    atomically adds fp32 partials into the flat gradient, or hipBLASLt's
-    fp32-output addmm (beta=1), whichever the per-shape tuner measured faster.
-    No bf16 dW and no separate accumulate pass either way."""
+    On MI355X the accumulate runs in the GEMM itself: our split-K MFMA kernel adds its
+    fp32 partial tiles straight into the flat gradient (no bf16 dW, no separate
+    accumulate pass)."""
     mg = getattr(p, "main_grad", None)
     if dy2.is_cuda and dy2.dtype == BF16:
         dy2 = dy2.contiguous()
         x2 = x2.contiguous()
         if mg is not None:
-            with _streams.fork(dy2, x2):  # beside the serial input-gradient chain
-                _tune.wgrad_acc(dy2, x2, mg)
+            _gd.wgrad_acc(dy2, x2, mg)
             notify_grad_ready(p)
             return None
         g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
-        _tune.wgrad_acc(dy2, x2, g)
+        _gd.wgrad_acc(dy2, x2, g)
         return g.to(p.dtype)
     g = dy2.t().float() @ x2.float()
     return _accumulate(p, g)
+
+
+def bias_grad(p, dy2: torch.Tensor):
+    """db = dy2.sum(0) accumulated in fp32 (into ``p.main_grad`` when present): our
+    column-sum kernel on MI355X."""
+    if p is None:
+        return None
+    mg = getattr(p, "main_grad", None)
+    if dy2.is_cuda and dy2.dtype == BF16:
+        dy2 = dy2.contiguous()
+        if mg is not None:
+            _gd.bias_grad_acc(dy2, mg)
+            notify_grad_ready(p)
+            return None
+        g = torch.zeros(p.shape, device=dy2.device, dtype=F32)
+        _gd.bias_grad_acc(dy2, g)
+        return g.to(p.dtype)
+    return _accumulate(p, dy2.float().sum(0))
 
 
 def new_seed() -> int:
@@ -130,7 +126,7 @@ def set_deterministic(flag: bool) -> None:
     reduce split-K partials in a fixed order and the embedding backward sums each vocab
     row's tokens in token order (no fp32 atomics anywhere on the step).  Every other
     kernel of the step is already order-deterministic."""
-    _tune.DETERMINISTIC = bool(flag)
+    _gd.DETERMINISTIC = bool(flag)
 
 
 def rng_set(device, value: int = 0) -> None:
@@ -156,9 +152,17 @@ def rng_advance(device) -> None:
 # dropout (hash-based on GPU: the mask is regenerated in backward, never stored)
 # ----------------------------------------------------------------------------
 
-def _cpu_keep_mask(shape, p, seed):
+def _cpu_keep_mask(shape, p, seed, device=None):
     g = torch.Generator().manual_seed(seed)
-    return torch.rand(shape, generator=g) >= p
+    m = torch.rand(shape, generator=g) >= p
+    return m if device is None else m.to(device)
+
+
+def _kern(t) -> bool:
+    """Whether an activation runs on our kernels: bf16 on the GPU.  fp32 / fp16 compute on
+    the GPU (``--dtype=float32`` / ``float16``) takes the plain torch reference path of each
+    op (the numerics contract, not the performance path)."""
+    return t.is_cuda and t.dtype == BF16
 
 
 class DropoutFn(torch.autograd.Function):
@@ -166,23 +170,23 @@ class DropoutFn(torch.autograd.Function):
     def forward(ctx, x, p):
         seed = new_seed()
         ctx.p, ctx.seed = p, seed
-        if x.is_cuda:
+        if _kern(x):
             y = torch.empty_like(x)
             xc = x.contiguous()
             _lib.call("nsa_dropout", _lib.ptr(xc), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
             return y
-        mask = _cpu_keep_mask(x.shape, p, seed)
+        mask = _cpu_keep_mask(x.shape, p, seed, x.device)
         return x * mask / (1.0 - p)
 
     @staticmethod
     def backward(ctx, dy):
-        if dy.is_cuda:
+        if _kern(dy):
             dx = torch.empty_like(dy)
             dyc = dy.contiguous()
             _lib.call("nsa_dropout", _lib.ptr(dyc), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
                       _lib.stream())
             return dx, None
-        mask = _cpu_keep_mask(dy.shape, ctx.p, ctx.seed)
+        mask = _cpu_keep_mask(dy.shape, ctx.p, ctx.seed, dy.device)
         return dy * mask / (1.0 - ctx.p), None
 
 
@@ -198,16 +202,17 @@ def dropout(x, p: float, training: bool):
 
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, idx, wte, wpe, p, dtype):
+    def forward(ctx, idx, wte, wpe, p, dtype, cdtype):
         B, T = idx.shape
         V, C = wte.shape
         seed = new_seed() if p > 0 else 0
         ctx.p, ctx.seed, ctx.shape = p, seed, (B, T, V, C)
+        ctx.kern = idx.is_cuda and cdtype == BF16
         # the kernels index idx as a dense [B*T] array in both passes: save the
         # contiguous copy (a sliced batch such as d[:, :-1] has row stride T+1)
         idx = idx.contiguous()
         ctx.save_for_backward(idx, wte, wpe)
-        if idx.is_cuda:
+        if ctx.kern:
             # bf16 weight shadows; the sum (the residual stream) is written in ``dtype``:
             # fp32 (nanoGPT autocast contract) or bf16
             assert C % 8 == 0, "embedding kernel needs n_embd % 8 == 0"
@@ -220,19 +225,19 @@ class EmbeddingFn(torch.autograd.Function):
             _lib.call("nsa_embedding_fwd_x32" if dtype == F32 else "nsa_embedding_fwd", _lib.ptr(idx),
                       _lib.ptr(wte_c), _lib.ptr(wpe_c), _lib.ptr(out), B * T, T, C, p, seed, _lib.stream())
             return out
-        x = wte.detach()[idx] + wpe.detach()[:T].unsqueeze(0)
+        # fp32 master weights, as nanoGPT's autocast leaves nn.Embedding in fp32
+        x = wte.detach().float()[idx] + wpe.detach().float()[:T].unsqueeze(0)
         if p > 0:
-            x = x * _cpu_keep_mask(x.shape, p, seed) / (1.0 - p)
+            x = x * _cpu_keep_mask(x.shape, p, seed, x.device) / (1.0 - p)
         return x.to(dtype)
 
     @staticmethod
     def backward(ctx, dx):
         idx, wte, wpe = ctx.saved_tensors
         B, T, V, C = ctx.shape
-        if dx.is_cuda:
+        if ctx.kern:
             assert idx.is_contiguous()
             dx = dx.contiguous()
-            _streams.join(dx.device)  # the tied lm_head weight gradient may still be on the side stream
             gwte = getattr(wte, "main_grad", None)
             gwpe = getattr(wpe, "main_grad", None)
             ret_wte = gwte is None
@@ -242,7 +247,7 @@ class EmbeddingFn(torch.autograd.Function):
             if ret_wpe:
                 gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
             assert dx.dtype in (F32, BF16)
-            if _tune.DETERMINISTIC:
+            if _gd.DETERMINISTIC:
                 # atomic-free: token positions stably sorted by id, one writer per vocab row
                 # segment starts by binary search over the sorted ids: no host sync
                 # (torch.bincount reads its max back to the host, which HIP-graph
@@ -261,19 +266,24 @@ class EmbeddingFn(torch.autograd.Function):
                 notify_grad_ready(wte)
             if not ret_wpe:
                 notify_grad_ready(wpe)
-            return None, out_wte, out_wpe, None, None
+            return None, out_wte, out_wpe, None, None, None
         d = dx.float()
         if ctx.p > 0:
-            d = d * _cpu_keep_mask(d.shape, ctx.p, ctx.seed) / (1.0 - ctx.p)
-        gwte = torch.zeros(V, C, dtype=F32)
+            d = d * _cpu_keep_mask(d.shape, ctx.p, ctx.seed, d.device) / (1.0 - ctx.p)
+        gwte = torch.zeros(V, C, dtype=F32, device=d.device)
         gwte.index_add_(0, idx.reshape(-1), d.reshape(-1, C))
-        gwpe = torch.zeros(wpe.shape[0], C, dtype=F32)
+        gwpe = torch.zeros(wpe.shape[0], C, dtype=F32, device=d.device)
         gwpe[:T] = d.sum(0)
-        return None, _accumulate(wte, gwte), _accumulate(wpe, gwpe), None, None
+        return None, _accumulate(wte, gwte), _accumulate(wpe, gwpe), None, None, None
 
 
-def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32):
-    return EmbeddingFn.apply(idx, wte, wpe, p if training else 0.0, dtype)
+def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32, cdtype=None):
+    """x = drop(wte[idx] + wpe[t]) in ``dtype`` (the residual stream).  ``cdtype``: the compute
+    dtype of the weights (default: bf16 on the GPU -> our kernel; anything else, or the CPU,
+    takes the fp32 torch path)."""
+    if cdtype is None:
+        cdtype = BF16 if idx.is_cuda else F32
+    return EmbeddingFn.apply(idx, wte, wpe, p if training else 0.0, dtype, cdtype)
 
 
 # ----------------------------------------------------------------------------
@@ -314,7 +324,8 @@ class LayerNormFn(torch.autograd.Function):
         ctx.passthrough = passthrough and y is None
         out_dtype = out_dtype or (y.dtype if y is not None else x.dtype)
         ctx.y_dtype = y.dtype if y is not None else None
-        if x.is_cuda:
+        ctx.kern = x.is_cuda and out_dtype == BF16
+        if ctx.kern:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
             x32 = x.dtype == F32
             assert x.dtype in (F32, BF16) and out_dtype == BF16, "layernorm kernel: bf16/fp32 stream, bf16 out"
@@ -369,7 +380,7 @@ class LayerNormFn(torch.autograd.Function):
             dyb = ds.to(ctx.y_dtype) if (ctx.fused and not ctx.passthrough) else None
             return ds, dyb, None, None, None, None
         dy2 = dh.reshape(-1, C)
-        if dh.is_cuda:
+        if ctx.kern:
             x32 = x2.dtype == F32
             dy2 = dy2.contiguous()
             ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
@@ -417,7 +428,7 @@ def _colsum_into(p, partial):
     """Reduce per-block partial column sums into p.main_grad (fused) or a fresh fp32 grad."""
     mg = getattr(p, "main_grad", None)
     rows, C = partial.shape
-    fn = "nsa_colsum_accum_ordered" if _tune.DETERMINISTIC else "nsa_colsum_accum"
+    fn = "nsa_colsum_accum_ordered" if _gd.DETERMINISTIC else "nsa_colsum_accum"
     if mg is not None:
         _lib.call(fn, _lib.ptr(partial), _lib.ptr(mg), rows, C, _lib.stream())
         notify_grad_ready(p)
@@ -449,7 +460,7 @@ def add_layer_norm(x, y, w, b, out_dtype=None):
 
 
 # ----------------------------------------------------------------------------
-# Linear: out = residual + x @ W^T + b     (GEMM on hipBLASLt, fp32 dW fused)
+# Linear: out = x @ W^T + b (+ residual)   (our MFMA GEMMs, bias in the epilogue, fp32 dW fused)
 # ----------------------------------------------------------------------------
 
 class LinearFn(torch.autograd.Function):
@@ -460,19 +471,16 @@ class LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         wc = compute_weight(w, x.dtype)
         bc = compute_weight(b, x.dtype) if b is not None else None
-        if residual is not None:
-            r2 = residual.reshape(-1, Nout)
-            base = r2 if bc is None else r2 + bc
-            out = torch.addmm(base, x2, wc.t())
-        elif bc is not None:
-            out = torch.addmm(bc, x2, wc.t())
-        elif x2.is_cuda and x2.dtype == BF16:
-            out = _tune.fwd(x2.contiguous(), wc)
+        if x2.is_cuda and x2.dtype == BF16:
+            out = _gd.fwd(x2.contiguous(), wc, bc)
         else:
             out = x2 @ wc.t()
-        ctx.has_bias = b is not None
+            if bc is not None:
+                out = out + bc
+        if residual is not None:  # (tests only: the model fuses its residual adds into LayerNorm)
+            out = out + residual.reshape(-1, Nout)
         ctx.has_residual = residual is not None
-        ctx.save_for_backward(x2, w, b if b is not None else w)
+        ctx.save_for_backward(x2, w, b)
         return out.view(*x.shape[:-1], Nout)
 
     @staticmethod
@@ -480,18 +488,13 @@ class LinearFn(torch.autograd.Function):
         x2, w, b = ctx.saved_tensors
         Nout = w.shape[0]
         d2 = dout.reshape(-1, Nout)
-        # input gradient first, then the weight gradient: with the side stream on
-        # (ops/streams.py) the weight GEMM then starts after this input-gradient GEMM
-        # and runs beside the memory-bound kernels that follow it on the main stream
         dx = None
         if ctx.needs_input_grad[0]:
             wc = compute_weight(w, d2.dtype)
-            dx = _tune.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
+            dx = _gd.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
             dx = dx.view(*dout.shape[:-1], x2.shape[-1])
         gw = weight_grad(w, d2, x2)
-        gb = None
-        if ctx.has_bias:
-            gb = _accumulate(b, d2.sum(0, dtype=F32))
+        gb = bias_grad(b, d2)
         dres = dout if ctx.has_residual else None
         return dx, gw, gb, dres
 
@@ -501,69 +504,47 @@ def linear(x, w, b=None, residual=None):
 
 
 # ----------------------------------------------------------------------------
-# MLP: c_proj(gelu(c_fc(x))) with GELU fused into GEMM epilogues (MI355X path)
+# MLP: c_proj(gelu(c_fc(x))) with the GELU in the GEMM epilogues (MI355X path)
 # ----------------------------------------------------------------------------
 
-# Whether the GELU rides in a GEMM epilogue is decided per shape by the tuner
-# (gemm_tune.fwd_gelu / dgrad_dgelu time the fused epilogues against the best GEMM +
-# the standalone GELU kernel).  FUSE_GELU_EPILOGUE=True forces the fused form
-# (tests/test_kernels_gpu.py::test_fused_mlp covers both).
-FUSE_GELU_EPILOGUE = False
-
-
 class MLPFn(torch.autograd.Function):
-    """c_proj(gelu(c_fc(x))) as ONE autograd node (bias-free GPT-2 configs).
+    """c_proj(gelu(c_fc(x) + b_fc)) + b_proj as ONE autograd node.
 
-    Forward: u = x W_fc^T, g = gelu(u), y = g W_proj^T.  Backward: dg = dy W_proj,
-    du = dg * gelu'(u), dx = du W_fc, and both weight gradients accumulated in fp32
-    by our split-K GEMM.  With FUSE_GELU_EPILOGUE the activation (forward) and its
-    derivative (backward) run inside the GEMM epilogues instead."""
+    Forward: the c_fc GEMM's epilogue adds b_fc and writes both u and g = gelu(u); the
+    c_proj GEMM adds b_proj.  Backward: du = (dy W_proj) * gelu'(u) from one GEMM epilogue,
+    dx = du W_fc, both weight gradients accumulated in fp32 by the split-K GEMM, bias
+    gradients by the column-sum kernel."""
 
     @staticmethod
-    def forward(ctx, x, w_fc, w_proj):
+    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
         C = x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
         wf = compute_weight(w_fc, x.dtype)
-        if FUSE_GELU_EPILOGUE:
-            u, g = _gemm.fwd_gelu(x2, wf)
-        else:
-            u, g = _tune.fwd_gelu(x2, wf)
-        y = _tune.fwd(g, compute_weight(w_proj, x.dtype))
-        ctx.save_for_backward(x2, u, g, w_fc, w_proj)
+        bf = compute_weight(b_fc, x.dtype) if b_fc is not None else None
+        bp = compute_weight(b_proj, x.dtype) if b_proj is not None else None
+        u, g = _gd.fwd_gelu(x2, wf, bf)
+        y = _gd.fwd(g, compute_weight(w_proj, x.dtype), bp)
+        ctx.save_for_backward(x2, u, g, w_fc, b_fc, w_proj, b_proj)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w_proj.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, u, g, w_fc, w_proj = ctx.saved_tensors
+        x2, u, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        wp = compute_weight(w_proj, dy.dtype)
-        if _streams.active(dy2) and not FUSE_GELU_EPILOGUE:
-            # side-stream order (ops/streams.py): each weight GEMM is forked right after
-            # an input-gradient GEMM, so it overlaps the memory-bound kernel that follows
-            # on the main stream (GELU backward here, the LayerNorm backward after dX)
-            out = {}
-            du = _tune.dgrad_dgelu(dy2, wp, u,
-                                   between=lambda: out.setdefault("gw", weight_grad(w_proj, dy2, g)))
-            dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
-            gw_fc = weight_grad(w_fc, du, x2)
-            return dx.view(ctx.xshape), gw_fc, out["gw"]
         gw_proj = weight_grad(w_proj, dy2, g)
-        if FUSE_GELU_EPILOGUE:
-            du = _gemm.dgrad(dy2, wp, u=u, wt=_tune._wt(wp))
-        else:
-            du = _tune.dgrad_dgelu(dy2, wp, u)
+        gb_proj = bias_grad(b_proj, dy2)
+        du = _gd.dgrad_dgelu(dy2, compute_weight(w_proj, dy.dtype), u)
         gw_fc = weight_grad(w_fc, du, x2)
-        dx = _tune.dgrad(du, compute_weight(w_fc, dy.dtype))
-        return dx.view(ctx.xshape), gw_fc, gw_proj
+        gb_fc = bias_grad(b_fc, du)
+        dx = _gd.dgrad(du, compute_weight(w_fc, dy.dtype))
+        return dx.view(ctx.xshape), gw_fc, gb_fc, gw_proj, gb_proj
 
 
 def mlp(x, w_fc, b_fc, w_proj, b_proj):
-    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X when bias-free."""
-    M = x.numel() // x.shape[-1]
-    if (x.is_cuda and x.dtype == BF16 and b_fc is None and b_proj is None and M % 64 == 0
-            and x.shape[-1] % 64 == 0 and w_fc.shape[0] % 64 == 0):
-        return MLPFn.apply(x, w_fc, w_proj)
+    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X (bf16)."""
+    if x.is_cuda and x.dtype == BF16:
+        return MLPFn.apply(x, w_fc, b_fc, w_proj, b_proj)
     return linear(gelu(linear(x, w_fc, b_fc)), w_proj, b_proj)
 
 
@@ -579,7 +560,7 @@ class GeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         ctx.save_for_backward(x)
-        if x.is_cuda:
+        if _kern(x):
             x = x.contiguous()
             y = torch.empty_like(x)
             _lib.call("nsa_gelu_fwd", _lib.ptr(x), _lib.ptr(y), x.numel(), _lib.stream())
@@ -589,7 +570,7 @@ class GeluFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
-        if dy.is_cuda:
+        if _kern(dy):
             dy = dy.contiguous()
             dx = torch.empty_like(x)
             _lib.call("nsa_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dx), x.numel(), _lib.stream())
@@ -649,7 +630,8 @@ class AttentionFn(torch.autograd.Function):
         seed = new_seed() if p > 0 else 0
         ctx.meta = (B, T, H, D, p, seed)
         scale = 1.0 / math.sqrt(D)
-        if qkv.is_cuda:
+        ctx.kern = _kern(qkv)
+        if ctx.kern:
             assert D in (32, 64, 128), "flash kernel supports head_dim 32/64/128"
             qkv = qkv.contiguous()
             y = torch.empty(B, T, C, device=qkv.device, dtype=qkv.dtype)
@@ -667,11 +649,10 @@ class AttentionFn(torch.autograd.Function):
     def backward(ctx, dy):
         B, T, H, D, p, seed = ctx.meta
         C = H * D
-        if dy.is_cuda:
+        if ctx.kern:
             qkv, y, lse = ctx.saved_tensors
             dy = dy.contiguous()
             dqkv = torch.empty_like(qkv)
-            _streams.before_compute(dy)
             # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
             # dQ is written once, in bf16, by its own kernel (no atomics)
             ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
@@ -886,17 +867,19 @@ def decode_embed_linear_ln(tok, pos, wte, wpe, ln_w, ln_b, w, b=None, dtype=BF16
     return decode_linear_ln(x, None, ln_w, ln_b, w, b, out_dtype=out_dtype)
 
 
-def sample_topk_(logits, temperature: float, top_k, salt: int, pos, tok, gen):
+def sample_topk_(logits, temperature: float, top_k, salt: int, pos, tok, gen, salt_dev=None):
     """Device-side nanoGPT sampling (logits / temperature, top-k, softmax, multinomial)
     of logits [B, V] fp32: the drawn ids go to ``tok`` [B, 1] and ``gen[:, pos]``
     (``pos``: int64 device scalar).  One kernel, graph-capturable; the uniform draw is a
-    counter hash of (salt, row, position), so a run is reproducible from its salt."""
+    counter hash of (salt ^ salt_dev, row, position), so a run is reproducible from its
+    salts.  ``salt_dev`` (int64 device scalar, optional) is read at run time: rewriting it
+    gives a captured sampling graph a fresh stream."""
     B, V = logits.shape
     k = 0 if top_k is None else min(int(top_k), V)
     if logits.is_cuda:
         lg = logits if logits.dtype == F32 and logits.stride(1) == 1 else logits.float().contiguous()
         _lib.call("nsa_sample_topk", _lib.ptr(lg), B, V, lg.stride(0), float(temperature), k, int(salt) & (2 ** 64 - 1),
-                  _lib.ptr(pos), _lib.ptr(tok), _lib.ptr(gen), gen.stride(0), _lib.stream())
+                  _lib.ptr(salt_dev), _lib.ptr(pos), _lib.ptr(tok), _lib.ptr(gen), gen.stride(0), _lib.stream())
         return
     lg = logits.float() / temperature
     if k > 0:
@@ -911,12 +894,59 @@ def sample_topk_(logits, temperature: float, top_k, salt: int, pos, tok, gen):
 # tied lm_head + cross-entropy (ignore_index=-1, mean over valid targets)
 # ----------------------------------------------------------------------------
 
+def lm_head_rows(V: int) -> int:
+    """Rows of the lm_head GEMM operand: V padded to a multiple of 64 (and >= 256, one NT
+    tile) so every vocabulary runs on the persistent GEMM kernel.  GPT-2's 50257 -> 50304
+    (the same padding nanoGPT's scratch config applies to the vocabulary itself); the
+    padding rows are zero and their logits are excluded from the softmax."""
+    return V if (V % 64 == 0 and V >= 256) else max(256, -(-V // 64) * 64)
+
+
+def _lm_weight(w):
+    """(bf16 [Vpad, C] operand, fp32 [Vpad, C] gradient view or None).  A FlatParamStore keeps
+    padded views of the tied weight (``compute_padded`` / ``main_grad_padded``); otherwise
+    the padded operand is a per-call copy and the gradient is returned to autograd."""
+    V, C = w.shape
+    Vp = lm_head_rows(V)
+    cp = getattr(w, "compute_padded", None)
+    if cp is not None and cp.dtype == BF16:
+        return cp, getattr(w, "main_grad_padded", None)
+    wc = compute_weight(w, BF16)
+    if Vp == V:
+        return wc, getattr(w, "main_grad", None)
+    wp = torch.zeros(Vp, C, device=w.device, dtype=BF16)
+    wp[:V] = wc
+    return wp, None
+
+
+def _lm_grad_out(w, gw, scratch):
+    """Finish the lm_head weight gradient: ``gw`` is the padded gradient view itself (already
+    accumulated), or a scratch [Vpad, C] buffer whose first V rows go to ``main_grad`` (or to
+    autograd when there is none)."""
+    V = w.shape[0]
+    if scratch:
+        mg = getattr(w, "main_grad", None)
+        if mg is None:
+            return gw[:V].to(w.dtype)
+        mg.add_(gw[:V])
+    notify_grad_ready(w)
+    return None
+
+
+def _fused_xent_ok(M, C, Vp):
+    return (not _gd.DETERMINISTIC and M % 4 == 0 and _gemm.nt_supported(M, Vp, C) and _gemm.nt_supported(M, C, Vp)
+            and C <= 8192)
+
+
 class LMHeadLossFn(torch.autograd.Function):
     """loss = cross_entropy(x @ wte^T, targets, ignore_index=-1).
 
-    GPU: the [N, V] bf16 logits buffer is overwritten in place by the fused
-    CE kernel with (softmax - onehot); backward applies grad/n_valid to the
-    small [N, C] side of each GEMM instead of re-scaling the [N, V] tensor.
+    GPU, fused (``csrc/kernels/xent_fused.hip``): the lm_head GEMM's epilogue writes
+    E = exp(logit - target logit) and per-tile row sums instead of the logits, so the
+    [N, V] logits are never stored and never re-read; the backward GEMMs consume E with
+    the softmax normalisation and the onehot term applied in fp32 in their epilogue / a
+    row-scatter.  GPU, deterministic mode or shapes outside the NT kernel: logits GEMM +
+    the separate cross-entropy pass that overwrites the logits with (softmax - onehot).
     """
 
     @staticmethod
@@ -925,19 +955,43 @@ class LMHeadLossFn(torch.autograd.Function):
         x2 = x.reshape(-1, C)
         t = targets.reshape(-1)
         N = x2.shape[0]
-        wc = compute_weight(w, x.dtype)
-        if x.is_cuda:
-            V = wc.shape[0]
-            logits = _tune.fwd(x2.contiguous(), wc)
-            row_loss = torch.empty(N, device=x.device, dtype=F32)
+        V = w.shape[0]
+        ctx.xshape = x.shape
+        ctx.V = V
+        if x.is_cuda and x.dtype == BF16:
+            x2 = x2.contiguous()
             t = t.contiguous()
-            _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t), _lib.ptr(row_loss), N, V,
-                      1 if need_grad else 0, _lib.stream())
-            n_valid = (t != -1).sum().to(F32)
-            loss = row_loss.sum() / n_valid
-            ctx.save_for_backward(x2, w, logits, n_valid)
-            ctx.xshape = x.shape
-            return loss
+            wp, _ = _lm_weight(w)
+            Vp = wp.shape[0]
+            row_loss = torch.empty(N, device=x.device, dtype=F32)
+            ctx.fused = _fused_xent_ok(N, C, Vp)
+            if ctx.fused:
+                crow = torch.empty(N, device=x.device, dtype=F32)
+                t32 = torch.empty(N, device=x.device, dtype=torch.int32)
+                _lib.call("nsa_xent_tlogit", _lib.ptr(x2), C, _lib.ptr(wp), C, _lib.ptr(t), _lib.ptr(crow),
+                          _lib.ptr(t32), N, C, V, _lib.stream())
+                slots = 2 * (-(-Vp // _gemm.TILE))
+                part = torch.empty(slots, N, device=x.device, dtype=F32)
+                e = _gemm.nt_xent(x2, wp, crow, part, V)
+                inv_s = torch.empty(N, device=x.device, dtype=F32)
+                nfix = torch.zeros(1, device=x.device, dtype=torch.int32)
+                fixlist = torch.empty(N, device=x.device, dtype=torch.int32)
+                _lib.call("nsa_xent_combine", _lib.ptr(part), slots, _lib.ptr(t32), _lib.ptr(row_loss),
+                          _lib.ptr(inv_s), _lib.ptr(nfix), _lib.ptr(fixlist), N, _lib.stream())
+                _lib.call("nsa_xent_fixup", _lib.ptr(x2), C, _lib.ptr(wp), C, _lib.ptr(e), Vp, _lib.ptr(t32),
+                          _lib.ptr(nfix), _lib.ptr(fixlist), _lib.ptr(row_loss), _lib.ptr(inv_s), C, V, Vp,
+                          _lib.stream())
+                n_valid = (t32 >= 0).sum().to(F32)
+                ctx.save_for_backward(x2, w, e, t32, inv_s, n_valid)
+            else:
+                logits = _gd.fwd(x2, wp)
+                _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t), _lib.ptr(row_loss), N, V, Vp,
+                          1 if need_grad else 0, _lib.stream())
+                n_valid = ((t >= 0) & (t < V)).sum().to(F32)
+                ctx.save_for_backward(x2, w, logits, n_valid)
+            return row_loss.sum() / n_valid
+        ctx.fused = False
+        wc = compute_weight(w, x.dtype)
         logits = x2.float() @ wc.float().t()
         logp = torch.log_softmax(logits, dim=-1)
         valid = t != -1
@@ -946,29 +1000,49 @@ class LMHeadLossFn(torch.autograd.Function):
         row_loss = -logp.gather(1, tt[:, None]).squeeze(1) * valid
         loss = row_loss.sum() / n_valid
         dlogits = logp.exp()
-        dlogits[torch.arange(N), tt] -= 1.0
+        dlogits[torch.arange(N, device=dlogits.device), tt] -= 1.0
         dlogits = dlogits * valid[:, None]
         ctx.save_for_backward(x2, w, dlogits, n_valid)
-        ctx.xshape = x.shape
         return loss
 
     @staticmethod
     def backward(ctx, gl):
+        V = ctx.V
+        if ctx.fused:
+            x2, w, e, t32, inv_s, n_valid = ctx.saved_tensors
+            N, C = x2.shape
+            wp, gwp = _lm_weight(w)
+            Vp = wp.shape[0]
+            g = (gl.float() / n_valid).reshape(1).contiguous()
+            coef = torch.empty(N, 2, device=x2.device, dtype=F32)
+            wrows = torch.empty(N, C, device=x2.device, dtype=BF16)
+            xs = torch.empty(N, C, device=x2.device, dtype=BF16)
+            _lib.call("nsa_xent_bwd_prep", _lib.ptr(x2), C, _lib.ptr(wp), C, _lib.ptr(t32), _lib.ptr(inv_s),
+                      _lib.ptr(g), _lib.ptr(coef), _lib.ptr(wrows), _lib.ptr(xs), N, C, _lib.stream())
+            dx = _gemm.nt_xdx(e, _gd._wt(wp), wrows, coef)
+            ret = gwp is None
+            gw = torch.zeros(Vp, C, device=x2.device, dtype=F32) if ret else gwp
+            _gd.wgrad_acc(e, xs, gw)
+            _lib.call("nsa_xent_dw_fix", _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32), _lib.ptr(inv_s), _lib.ptr(g),
+                      _lib.ptr(gw), C, N, C, _lib.stream())
+            return dx.view(ctx.xshape), _lm_grad_out(w, gw, ret), None, None
         x2, w, dlogits, n_valid = ctx.saved_tensors
         g = (gl.float() / n_valid)
-        wc = compute_weight(w, x2.dtype)
-        if x2.is_cuda:
+        if x2.is_cuda and x2.dtype == BF16:
             # the loss scale g = grad / n_valid stays fp32 (a device scalar read by the
             # kernel): only the scaled products are rounded to bf16, not g itself
+            wp, gwp = _lm_weight(w)
+            Vp = wp.shape[0]
             g = g.reshape(1).contiguous()
             xs = torch.empty_like(x2)
-            x2c = x2.contiguous()
-            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2c), _lib.ptr(xs), _lib.ptr(g), xs.numel(),
-                      _lib.stream())
-            dx = _tune.dgrad(dlogits, wc)
+            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2), _lib.ptr(xs), _lib.ptr(g), xs.numel(), _lib.stream())
+            dx = _gd.dgrad(dlogits, wp)
             _lib.call("nsa_scale_rows_bf16", _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())
-            gw = weight_grad(w, dlogits, xs)  # after dX: see LinearFn.backward
-            return dx.view(ctx.xshape), gw, None, None
+            ret = gwp is None
+            gw = torch.zeros(Vp, x2.shape[1], device=x2.device, dtype=F32) if ret else gwp
+            _gd.wgrad_acc(dlogits, xs, gw)
+            return dx.view(ctx.xshape), _lm_grad_out(w, gw, ret), None, None
+        wc = compute_weight(w, x2.dtype)
         dx = (dlogits @ wc.float()) * g
         gw = weight_grad(w, dlogits, x2.float() * g)
         return dx.to(x2.dtype).view(ctx.xshape), gw, None, None
@@ -983,5 +1057,10 @@ def lm_head_loss(x, w, targets):
 
 def lm_head_logits(x, w):
     """Inference-time logits for the given positions: x @ wte^T (fp32 result)."""
+    if x.is_cuda and x.dtype == BF16:
+        V, C = w.shape
+        wp, _ = _lm_weight(w)
+        y = _gd.fwd(x.reshape(-1, C).contiguous(), wp)
+        return y[:, :V].float().view(*x.shape[:-1], V)
     wc = compute_weight(w, x.dtype)
     return (x @ wc.t()).float()

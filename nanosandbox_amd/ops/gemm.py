@@ -1,13 +1,20 @@
-"""Python front-end of our gfx950 MFMA GEMMs.
+"""Python front-ends of our gfx950 MFMA GEMM kernels (no vendor library on any of them).
 
-* ``nt(a, b)``             C  = A · B^T   (both K-contiguous; ``csrc/kernels/gemm_nt.hip``):
-                                           every forward Y = X · W^T and, on the cached
-                                           weight transpose, every input grad dX = dY · W;
-                                           fused GELU / GELU' epilogues
-* ``fwd``, ``dgrad``, ``fwd_gelu``         convenience wrappers over ``nt``
-* ``wgrad_acc(dy, x, g)``  g += dY^T · X  (fp32; ``csrc/kernels/gemm.hip``) split over the
-                                           token dim, atomically accumulated into the flat
-                                           fp32 gradient (no bf16 dW)
+* ``nt(a, b, ...)``        C = A · B^T, both operands K-contiguous, on the persistent four-wave
+                           kernel (``csrc/kernels/gemm_nt4.hip``; M, N >= 256, K % 64 == 0,
+                           N % 8 == 0): every forward Y = X · W^T and, on the cached weight
+                           transpose, every input grad dX = dY · W.  Epilogues: bf16 (+ bias),
+                           u + gelu(u), acc · gelu'(U); the fused cross-entropy pair
+                           ``nt_xent`` / ``nt_xdx``.
+* ``small(a, b, ...)``     the same contract for any M, N (K % 8 == 0) on the bounds-checked
+                           64 x 64 kernel (``csrc/kernels/gemm_small.hip``): tiny models, short
+                           prefills, odd widths.
+* ``wgrad_acc(dy, x, g)``  g += dY^T · X in fp32, split over the token dim, accumulated straight
+                           into the flat fp32 gradient: the four-wave kernel
+                           (``csrc/kernels/gemm_wg4.hip``) when both output sides are >= 256,
+                           else the ring64 kernel (``csrc/kernels/gemm.hip``).
+
+Which of these runs for a given shape is a fixed rule in ``ops/gemm_dispatch.py``.
 """
 
 from __future__ import annotations
@@ -23,8 +30,6 @@ LAYOUT_TN = 2
 EPI_ATOMIC, EPI_STORE_F32 = 1, 4
 BK = 64
 TILE = 256
-# weight-grad variant (csrc/kernels/gemm.hip nsa_gemm): 1 = ring (32-deep slices), 7 = ring64 (default)
-VARIANT = int(os.environ.get("NSA_GEMM_VARIANT", "7"))
 
 
 def _check(t, name):
@@ -34,139 +39,139 @@ def _check(t, name):
         raise ValueError(f"{name} must be 16-byte aligned")
 
 
-def supported(M, N, K) -> bool:
-    return M % 8 == 0 and N % 8 == 0 and K % BK == 0 and M >= 8 and N >= 8
-
-
-WGRAD4 = 10  # variant id of the four-wave weight-grad kernel (csrc/kernels/gemm_wg4.hip)
-
-
-def _call(layout, epi, A, lda, B, ldb, C, ldc, M, N, K, splits=1, variant=None):
-    v = VARIANT if variant is None else variant
-    if v == WGRAD4 and M >= TILE and N >= TILE:
-        _lib.call("nsa_gemm_wgrad4", epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, M, N, K, splits,
-                  _lib.stream())
-        return
-    epi = epi | ((7 if v == WGRAD4 else v) << 8)
-    _lib.call("nsa_gemm", layout, epi, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc, None, None,
-              M, N, K, splits, _lib.stream())
-
-
-# ---------------------------------------------------------------------------------
-# Persistent NT kernel (csrc/kernels/gemm_nt.hip): forward and input grads, both
-# operands K-contiguous; the input grad uses the cached weight transpose.
-# ---------------------------------------------------------------------------------
 NT_EPI_BF16, NT_EPI_GELU, NT_EPI_DGELU = 0, 1, 2
 _NCU = {}
 
 
 def num_cus(device=None):
-    d = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    d = torch.cuda.current_device() if device is None else (torch.device(device).index or 0)
     if d not in _NCU:
         _NCU[d] = torch.cuda.get_device_properties(d).multi_processor_count
     return _NCU[d]
 
 
 def nt_supported(M, N, K) -> bool:
-    return M >= 256 and N >= 256 and K >= BK and K % BK == 0 and N % 8 == 0
+    """Shape rules of the persistent four-wave NT kernel."""
+    return M >= TILE and N >= TILE and K >= BK and K % BK == 0 and N % 8 == 0
 
 
-def nt4_supported(M, N, K) -> bool:
-    """Shape rules of the four-wave kernel (the same as the eight-wave kernel's)."""
-    return nt_supported(M, N, K)
+def small_supported(M, N, K) -> bool:
+    """Shape rules of the bounds-checked small-tile NT kernel."""
+    return M >= 1 and N >= 1 and K >= 8 and K % 8 == 0
+
+
+def wgrad4_supported(n_out, n_in, tokens) -> bool:
+    return n_out >= TILE and n_in >= TILE and n_out % 8 == 0 and n_in % 8 == 0 and tokens % BK == 0
+
+
+def wgrad_supported(n_out, n_in, tokens) -> bool:
+    return n_out >= 8 and n_in >= 8 and n_out % 8 == 0 and n_in % 8 == 0 and tokens % BK == 0 and tokens >= BK
 
 
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 
-def _nt_call(epi, A, B, C, M, N, K, C2=None, U=None, grid=None, probe=0, var=None, gm=0, w4=False):
-    var = NT_VAR if var is None else var
-    _lib.call("nsa_gemm_nt4" if w4 else "nsa_gemm_nt", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(A), A.stride(0), _lib.ptr(B), B.stride(0), _lib.ptr(C),
-              C.stride(0), _lib.ptr(C2), _lib.ptr(U), M, N, K, grid or num_cus(A.device), _lib.stream())
+def _out(M, N, device, out):
+    if out is None:
+        return torch.empty(M, N, device=device, dtype=BF16)
+    _check(out, "out")
+    return out
 
 
-def nt(a, b, epi=NT_EPI_BF16, u=None, grid=None, probe=0, var=None, gm=0, w4=False):
-    """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the persistent kernel
-    (``w4``: the four-wave kernel of gemm_nt4.hip, else the eight-wave gemm_nt.hip).
+def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, gm=0, out=None, out2=None):
+    """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the four-wave kernel.
 
-    epi NT_EPI_GELU returns (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u)."""
+    ``bias`` [N] (bf16) is added in the epilogue (before the GELU).  epi NT_EPI_GELU returns
+    (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u).  ``probe`` needs a library built
+    with -DNSA_PROBES (scripts/gemm_nt_ab.py)."""
     M, K = a.shape
     N = b.shape[0]
     _check(a, "a")
     _check(b, "b")
-    out = torch.empty(M, N, device=a.device, dtype=BF16)
-    if epi == NT_EPI_GELU:
-        act = torch.empty_like(out)
-        _nt_call(epi, a, b, out, M, N, K, C2=act, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
-        return out, act
+    if bias is not None:
+        _check(bias, "bias")
+    c = _out(M, N, a.device, out)
+    var = NT_VAR if var is None else var
+    c2 = (_out(M, N, a.device, out2)) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
         _check(u, "u")
-        _nt_call(epi, a, b, out, M, N, K, U=u, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
-        return out
-    _nt_call(epi, a, b, out, M, N, K, grid=grid, probe=probe, var=var, gm=gm, w4=w4)
-    return out
+    _lib.call("nsa_gemm_nt4", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
+              b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
+              grid or num_cus(a.device), _lib.stream())
+    return (c, c2) if epi == NT_EPI_GELU else c
 
 
-# the fixed-kernel entry points below use the four-wave kernel (faster on every GPT-2 shape,
-# docs/performance.md); the tuner (ops/gemm_tune.py) still races both against hipBLASLt
-def fwd(x2, w):
-    """Y = X · W^T (nn.Linear forward, bf16)."""
-    return nt(x2, w, w4=True)
+def small(a, b, epi=NT_EPI_BF16, u=None, bias=None, out=None, out2=None):
+    """The ``nt`` contract on the bounds-checked small-tile kernel (any M, N; K % 8 == 0)."""
+    M, K = a.shape
+    N = b.shape[0]
+    _check(a, "a")
+    _check(b, "b")
+    c = _out(M, N, a.device, out)
+    c2 = _out(M, N, a.device, out2) if epi == NT_EPI_GELU else None
+    if epi == NT_EPI_DGELU:
+        _check(u, "u")
+    _lib.call("nsa_gemm_small", epi, _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), _lib.ptr(c), c.stride(0),
+              _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K, _lib.stream())
+    return (c, c2) if epi == NT_EPI_GELU else c
 
 
-def fwd_gelu(x2, w):
-    """(u, gelu(u)) with u = x2 @ w^T, from one GEMM pass."""
-    return nt(x2, w, epi=NT_EPI_GELU, w4=True)
+def nt_xent(x, w, crow, part, nvalid, out=None):
+    """Fused cross-entropy forward GEMM: E = exp(x @ w^T - crow[:, None]) (bf16, columns >=
+    ``nvalid`` zero) and the per-half-tile row sums into ``part`` [2 * ceil(N / 256), M]."""
+    M, K = x.shape
+    N = w.shape[0]
+    _check(x, "x")
+    _check(w, "w")
+    e = _out(M, N, x.device, out)
+    _lib.call("nsa_gemm_nt4_xent", _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(e), e.stride(0),
+              _lib.ptr(crow), _lib.ptr(part), M, N, int(nvalid), K, num_cus(x.device), _lib.stream())
+    return e
 
 
-def dgrad(dy2, w, u=None, wt=None):
-    """dX = dY · W through W^T (``wt``, K-contiguous; transposed here when not given);
-    with ``u`` also multiplied by gelu'(u)."""
-    wt = w.t().contiguous() if wt is None else wt
-    if u is None:
-        return nt(dy2, wt, w4=True)
-    return nt(dy2, wt, epi=NT_EPI_DGELU, u=u, w4=True)
+def nt_xdx(e, wt, wrows, coef, out=None):
+    """Fused cross-entropy input gradient: coef[:, 0:1] * (e @ wt^T) - coef[:, 1:2] * wrows."""
+    M, K = e.shape
+    N = wt.shape[0]
+    _check(e, "e")
+    _check(wt, "wt")
+    _check(wrows, "wrows")
+    c = _out(M, N, e.device, out)
+    _lib.call("nsa_gemm_nt4_xdx", _lib.ptr(e), e.stride(0), _lib.ptr(wt), wt.stride(0), _lib.ptr(c), c.stride(0),
+              _lib.ptr(wrows), _lib.ptr(coef), M, N, K, num_cus(e.device), _lib.stream())
+    return c
+
+
+WGRAD_FILL = float(os.environ.get("NSA_WGRAD_FILL", "0.97"))
+WGRAD_SPLITS = int(os.environ.get("NSA_WGRAD_SPLITS", "0"))  # > 0: force a split count (A/B runs)
 
 
 def wgrad_splits(n_out, n_in, tokens, cus=256):
-    """Largest split count with at most two rounds of blocks (one 512-thread block per CU)."""
+    """Fixed K-split rule of the weight-gradient GEMMs (one 256 x 256 tile per workgroup).
+
+    Fewer output tiles than CUs: as many splits as fill one round of CUs (27 tiles -> 9,
+    36 -> 7, 9 -> 28).  Otherwise the fewest splits (<= 8) whose work items fill at least
+    ``WGRAD_FILL`` of their last round of CUs, else the best-filling count (the tied 124M
+    lm_head: 591 tiles x 3 = 1773 items = 99 % of 7 rounds).  These are the split counts
+    the round-3 start-up race picked on every GPT-2 shape (profiles/r3_bench_*.log)."""
+    if WGRAD_SPLITS > 0:
+        return max(1, min(WGRAD_SPLITS, max(1, tokens // BK)))
     tiles = -(-n_out // TILE) * -(-n_in // TILE)
     nkb = max(1, tokens // BK)
-    best = 1
-    for s in range(1, min(64, nkb) + 1):
-        if tiles * s <= 2 * cus:
-            best = s
+    if tiles < cus:
+        return max(1, min(cus // tiles, nkb))
+    best, best_fill = 1, -1.0
+    for s in range(1, min(8, nkb) + 1):
+        items = tiles * s
+        fill = items / (cus * -(-items // cus))
+        if fill >= WGRAD_FILL:
+            return s
+        if fill > best_fill + 1e-9:
+            best, best_fill = s, fill
     return best
 
 
-WGRAD_MAX_ROUNDS = int(os.environ.get("NSA_WGRAD_MAX_ROUNDS", "6"))
-
-
-def wgrad_splits_balanced(n_out, n_in, tokens, cus=256, max_rounds=None):
-    """Split count whose block count fills whole rounds of the CUs best.
-
-    The kernels take any split count (split z owns K blocks [z*n/S, (z+1)*n/S)),
-    so e.g. 27 output tiles x 28 splits = 756 blocks = 2.95 rounds (98 % of the
-    last round busy) instead of 27 x 16 = 432 = 1.69 rounds (the default rule).
-    Ties go to fewer splits (fewer fp32 atomics).
-    """
-    if max_rounds is None:
-        max_rounds = WGRAD_MAX_ROUNDS
-    tiles = -(-n_out // TILE) * -(-n_in // TILE)
-    nkb = max(1, tokens // BK)
-    best, best_eff = 1, -1.0
-    for s in range(1, min(128, nkb) + 1):
-        blocks = tiles * s
-        rounds = -(-blocks // cus)
-        if rounds > max_rounds:
-            break
-        eff = blocks / (rounds * cus)
-        if eff > best_eff + 1e-9:
-            best, best_eff = s, eff
-    return best
-
-
-def wgrad_acc(dy2, x2, g32, splits=None, variant=None, deterministic=False):
+def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False):
     """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel.
 
     Default: every K split adds its partial tile into g32 with fp32 atomics (arrival
@@ -181,12 +186,33 @@ def wgrad_acc(dy2, x2, g32, splits=None, variant=None, deterministic=False):
     _check(g32, "grad")
     if splits is None:
         splits = wgrad_splits(N_out, K_in, T)
+    four = wgrad4_supported(N_out, K_in, T)
+
+    def launch(epi, C):
+        if four:
+            _lib.call("nsa_gemm_wgrad4", epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(C),
+                      K_in, N_out, K_in, T, splits, _lib.stream())
+        else:
+            _lib.call("nsa_gemm", LAYOUT_TN, epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
+                      _lib.ptr(C), K_in, None, None, N_out, K_in, T, splits, _lib.stream())
+
     if deterministic and splits > 1:
         ws = torch.empty(splits, N_out, K_in, device=g32.device, dtype=torch.float32)
-        _call(LAYOUT_TN, EPI_STORE_F32, dy2, N_out, x2, K_in, ws, K_in, N_out, K_in, T, splits=splits,
-              variant=variant)
+        launch(EPI_STORE_F32, ws)
         _lib.call("nsa_splitk_reduce", _lib.ptr(ws), _lib.ptr(g32), g32.numel(), splits, _lib.stream())
         return g32
-    _call(LAYOUT_TN, EPI_ATOMIC, dy2, N_out, x2, K_in, g32, K_in, N_out, K_in, T, splits=splits,
-          variant=variant)
+    launch(EPI_ATOMIC, g32)
     return g32
+
+
+def bias_grad_acc(dy2, gb32, deterministic=False):
+    """gb32 (fp32 [N]) += column sums of dy2 [T, N] (bf16): one partial pass over row slices
+    plus the column reduction into the gradient (ordered in deterministic mode)."""
+    T, N = dy2.shape
+    _check(dy2, "dy")
+    nblk = max(1, min(256, T // 64))
+    part = torch.empty(nblk, N, device=dy2.device, dtype=torch.float32)
+    _lib.call("nsa_colsum_bf16_partial", _lib.ptr(dy2), dy2.stride(0), T, N, _lib.ptr(part), nblk, _lib.stream())
+    _lib.call("nsa_colsum_accum_ordered" if deterministic else "nsa_colsum_accum", _lib.ptr(part), _lib.ptr(gb32),
+              nblk, N, _lib.stream())
+    return gb32

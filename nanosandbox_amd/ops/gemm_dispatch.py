@@ -1,0 +1,179 @@
+"""Fixed, shape-derived GEMM kernel selection for every training GEMM (no vendor library).
+
+One native kernel family per op, chosen by the operand shapes alone, identical in every run,
+on every box and on every DDP rank (no start-up timing race, nothing to agree on):
+
+============================  ==============================================  ==========================
+op                            shape rule                                      kernel
+============================  ==============================================  ==========================
+forward Y = X·W^T (+ b)       M, N >= 256, K % 64 == 0, N % 8 == 0            ``gemm_nt4.hip`` (persistent)
+  (c_fc: u and gelu(u))       otherwise, K % 8 == 0                           ``gemm_small.hip``
+input grad dX = dY·W          the same rules on dY · (W^T)^T, W^T cached      as above
+  (mlp.c_proj: · gelu'(u))
+weight grad dW += dY^T·X      both output sides >= 256                        ``gemm_wg4.hip`` (split-K)
+  (fp32, into the flat grad)  otherwise (sides >= 8)                          ``gemm.hip`` ring64
+bias grad db += colsum(dY)    any                                             ``optim.hip`` colsum
+============================  ==============================================  ==========================
+
+Anything outside every rule (K % 8 != 0, a side < 8, fp32 inputs) is out of the kernels'
+contract and runs as a plain torch matmul — no GPT configuration in ``config/`` reaches it
+(``tests/test_dispatch_cpu.py`` enumerates them).  The round-3 runtime race against hipBLASLt
+(``NSA_GEMM_BACKEND`` / TunableOp tables) is gone: its last library wins were 1-5 % on four
+shapes (docs/performance.md), and it made the kernel set depend on the box.
+
+Env knobs for A/B experiments only: ``NSA_WGRAD_SPLITS`` (force a weight-grad split count),
+``NSA_WGRAD_FILL`` (the split rule's round-fill threshold), ``NSA_NT_STORE`` (epilogue store
+policy).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import gemm as _gemm
+
+F32 = torch.float32
+BF16 = torch.bfloat16
+
+# Deterministic mode (config key ``deterministic``, ops.set_deterministic): weight gradients
+# reduce their K splits in a fixed order (no fp32 atomics); the embedding backward and the
+# lm_head loss switch to their sorted / atomic-free paths.
+DETERMINISTIC = False
+
+
+def _ok(*ts):
+    return all(t.is_cuda and t.dtype == BF16 and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def kernel_for(op: str, M: int, N: int, K: int) -> str:
+    """The kernel the rule picks for a GEMM of this shape ("nt4", "small", "wgrad4", "ring64",
+    "torch").  ``op``: "fwd" / "dgrad" (C[M, N] = A[M, K] · B^T) or "wgrad" (M = output rows,
+    N = input features, K = tokens)."""
+    if op == "wgrad":
+        if _gemm.wgrad4_supported(M, N, K):
+            return "wgrad4"
+        return "ring64" if _gemm.wgrad_supported(M, N, K) else "torch"
+    if _gemm.nt_supported(M, N, K):
+        return "nt4"
+    return "small" if _gemm.small_supported(M, N, K) else "torch"
+
+
+_used: dict = {}
+
+
+def kernels_used() -> dict:
+    """{(op, M, N, K): kernel} of every GEMM shape this process has run (bench / logs)."""
+    return dict(_used)
+
+
+def _nt(a, b, epi=_gemm.NT_EPI_BF16, u=None, bias=None, op="fwd"):
+    M, K = a.shape
+    N = b.shape[0]
+    k = kernel_for("fwd", M, N, K) if _ok(a, b) and (bias is None or _ok(bias)) else "torch"
+    _used.setdefault((op, M, N, K), k)
+    if k == "nt4":
+        return _gemm.nt(a, b, epi=epi, u=u, bias=bias)
+    if k == "small":
+        return _gemm.small(a, b, epi=epi, u=u, bias=bias)
+    y = a @ b.t()
+    if bias is not None:
+        y = y + bias
+    if epi == _gemm.NT_EPI_GELU:
+        return y, _gelu_torch(y)
+    if epi == _gemm.NT_EPI_DGELU:
+        return (y.float() * _gelu_grad_torch(u.float())).to(y.dtype)
+    return y
+
+
+def _gelu_torch(u):
+    return torch.nn.functional.gelu(u.float()).to(u.dtype)
+
+
+def _gelu_grad_torch(uf):
+    cdf = 0.5 * (1.0 + torch.erf(uf * 0.7071067811865476))
+    return cdf + uf * torch.exp(-0.5 * uf * uf) * 0.3989422804014327
+
+
+def fwd(x2, w, b=None):
+    """y = x2 @ w^T (+ b), bf16."""
+    return _nt(x2, w, bias=b)
+
+
+def fwd_gelu(x2, w, b=None):
+    """(u, gelu(u)) with u = x2 @ w^T (+ b), both from one GEMM epilogue."""
+    return _nt(x2, w, epi=_gemm.NT_EPI_GELU, bias=b, op="fwd_gelu")
+
+
+def dgrad(dy2, w):
+    """dx = dy2 @ w (bf16), through the cached K-contiguous w^T."""
+    return _nt(dy2, _wt(w), op="dgrad")
+
+
+def dgrad_dgelu(dy2, w, u):
+    """(dy2 @ w) * gelu'(u) from one GEMM epilogue."""
+    return _nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, op="dgrad_dgelu")
+
+
+def wgrad_acc(dy2, x2, g32):
+    """g32 += dy2^T @ x2 in fp32 (g32: a view of the flat gradient, or a fresh buffer)."""
+    T, N = dy2.shape
+    K = x2.shape[1]
+    k = kernel_for("wgrad", N, K, T) if _ok(dy2, x2) and g32.is_contiguous() else "torch"
+    _used.setdefault(("wgrad", N, K, T), k if k == "torch" else f"{k}/s{_gemm.wgrad_splits(N, K, T)}")
+    if k != "torch":
+        _gemm.wgrad_acc(dy2, x2, g32, deterministic=DETERMINISTIC)
+        return
+    g32.add_(dy2.t().float() @ x2.float())
+
+
+def bias_grad_acc(dy2, gb32):
+    """gb32 += dy2.sum(0) in fp32."""
+    if _ok(dy2) and dy2.shape[1] % 8 == 0 and gb32.is_contiguous():
+        _gemm.bias_grad_acc(dy2, gb32, deterministic=DETERMINISTIC)
+        return
+    gb32.add_(dy2.float().sum(0))
+
+
+# Weight generation: bumped whenever the bf16 compute weights are rewritten outside
+# torch's in-place ops (fused AdamW kernel, FlatParamStore.refresh_compute), so cached
+# derived copies of a weight (its transpose, below) are rebuilt once per optimizer step.
+_weight_gen = 0
+
+
+def weights_changed():
+    global _weight_gen
+    _weight_gen += 1
+
+
+def _wt(w):
+    """w^T as a contiguous tensor, cached on the weight tensor for the current generation.
+
+    The input gradient dX = dY · W runs on the NT kernel, whose B operand must be
+    K-contiguous: W^T.  Transposing a weight costs microseconds and is amortised over every
+    micro-step of an optimizer step.  Inside HIP-graph capture the transpose is recomputed
+    (captured into the graph) instead of cached."""
+    if w.is_cuda and torch.cuda.is_current_stream_capturing():
+        return _transpose(w)
+    key = (_weight_gen, w._version, w.data_ptr())
+    hit = getattr(w, "_nsa_wt", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    t = _transpose(w, out=hit[1] if hit is not None else None)  # rebuilt in place each step
+    try:
+        w._nsa_wt = (key, t)
+    except (AttributeError, RuntimeError):
+        pass
+    return t
+
+
+def _transpose(w, out=None):
+    """w^T, contiguous: our bf16 transpose kernel (LDS-free 8x8 register blocks) when the
+    shape allows, else torch's copy."""
+    R, C = w.shape
+    if w.is_cuda and w.dtype == BF16 and R % 64 == 0 and C % 64 == 0 and w.is_contiguous():
+        if out is None or out.shape != (C, R) or out.dtype != w.dtype or out.device != w.device:
+            out = torch.empty(C, R, device=w.device, dtype=w.dtype)
+        _lib.call("nsa_transpose_bf16", _lib.ptr(w), _lib.ptr(out), R, C, _lib.stream())
+        return out
+    return w.t().contiguous()

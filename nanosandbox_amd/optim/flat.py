@@ -15,6 +15,10 @@ win is in the number and size of passes):
 * ``wd_mask`` — one byte per 64-element chunk: 1 where weight decay applies
   (nanoGPT rule: tensors with ``dim >= 2``).  Each parameter is padded to a
   multiple of 64 elements so a chunk never straddles two parameters.
+* row padding — a parameter tagged ``_nsa_pad_rows = R`` (the tied wte / lm_head weight
+  of a vocabulary that is not a multiple of 64, e.g. GPT-2's 50257) gets R rows of room;
+  ``param.compute_padded`` / ``param.main_grad_padded`` view them as [R, C] for the lm_head
+  GEMMs.  The extra rows start at zero and stay zero (zero gradient, zero AdamW update).
 
 Parameters are laid out in *reverse registration order*, which is the order
 their gradients become final during backward (ln_f, last block ... first
@@ -49,7 +53,9 @@ class FlatParamStore:
         off = 0
         for name, p in reversed(named):
             n = p.numel()
-            padded = (n + CHUNK - 1) // CHUNK * CHUNK
+            rows = getattr(p, "_nsa_pad_rows", None)
+            room = rows * p.shape[1] if rows and p.dim() == 2 and rows > p.shape[0] else n
+            padded = (room + CHUNK - 1) // CHUNK * CHUNK
             self.slots.append(ParamSlot(name, p, off, n, padded, p.dim() >= 2))
             off += padded
         self.numel = off
@@ -69,6 +75,9 @@ class FlatParamStore:
             g = self.grad[s.offset:s.offset + s.numel].view(s.param.shape)
             if fused_grad:
                 s.param.main_grad = g
+                pr = self._pad_shape(s)
+                if pr is not None:
+                    s.param.main_grad_padded = self.grad[s.offset:s.offset + pr[0] * pr[1]].view(pr)
             else:
                 s.param.grad = g
         self.compute_dtype = compute_dtype
@@ -77,7 +86,17 @@ class FlatParamStore:
             self.compute = torch.empty(off, dtype=compute_dtype, device=self.device)
             for s in self.slots:
                 s.param.compute = self.compute[s.offset:s.offset + s.numel].view(s.param.shape)
+                pr = self._pad_shape(s)
+                if pr is not None:
+                    s.param.compute_padded = self.compute[s.offset:s.offset + pr[0] * pr[1]].view(pr)
             self.refresh_compute()
+
+    @staticmethod
+    def _pad_shape(s: ParamSlot):
+        rows = getattr(s.param, "_nsa_pad_rows", None)
+        if rows and s.param.dim() == 2 and rows > s.param.shape[0]:
+            return (rows, s.param.shape[1])
+        return None
 
     # ----------------------------------------------------------------- views
     def slot_of(self, p) -> ParamSlot:
@@ -93,8 +112,8 @@ class FlatParamStore:
     @torch.no_grad()
     def refresh_compute(self):
         """Re-derive the bf16 compute shadow from the fp32 master (after load/broadcast)."""
-        from ..ops import gemm_tune
-        gemm_tune.weights_changed()
+        from ..ops import gemm_dispatch
+        gemm_dispatch.weights_changed()
         if self.compute is None:
             return
         if self.device.type == "cuda":
@@ -106,9 +125,6 @@ class FlatParamStore:
 
     @torch.no_grad()
     def zero_grad(self):
-        if self.grad.is_cuda:
-            from ..ops import streams
-            streams.join(self.grad.device)  # no side-stream accumulate may land after the zero
         self.grad.zero_()
         if not self.fused_grad:
             # torch DDP / plain autograd path: keep .grad pointing at the flat buffer

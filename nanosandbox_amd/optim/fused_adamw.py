@@ -82,8 +82,7 @@ class FusedAdamW:
         Returns the pre-clip total norm as a 1-element device tensor (no sync)."""
         g = self.store.grad
         if self._is_gpu:
-            from ..ops import _lib, streams
-            streams.join(g.device)  # weight gradients may still be accumulating on the side stream
+            from ..ops import _lib
             _lib.call("nsa_sumsq_partial", _lib.ptr(g), g.numel(), _lib.ptr(self._partial), _NORM_BLOCKS,
                       _lib.stream())
             _lib.call("nsa_clip_coef", _lib.ptr(self._partial), _NORM_BLOCKS, float(self.grad_scale),
@@ -109,9 +108,8 @@ class FusedAdamW:
         bc2_sqrt = math.sqrt(1.0 - beta2 ** t)
         st = self.store
         if self._is_gpu:
-            from ..ops import _lib, gemm_tune, streams
-            streams.join(st.grad.device)
-            gemm_tune.weights_changed()  # the kernel rewrites the bf16 compute weights
+            from ..ops import _lib, gemm_dispatch
+            gemm_dispatch.weights_changed()  # the kernel rewrites the bf16 compute weights
             _lib.call("nsa_adamw_step", _lib.ptr(st.master), _lib.ptr(st.grad), _lib.ptr(self.exp_avg),
                       _lib.ptr(self.exp_avg_sq), _lib.ptr(st.compute), _lib.ptr(st.wd_mask), st.numel,
                       float(lr), float(beta1), float(beta2), float(eps), float(wd), float(bc1), float(bc2_sqrt),
@@ -128,8 +126,8 @@ class FusedAdamW:
         p.addcdiv_(m, denom, value=-lr / bc1)
         if st.compute is not None:
             st.compute.copy_(p)
-            from ..ops import gemm_tune
-            gemm_tune.weights_changed()
+            from ..ops import gemm_dispatch
+            gemm_dispatch.weights_changed()
 
     def zero_grad(self, set_to_none: bool = True):
         # the flat buffer is persistent (gradient views, bucket views) -> zero instead of None

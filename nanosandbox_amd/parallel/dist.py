@@ -100,9 +100,12 @@ _rccl_log_dir = None
 
 def enable_transport_log() -> str | None:
     """Route RCCL's INIT-subsystem log to a per-process file (before the communicator
-    exists).  User-set NCCL_DEBUG / NCCL_DEBUG_FILE win; NSA_RCCL_TRANSPORT_LOG=0 opts out."""
+    exists).  A user who set NCCL_DEBUG or NCCL_DEBUG_FILE keeps their own log untouched (the
+    transport then reads 'unknown'); NSA_RCCL_TRANSPORT_LOG=0 opts out.  The file's directory
+    is removed once ``report_transport`` has read it."""
     global _rccl_log_dir
-    if os.environ.get("NSA_RCCL_TRANSPORT_LOG", "1") == "0" or "NCCL_DEBUG_FILE" in os.environ:
+    if (os.environ.get("NSA_RCCL_TRANSPORT_LOG", "1") == "0" or "NCCL_DEBUG_FILE" in os.environ
+            or "NCCL_DEBUG" in os.environ):
         return None
     import tempfile
     _rccl_log_dir = tempfile.mkdtemp(prefix="nsa_rccl_")
@@ -124,10 +127,11 @@ def parse_transports(lines) -> dict:
 
 
 def transport_kind(counts: dict) -> str:
-    """Collapse transport names to P2P / SHM / NET / none / mixed."""
+    """Collapse transport names to P2P / SHM / NET / mixed; 'unknown' when no channel line
+    was parsed (log not captured)."""
     kinds = {k.split("/")[0] for k in counts}
     if not kinds:
-        return "none"
+        return "unknown"
     return kinds.pop() if len(kinds) == 1 else "mixed:" + "+".join(sorted(kinds))
 
 
@@ -166,6 +170,7 @@ def report_transport(info: "DistInfo", nbytes: int = 64 << 20, iters: int = 5, v
     n = info.world_size
     busbw = 2 * (n - 1) / n * nbytes / dt / 1e9
     counts = parse_transports(_own_log_lines()) if be == "nccl" else {"gloo": 1}
+    _drop_transport_log()
     gathered = [None] * n
     dist.all_gather_object(gathered, {"rank": info.rank, "transports": counts})
     rep = {"backend": be, "preset": os.environ.get("NSA_RCCL_PRESET", "xgmi"), "world": n,
@@ -175,11 +180,19 @@ def report_transport(info: "DistInfo", nbytes: int = 64 << 20, iters: int = 5, v
     if info.rank == 0 and verbose:
         print("rccl: " + json.dumps(rep), flush=True)
         want = PRESET_TRANSPORT.get(rep["preset"])
-        bad = {r: k for r, k in rep["transport"].items() if k != want}
+        bad = {r: k for r, k in rep["transport"].items() if k not in (want, "unknown")}
         if be == "nccl" and want and bad:
             print(f"WARNING: NSA_RCCL_PRESET={rep['preset']} expects {want} but RCCL picked {bad}; "
                   "see docs/rccl.md 'Which transport each topology gets'", flush=True)
     return rep
+
+
+def _drop_transport_log():
+    global _rccl_log_dir
+    if _rccl_log_dir is not None:
+        import shutil
+        shutil.rmtree(_rccl_log_dir, ignore_errors=True)
+        _rccl_log_dir = None
 
 
 def allreduce_sweep(info: "DistInfo", sizes_mib=(4, 16, 64, 256), iters: int = 3, verbose: bool = True) -> list:

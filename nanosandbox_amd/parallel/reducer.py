@@ -30,12 +30,10 @@ flat fp32 master buffer.
 
 from __future__ import annotations
 
-import contextlib
 
 import torch
 import torch.distributed as dist
 
-from ..ops import streams as _streams
 from ..optim.flat import FlatParamStore
 
 
@@ -115,21 +113,11 @@ class FlatBucketReducer:
 
     def _launch(self, b: _Bucket):
         flat = self.store.grad[b.start:b.end]
-        # weight gradients accumulate on the side stream (ops/streams.py): issue the
-        # all-reduce from there, after the side stream has also caught up with the main
-        # stream's accumulates (LayerNorm / bias grads), so RCCL sees a complete bucket
-        # without stalling the main stream's input-gradient chain
-        ctx = contextlib.nullcontext()
-        if flat.is_cuda and _streams.active(flat):
-            side = _streams.side_stream(flat.device)
-            side.wait_stream(torch.cuda.current_stream(flat.device))
-            ctx = torch.cuda.stream(side)
-        with ctx:
-            if self.reduce_dtype == torch.float32:
-                b.comm_buf = flat
-            else:
-                b.comm_buf = flat.to(self.reduce_dtype)
-            b.work = dist.all_reduce(b.comm_buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.reduce_dtype == torch.float32:
+            b.comm_buf = flat
+        else:
+            b.comm_buf = flat.to(self.reduce_dtype)
+        b.work = dist.all_reduce(b.comm_buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     @torch.no_grad()
     def finish(self):
@@ -143,14 +131,11 @@ class FlatBucketReducer:
         for b in self.buckets:
             b.count = max(b.count, b.expected)
         self._launch_ready()
-        _streams.join(self.store.grad.device if self.store.grad.is_cuda else None)
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
                 if b.comm_buf is not None and b.comm_buf.data_ptr() != self.store.grad[b.start:].data_ptr():
                     self.store.grad[b.start:b.end].copy_(b.comm_buf)
-                    if b.comm_buf.is_cuda:  # allocated on the side stream, read here on the main one
-                        b.comm_buf.record_stream(torch.cuda.current_stream(b.comm_buf.device))  # one per bucket
                 b.work = None
                 b.comm_buf = None
         self.armed = False

@@ -57,6 +57,9 @@ class Decoder:
         # generated tokens by position: gen[:, p] is the token fed at position p
         self.gen = torch.zeros(batch_size, self.T + 1, device=self.device, dtype=torch.int64)
         self.salt = int(torch.randint(0, 2 ** 62, (1,)).item())  # sampling stream (torch.manual_seed governs)
+        # per-call part of the sampling stream, read by the kernel at run time (so a captured
+        # sampling graph, reused across generate calls, draws independent samples each call)
+        self.salt_dev = torch.zeros(1, device=self.device, dtype=torch.int64)
         self.use_graph = (self.device.type == "cuda") if use_graph is None else use_graph
         if self.use_graph and not self.graph_capable(model):
             # the fused decode kernels cover head_dim 64, bf16 and V <= 53248; the fallback
@@ -152,7 +155,7 @@ class Decoder:
         B, T0 = idx.shape
         assert B == self.B and 1 <= T0 <= self.T
         tr = self.model.transformer
-        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.rdtype)
+        x = ops.embedding(idx, tr.wte.weight, tr.wpe.weight, 0.0, False, dtype=self.rdtype, cdtype=self.dtype)
         h = self._prefill_layers(x)
         self.pos.fill_(T0)
         return ops.lm_head_logits(h[:, [-1], :], self.model.lm_head.weight)[:, 0]
@@ -196,7 +199,11 @@ class Decoder:
     def sample_into(self, logits, temperature, top_k):
         """Draw the next token of every row from ``logits`` [B, V] into ``tok`` and
         ``gen[:, pos]`` (device kernel on the GPU: ``ops.sample_topk_``)."""
-        ops.sample_topk_(logits, temperature, top_k, self.salt, self.pos, self.tok, self.gen)
+        ops.sample_topk_(logits, temperature, top_k, self.salt, self.pos, self.tok, self.gen, salt_dev=self.salt_dev)
+
+    def reseed(self):
+        """A fresh sampling stream for the next generate call (torch.manual_seed governs)."""
+        self.salt_dev.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
 
     def _step_sample_impl(self, temperature, top_k):
         self.sample_into(self._step_impl(), temperature, top_k)  # pos is now p + 1
@@ -256,6 +263,7 @@ def generate_cached(model, idx: torch.Tensor, max_new_tokens: int, temperature: 
     own = decoder is None or decoder.B != B
     dec = Decoder(model, B, max_len=model.config.block_size, use_graph=use_graph) if own else decoder
     try:
+        dec.reseed()  # every call draws its own samples, also on a reused decoder / graph
         dec.sample_into(dec.prefill(idx), temperature, top_k)  # pos = T0: gen[:, T0]
         dec.run(max_new_tokens - 1, temperature, top_k)
         return torch.cat([idx, dec.gen[:, T0:T0 + max_new_tokens]], dim=1)

@@ -37,13 +37,20 @@ from .parallel import FlatBucketReducer, destroy, init_distributed
 from .utils import MetricsLogger, get_lr, load_checkpoint, load_model_state, save_checkpoint
 
 
+_DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}
+
+
 def _compute_dtype(device_type: str, dtype: str) -> torch.dtype:
+    """nanoGPT's ``dtype`` key: 'bfloat16' (default on MI355X), 'float16' (with a dynamic loss
+    scale) or 'float32'.  On the GPU bf16 runs our HIP kernels; fp16 and fp32
+    run every op's torch reference implementation (the numerics contract, at library speed:
+    gfx950's fp16 MFMA rate equals bf16's, so fp16 buys nothing but the scaler here).  The
+    CPU always computes in fp32 (nanoGPT: nullcontext on CPU)."""
+    if dtype not in _DTYPES:
+        raise ValueError(f"dtype must be one of {sorted(_DTYPES)}, got {dtype!r}")
     if device_type != "cuda":
-        return torch.float32  # nanoGPT: nullcontext on CPU -> fp32
-    if dtype in ("bfloat16", "float16"):
-        # MI355X runs bf16 and fp16 MFMA at the same rate; bf16 needs no GradScaler
-        return torch.bfloat16
-    raise NotImplementedError("GPU path computes in bf16 (MFMA); use --dtype=bfloat16")
+        return torch.float32
+    return _DTYPES[dtype]
 
 
 class Trainer:
@@ -66,10 +73,14 @@ class Trainer:
             os.makedirs(c["out_dir"], exist_ok=True)
         torch.manual_seed(c["seed"] + info.seed_offset)
         self.compute_dtype = _compute_dtype(self.device_type, c["dtype"])
-        if self.device_type == "cuda":
-            from .ops import blas_tuning
-            if blas_tuning.enable():
-                print(f"library GEMMs: tuned solution table {os.path.basename(blas_tuning.DEFAULT_FILE)}")
+        # nanoGPT: GradScaler(enabled=(dtype == 'float16')) -- a no-op off the GPU
+        self.scaler = None
+        if self.compute_dtype == torch.float16:
+            from .optim.loss_scale import DynamicLossScale
+            self.scaler = DynamicLossScale()
+        if self.device_type == "cuda" and self.compute_dtype != torch.bfloat16 and self.master:
+            print(f"dtype={c['dtype']}: torch reference ops (HIP kernels run bf16 only)"
+                  + (", dynamic loss scale" if self.scaler else ""))
 
         # ---------------------------------------------------------------- data
         self.data_dir = resolve_data_dir(c["dataset"], c["data_dir"])
@@ -131,7 +142,7 @@ class Trainer:
         self.ddp_impl = c["ddp_impl"] if info.ddp else "none"
         fused_grad = self.ddp_impl != "torch"
         self.store = FlatParamStore(model, self.device,
-                                    compute_dtype=self.compute_dtype if self.device_type == "cuda" else None,
+                                    compute_dtype=torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None,
                                     fused_grad=fused_grad)
         self.optimizer = model.configure_optimizers(c["weight_decay"], c["learning_rate"], (c["beta1"], c["beta2"]),
                                                     self.device_type, store=self.store)
@@ -156,6 +167,8 @@ class Trainer:
         self.use_graph = False
         if c["compile"]:
             ok, why = graph_capture_supported(self.device, c["dropout"], info.world_size, self.ddp_impl, self.gas)
+            if ok and self.compute_dtype != torch.bfloat16:
+                ok, why = False, f"dtype={c['dtype']} runs the torch reference ops"
             self.use_graph = ok
             if self.master:
                 print(("compile=True: micro-step captured as a HIP graph" +
@@ -189,6 +202,7 @@ class Trainer:
             from .parallel import report_transport
             self.rccl_report = report_transport(info)
 
+        self._grad_scale0 = self.optimizer.grad_scale  # 1/world (flat reducer) or 1
         self.batches = make_batch_source(c["dataset"], c["data_dir"], c["block_size"], c["batch_size"], self.device,
                                          seed=c["seed"] + info.seed_offset, vocab_size=model_args["vocab_size"])
         run_name = c["wandb_run_name"] or "run"
@@ -249,12 +263,23 @@ class Trainer:
             loss = loss / self.gas  # scale the loss to account for gradient accumulation
             # immediately async prefetch next batch while model is doing the forward pass on the GPU
             X, Y = self.batches.get_batch("train")
-            loss.backward()
+            (loss * self.scaler.scale if self.scaler is not None else loss).backward()
         if self.reducer is not None:
             self.reducer.finish()
         norm = None
+        if self.scaler is not None:
+            # unscale by folding 1/scale into the optimizer's gradient multiplier
+            self.optimizer.grad_scale = self._grad_scale0 / self.scaler.scale
         if c["grad_clip"] != 0.0:
             norm = self.optimizer.clip_grad_norm_(c["grad_clip"])
+        if self.scaler is not None:
+            gn = norm if norm is not None else (self.store.grad.float().norm() * self.optimizer.grad_scale)
+            found_inf = not self.scaler.finite(gn.item())
+            self.scaler.update(found_inf)
+            if found_inf:  # GradScaler: skip the step, back the scale off
+                self.optimizer._clip_pending = False
+                self.optimizer.zero_grad(set_to_none=True)
+                return loss, norm, X, Y
         self.optimizer.step()
         self.optimizer.zero_grad(set_to_none=True)
         return loss, norm, X, Y
@@ -323,8 +348,12 @@ class Trainer:
         The fault fires only on the job's first attempt: a marker file in ``out_dir``
         (shared storage: the PVC in the k8s topologies) records that it fired, and
         torchrun's ``TORCHELASTIC_RESTART_COUNT`` > 0 also suppresses it, so an elastic
-        restart (``--max-restarts``) that auto-resumes from ``ckpt.pt`` runs through."""
-        marker = os.path.join(self.cfg["out_dir"], f".fault_injected_rank{self.info.rank}")
+        restart (``--max-restarts``) that auto-resumes from ``ckpt.pt`` runs through.  The
+        marker is keyed to the job (torchrun's ``TORCHELASTIC_RUN_ID``, else this process), so
+        a later job reusing the same out_dir still gets its fault."""
+        job = os.environ.get("TORCHELASTIC_RUN_ID") or f"pid{os.getpid()}"
+        job = "".join(ch if ch.isalnum() or ch in "-_" else "_" for ch in job)
+        marker = os.path.join(self.cfg["out_dir"], f".fault_injected_rank{self.info.rank}.{job}")
         if os.path.exists(marker) or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) > 0:
             return
         os.makedirs(self.cfg["out_dir"], exist_ok=True)

@@ -30,3 +30,37 @@ def test_bad_plans_rejected():
         bench.batch_plan(7)
     with pytest.raises(AssertionError):
         bench.batch_plan(1, 7)
+
+
+@pytest.mark.slow
+def test_multirank_record_carries_rccl_block(tmp_path):
+    """bench.py's N > 1 path (torchrun, 2 ranks, gloo on the CPU, the tiny plumbing model):
+    the one stdout JSON record carries the per-rank transport and the all-reduce sweep, so a
+    driver SCALE run needs no log scraping."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=root)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--device", "cpu", "--model", "tiny", "--micro-batch", "24",
+                        "--block-size", "32", "--steps", "1", "--warmup", "1", "--rccl-sweep", "1,2"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    rc = rec["rccl"]
+    assert rc["backend"] == "gloo"
+    assert set(rc["transport_by_rank"]) == {"0", "1"}
+    assert [r["MiB"] for r in rc["sweep"]] == [1, 2] and all(r["busbw_GBps"] > 0 for r in rc["sweep"])
+    assert rc["allreduce_64MiB_ms"] > 0
+    assert "gemm_kernels" in rec  # per GEMM shape the kernel that ran it (empty on the CPU)

@@ -22,11 +22,6 @@ pytestmark = pytest.mark.gpu
 
 CFG = dict(n_layer=2, n_head=2, n_embd=128, block_size=64, vocab_size=512, bias=False, dropout=0.0)
 STEPS = 3
-# every process (both ranks and the single-process reference) runs the same library
-# GEMMs instead of letting each process's autotuner time its own picks: different
-# picks (split counts, kernels) round differently, and Adam amplifies that into
-# parameter differences the comparison below would have to absorb
-_PINNED_GEMM = "hipblaslt"
 GLOBAL_MICRO = 4
 MB = 4
 
@@ -40,8 +35,8 @@ def _free_port():
 
 
 # production-kernel rehearsal: every GEMM dimension >= 256 so the forward / input-grad
-# GEMMs can take our NT kernel and the weight grads our split-K kernel (tiny widths
-# fall back to the library whatever the tuner says)
+# GEMMs take the persistent NT kernel and the weight grads the four-wave split-K kernel
+# (CFG's widths run on the small-tile / ring64 kernels)
 CFG_PROD = dict(n_layer=2, n_head=4, n_embd=256, block_size=256, vocab_size=1024, bias=False, dropout=0.0)
 
 
@@ -81,7 +76,7 @@ def _train(model, store, opt, micro_batches, gas, before=None, after=None):
 
 def _worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1", NSA_GEMM_BACKEND=_PINNED_GEMM)
+                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1")
     from nanosandbox_amd.parallel import FlatBucketReducer
     from nanosandbox_amd.parallel.dist import init_distributed
 
@@ -99,10 +94,7 @@ def _worker(rank, world, port, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_ddp_gpu_two_ranks_match_single_process(tmp_path, monkeypatch):
-    from nanosandbox_amd.ops import gemm_tune
-
-    monkeypatch.setattr(gemm_tune, "FORCE", _PINNED_GEMM)  # the reference run below, this process
+def test_ddp_gpu_two_ranks_match_single_process(tmp_path):
     port = _free_port()
     mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
@@ -112,25 +104,23 @@ def test_ddp_gpu_two_ranks_match_single_process(tmp_path, monkeypatch):
     ref = _train(model, store, opt, _batches(), GLOBAL_MICRO)
     d = (res[0]["final"] - ref).abs()
     # the remaining differences: summation order (gloo's rank sum vs sequential
-    # accumulation, embedding/LayerNorm-partial atomics); Adam turns that noise into
-    # <= lr-sized steps on near-zero gradients
+    # accumulation, split-K / embedding / LayerNorm-partial atomics); Adam turns that noise
+    # into <= lr-sized steps on near-zero gradients
     assert d.max() <= STEPS * 3e-3 + 1e-6
     assert d.mean() < 2e-5
 
 
 def _worker_prod(rank, world, port, out_dir, mode):
-    """As _worker, but with the production GEMM selection: the timed autotuner (rank 0's
-    picks broadcast to every rank, gemm_tune._agree) or deterministic mode's fixed
-    native picks.  Collectives still run over gloo (one GPU)."""
+    """As _worker, with the production-size GEMMs (NT and four-wave weight-grad kernels, by
+    the fixed shape rule every rank evaluates identically) in default or deterministic mode.
+    Collectives still run over gloo (one GPU)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1")
-    os.environ.pop("NSA_GEMM_BACKEND", None)
     from nanosandbox_amd import ops
-    from nanosandbox_amd.ops import gemm_tune
+    from nanosandbox_amd.ops import gemm_dispatch
     from nanosandbox_amd.parallel import FlatBucketReducer
     from nanosandbox_amd.parallel.dist import init_distributed
 
-    gemm_tune.FORCE = ""
     ops.set_deterministic(mode == "deterministic")
     info = init_distributed("nccl", "cuda")
     assert info.world_size == world
@@ -141,41 +131,32 @@ def _worker_prod(rank, world, port, out_dir, mode):
     red.broadcast_parameters()
     opt.grad_scale = red.grad_scale
     final = _train(model, store, opt, mine, gas, before=red.prepare, after=red.finish)
-    table = {repr(k): v for k, v in gemm_tune.table().items()}
-    torch.save({"final": final, "n_buckets": len(red.buckets), "table": table},
+    used = {repr(k): v for k, v in gemm_dispatch.kernels_used().items()}
+    torch.save({"final": final, "n_buckets": len(red.buckets), "used": used},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode", ["tuned", "deterministic"])
-def test_ddp_gpu_production_kernels(tmp_path, monkeypatch, mode):
+@pytest.mark.parametrize("mode", ["default", "deterministic"])
+def test_ddp_gpu_production_kernels(tmp_path, mode):
     """The flat reducer's bucket hooks, our split-K weight-gradient kernels accumulating
-    into the flat gradient and the NT forward / input-gradient GEMMs, together under DDP
-    (VERDICT r2 'do this' 4.1).  Ranks must agree bitwise (same kernels on every rank);
-    the single-process reference replays rank 0's kernel table, so only the gradient
-    summation order differs."""
-    import ast
-
+    into the flat gradient and the NT forward / input-gradient GEMMs, together under DDP.
+    Every rank runs the same kernels (a fixed shape rule: no tuning decision to agree on)
+    and ranks agree bitwise; a single-process run of the global batch differs only in the
+    gradient summation order."""
     from nanosandbox_amd import ops
-    from nanosandbox_amd.ops import gemm_tune
 
     port = _free_port()
     mp.spawn(_worker_prod, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
     assert res[0]["n_buckets"] > 1
-    assert res[0]["table"] == res[1]["table"], "ranks tuned different kernels"
-    picks = res[0]["table"]
-    # our kernels actually ran: native weight-grad picks (nsa*/det*) and, for the
-    # deterministic rule, native forward / input-grad picks
-    assert any(k.startswith(("('wgrad'", "('wgrad_det'")) and not v.startswith("hipblaslt")
-               for k, v in picks.items()), picks
-    if mode == "deterministic":
-        assert all(v.startswith(("nt", "det")) for k, v in picks.items() if k.startswith(("('fwd'", "('dgrad'"))), picks
+    assert res[0]["used"] == res[1]["used"]
+    used = res[0]["used"]
+    assert any(v.startswith("wgrad4") for v in used.values()), used
+    assert any(v == "nt4" for v in used.values()), used
+    assert not any(v == "torch" for v in used.values()), used
     assert torch.equal(res[0]["final"], res[1]["final"]), "ranks diverged"
-    monkeypatch.setattr(gemm_tune, "FORCE", "")
-    monkeypatch.setattr(gemm_tune, "_table", {ast.literal_eval(k): v for k, v in picks.items()})
-    monkeypatch.setattr(gemm_tune, "_loaded", True)
     ops.set_deterministic(mode == "deterministic")
     try:
         model, store, opt = _build(seed=300, cfg=CFG_PROD)
@@ -191,7 +172,7 @@ def _worker_trainer(rank, world, port, out_dir, cfg, compile_):
     """Trainer-level DDP rehearsal (flat reducer over gloo, one GPU): compile=True captures
     the accumulation micro-steps as a HIP graph and runs the synchronising one eagerly."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1", NSA_GEMM_BACKEND=_PINNED_GEMM)
+                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1")
     from nanosandbox_amd.train import Trainer
 
     torch.manual_seed(0)

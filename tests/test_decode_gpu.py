@@ -112,6 +112,28 @@ def test_cached_generation_on_gpu(kernels):
     assert int(out.max()) < 512 and int(out.min()) >= 0
 
 
+def test_reused_decoder_draws_independent_samples(kernels):
+    """sample.py's loop reuses one Decoder (and its captured sampling graph) for every
+    sample: each generate call must still draw its own tokens (a salt baked into
+    the graph made every sample identical)."""
+    from nanosandbox_amd.runtime.decode import Decoder
+
+    m = _model()
+    idx = torch.randint(0, 512, (1, 8), device=DEV)
+    dec = Decoder(m, 1, max_len=m.config.block_size, use_graph=True)
+    try:
+        outs = [m.generate_cached(idx, 40, temperature=1.0, top_k=None, decoder=dec) for _ in range(3)]
+    finally:
+        dec.release()
+    assert dec.replays > 0
+    assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])
+    torch.manual_seed(11)
+    a = m.generate_cached(idx, 20, temperature=1.0)
+    torch.manual_seed(11)
+    b = m.generate_cached(idx, 20, temperature=1.0)
+    assert torch.equal(a, b)  # still reproducible from torch.manual_seed
+
+
 @pytest.mark.parametrize("B", [3, 1])
 def test_graph_sampling_loop_matches_eager_greedy(kernels, B):
     """run(): step + sampling + device-side token feedback replayed as one graph gives the

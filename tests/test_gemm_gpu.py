@@ -1,5 +1,11 @@
-"""Our MFMA GEMMs vs fp32 torch matmul: the persistent NT kernel (forward, input grad,
-GELU / GELU' epilogues, ragged shapes) and the split-K weight-gradient kernel."""
+"""Our MFMA GEMMs vs fp32 torch matmul, checked element by element.
+
+Every output is written into a NaN-prefilled buffer (a tile that skips rows or columns
+leaves NaN behind) and compared per element against the fp32 product of the same
+bf16-exact operands with the bound |C - C_ref| <= 2^-8 |C_ref| + 2^-16 (|A| |B|^T)
+(one bf16 rounding of the output plus fp32 accumulation-order noise), so a tail tile that
+drops or misplaces even one row fails.  Exact permutation / identity products at ragged
+shapes pin the tile and epilogue indexing bit for bit (guide §3: asymmetric operands)."""
 
 import pytest
 import torch
@@ -8,175 +14,244 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 BF = torch.bfloat16
+NAN = float("nan")
 
 
-def rel(a, b):
-    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+def nanbuf(*shape, dtype=BF):
+    return torch.full(shape, NAN, device=DEV, dtype=dtype)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
-                                   (256, 256, 3072), (1000, 1288, 640), (4096, 768, 4608)])
-def test_nt_forward_and_gelu_epilogue(kernels, M, N, K):
-    """Persistent NT kernels vs fp32 torch (gemm.fwd / fwd_gelu run the four-wave kernel):
-    plain, GELU epilogue, ragged M/N (tail tiles shifted back inside the matrix), several
-    tiles per workgroup; the eight-wave kernel (gemm_nt.hip) with either store policy gives
-    bitwise the same output (same accumulation order)."""
+def check(c, ref, absab, rel=2 ** -8, name=""):
+    """Per-element bound; no NaN / inf anywhere."""
+    c = c.float()
+    assert torch.isfinite(c).all(), f"{name}: {(~torch.isfinite(c)).sum().item()} non-finite outputs"
+    err = (c - ref).abs()
+    bound = rel * ref.abs() + 2 ** -16 * absab + 1e-30
+    bad = err > bound
+    assert not bad.any(), (f"{name}: {bad.sum().item()} elements out of bound, worst at "
+                           f"{tuple(torch.nonzero(bad)[0].tolist())}: got {c[bad][0].item()} want {ref[bad][0].item()}")
+
+
+def gelu_grad(uf):
+    return 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
+
+
+NT_SHAPES = [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768), (256, 256, 64),
+             (1000, 1288, 640), (8200, 768, 3072), (257, 264, 64), (4096, 768, 4608)]
+
+
+@pytest.mark.parametrize("M,N,K", NT_SHAPES)
+def test_nt4_elementwise(kernels, M, N, K):
+    """Four-wave persistent kernel: plain, bias, GELU (u and gelu(u)), GELU' epilogues;
+    ragged M / N exercise the shifted tail tiles, 8200 x 768 several tiles per workgroup."""
     from nanosandbox_amd.ops import gemm
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV).to(BF)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    y = gemm.fwd(x, w)
-    assert rel(y, x.float() @ w.float().t()) < 1e-2
-    u, g = gemm.fwd_gelu(x, w)
-    assert torch.equal(u, y)
-    assert rel(g, F.gelu(u.float())) < 1e-2
+    b = torch.randn(N, device=DEV).to(BF)
+    ref = x.float() @ w.float().t()
+    absab = x.float().abs() @ w.float().abs().t()
+    y = gemm.nt(x, w, out=nanbuf(M, N))
+    check(y, ref, absab, name="plain")
+    yb = gemm.nt(x, w, bias=b, out=nanbuf(M, N))
+    check(yb, ref + b.float(), absab + b.float().abs(), name="bias")
+    u, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N), out2=nanbuf(M, N))
+    assert torch.equal(u, yb)
+    check(g, F.gelu(u.float()), u.float().abs() + 1, rel=2 ** -7, name="gelu")
     for st in (1, 2):  # nontemporal / plain epilogue stores: identical results
-        assert torch.equal(gemm.nt(x, w, var=st), y)
+        assert torch.equal(gemm.nt(x, w, var=st, out=nanbuf(M, N)), y)
+    uu = torch.randn(M, N, device=DEV).to(BF)
+    d = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=uu, out=nanbuf(M, N))
+    gp = gelu_grad(uu.float())
+    check(d, y.float() * gp, (absab * gp).abs(), rel=2 ** -7, name="dgelu")
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 3072, 768), (264, 512, 256), (2048, 50304, 768),
-                                   (8192, 768, 3072), (8200, 768, 3072)])
-def test_nt_input_grad_and_dgelu_epilogue(kernels, M, N, K):
-    """dX = dY·W through the K-contiguous W^T, plain and with the GELU' epilogue; the
-    8192-row shapes give every workgroup several output tiles (deferred epilogue stores,
-    and with 8200 rows a shifted tail tile among them)."""
+@pytest.mark.parametrize("M,N,K", [(1000, 1288, 640), (8200, 768, 3072), (257, 264, 64), (2048, 50304, 768)])
+def test_nt4_exact_permutation(kernels, M, N, K):
+    """A = one-hot rows (row i selects column i % K): C[i, j] = B[j, i % K] exactly, so any
+    misplaced row / column of a ragged tail tile shows up bit for bit."""
     from nanosandbox_amd.ops import gemm
-    torch.manual_seed(0)
-    dy = torch.randn(M, N, device=DEV).to(BF)
-    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    dx = gemm.dgrad(dy, w)
-    ref = dy.float() @ w.float()
-    assert rel(dx, ref) < 1e-2
-    u = torch.randn(M, K, device=DEV).to(BF)
-    dxg = gemm.dgrad(dy, w, u=u)
-    uf = u.float()
-    gp = 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
-    assert rel(dxg, dx.float() * gp) < 1e-2
+    a = torch.zeros(M, K, device=DEV, dtype=BF)
+    idx = torch.arange(M, device=DEV) % K
+    a[torch.arange(M, device=DEV), idx] = 1
+    b = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K).remainder(251).sub(125).to(BF)
+    c = gemm.nt(a, b, out=nanbuf(M, N))
+    assert torch.equal(c.float(), b.float()[:, idx].t())
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 192, 64), (100, 72, 40), (2048, 64, 256), (17, 300, 128), (300, 17, 88)])
+def test_small_kernel(kernels, M, N, K):
+    """The bounds-checked kernel for shapes below one NT tile: every epilogue, any M / N."""
+    from nanosandbox_amd.ops import gemm
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.1).to(BF)
+    b = torch.randn(N, device=DEV).to(BF)
+    ref = x.float() @ w.float().t()
+    absab = x.float().abs() @ w.float().abs().t()
+    check(gemm.small(x, w, out=nanbuf(M, N)), ref, absab, name="small")
+    u, g = gemm.small(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N), out2=nanbuf(M, N))
+    check(u, ref + b.float(), absab + b.float().abs(), name="small bias")
+    check(g, F.gelu(u.float()), u.float().abs() + 1, rel=2 ** -7, name="small gelu")
+    uu = torch.randn(M, N, device=DEV).to(BF)
+    d = gemm.small(x, w, epi=gemm.NT_EPI_DGELU, u=uu, out=nanbuf(M, N))
+    gp = gelu_grad(uu.float())
+    check(d, ref * gp, (absab * gp).abs() + ref.abs() * gp.abs() * 2 ** -8, rel=2 ** -7, name="small dgelu")
 
 
 @pytest.mark.parametrize("T,N,K,splits", [(1024, 768, 768, None), (4096, 2304, 768, None), (512, 520, 200, 2),
-                                          (2048, 768, 3072, 4), (1024, 50304, 768, 1),
+                                          (2048, 768, 3072, 4), (1024, 50304, 768, 1), (1088, 1032, 264, 3),
                                           (1024, 768, 768, 3), (4096, 2304, 768, 28),  # uneven K splits
-                                          (1024, 768, 768, 16)])  # one K-tile per split
-@pytest.mark.parametrize("variant", [1, 7, 9, 10])
-def test_wgrad_acc(kernels, T, N, K, splits, variant):
+                                          (1024, 768, 768, 16), (512, 192, 64, 2)])  # one K-tile per split; ring64
+def test_wgrad_acc(kernels, T, N, K, splits):
     from nanosandbox_amd.ops import gemm
-    if K % 8:
-        K = K - K % 8
+    K = K - K % 8
     torch.manual_seed(0)
     dy = torch.randn(T, N, device=DEV).to(BF)
     x = torch.randn(T, K, device=DEV).to(BF)
     g = torch.randn(N, K, device=DEV)
     ref = g + dy.float().t() @ x.float()
-    gemm.wgrad_acc(dy, x, g, splits=splits, variant=variant)
-    assert rel(g, ref) < 5e-3
+    absab = g.abs() + dy.float().abs().t() @ x.float().abs()
+    gemm.wgrad_acc(dy, x, g, splits=splits)
+    check(g, ref, absab, rel=2 ** -20, name="wgrad")
     # deterministic form: partials reduced in split order, bitwise repeatable
     g1 = torch.randn(N, K, device=DEV)
     g2 = g1.clone()
-    gemm.wgrad_acc(dy, x, g1, splits=splits, variant=variant, deterministic=True)
-    gemm.wgrad_acc(dy, x, g2, splits=splits, variant=variant, deterministic=True)
+    gemm.wgrad_acc(dy, x, g1, splits=splits, deterministic=True)
+    gemm.wgrad_acc(dy, x, g2, splits=splits, deterministic=True)
     assert torch.equal(g1, g2)
 
 
-@pytest.mark.parametrize("variant", [1, 7, 9, 10])
-def test_asymmetric_identity(kernels, variant):
-    """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
+@pytest.mark.parametrize("T,N,K", [(1088, 1032, 264), (1024, 768, 768), (512, 192, 64)])
+def test_wgrad_exact_permutation(kernels, T, N, K):
+    """dY[t, n] = 1 iff n == t % N: dW[n] = sum of the x rows t = n, n + N, ... (at most two
+    bf16 values: exact in fp32) -- a misplaced output row / column of a ragged tail tile
+    fails bit for bit."""
     from nanosandbox_amd.ops import gemm
-    n = 256
+    dy = torch.zeros(T, N, device=DEV, dtype=BF)
+    t = torch.arange(T, device=DEV)
+    dy[t, t % N] = 1
+    x = torch.arange(T * K, device=DEV, dtype=torch.float32).view(T, K).remainder(97).sub(48).to(BF)
+    ref = torch.zeros(N, K, device=DEV)
+    ref.index_add_(0, t % N, x.float())
+    for det in (False, True):
+        g = torch.zeros(N, K, device=DEV)
+        gemm.wgrad_acc(dy, x, g, deterministic=det)
+        assert torch.equal(g, ref)
+
+
+def test_asymmetric_identity(kernels):
+    """A = I with an asymmetric B catches row/col swaps in the C write (guide §3)."""
+    from nanosandbox_amd.ops import gemm, gemm_dispatch
+    n = 512
     eye = torch.eye(n, device=DEV).to(BF)
     b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(251).to(BF)
-    assert torch.equal(gemm.fwd(eye, b).float(), b.float().t())  # I @ b^T
-    assert torch.equal(gemm.dgrad(eye, b).float(), b.float())     # I @ b
+    assert torch.equal(gemm.nt(eye, b).float(), b.float().t())  # I @ b^T
+    assert torch.equal(gemm.nt(b, eye).float(), b.float())
+    assert torch.equal(gemm_dispatch.dgrad(eye, b).float(), b.float())  # I @ b
     g = torch.zeros(n, n, device=DEV)
-    gemm.wgrad_acc(eye, b, g, variant=variant)                    # I^T @ b
+    gemm.wgrad_acc(eye, b, g)  # I^T @ b
     assert torch.equal(g, b.float())
 
 
-def test_tuner_prefers_native_within_margin(kernels, monkeypatch):
-    """gemm_tune.choose: a library candidate wins only when it is more than NATIVE_MARGIN
-    faster than the best native one; deterministic mode picks without timing."""
-    from nanosandbox_amd.ops import gemm_tune
-    monkeypatch.setattr(gemm_tune, "_time_all", lambda c, **k: {"hipblaslt": 1.0, "nt": 1.01})
-    monkeypatch.setattr(gemm_tune, "_table", {})
-    monkeypatch.setattr(gemm_tune, "FORCE", "")
-    cands = {"hipblaslt": lambda: None, "nt": lambda: None}
-    assert gemm_tune.choose(("t", 1), cands) == "nt"
-    monkeypatch.setattr(gemm_tune, "_time_all", lambda c, **k: {"hipblaslt": 1.0, "nt": 1.10})
-    assert gemm_tune.choose(("t", 2), cands) == "hipblaslt"
-    monkeypatch.setattr(gemm_tune, "DETERMINISTIC", True)
-    monkeypatch.setattr(gemm_tune, "_time_all", lambda c, **k: (_ for _ in ()).throw(AssertionError("timed")))
-    assert gemm_tune.choose(("t", 3), cands) == "nt"
+def test_bias_grad(kernels):
+    from nanosandbox_amd.ops import gemm
+    torch.manual_seed(0)
+    for T, N in [(122880 // 16, 768), (300, 72), (64, 2304)]:
+        dy = torch.randn(T, N, device=DEV).to(BF)
+        gb = torch.randn(N, device=DEV)
+        ref = gb + dy.float().sum(0)
+        gemm.bias_grad_acc(dy, gb)
+        assert torch.allclose(gb, ref, rtol=1e-5, atol=1e-4 * T ** 0.5)
+        g1 = torch.zeros(N, device=DEV)
+        g2 = torch.zeros(N, device=DEV)
+        gemm.bias_grad_acc(dy, g1, deterministic=True)
+        gemm.bias_grad_acc(dy, g2, deterministic=True)
+        assert torch.equal(g1, g2)
+
+
+def test_dispatch_records_native_kernels(kernels):
+    """The fixed rule's picks as the bench JSON reports them (no library kernel)."""
+    from nanosandbox_amd.ops import gemm_dispatch
+    x = torch.randn(512, 768, device=DEV).to(BF)
+    w = torch.randn(2304, 768, device=DEV).to(BF)
+    gemm_dispatch.fwd(x, w)
+    gemm_dispatch.fwd(x[:100].contiguous(), w)
+    used = gemm_dispatch.kernels_used()
+    assert used[("fwd", 512, 2304, 768)] == "nt4"
+    assert used[("fwd", 100, 2304, 768)] == "small"
 
 
 def test_transposed_weight_dgrad_cache(kernels):
-    """dX = dY·W through the cached K-contiguous W^T (gemm_tune._wt): equal to the plain
-    product, rebuilt after an in-place update (version bump) and after a raw rewrite
-    announced by weights_changed() (what the fused AdamW kernel does)."""
-    from nanosandbox_amd.ops import gemm_tune
+    """dX = dY·W through the cached K-contiguous W^T: equal to the plain product, rebuilt after
+    an in-place update (version bump) and after a raw rewrite announced by weights_changed()
+    (what the fused AdamW kernel does)."""
+    from nanosandbox_amd.ops import gemm_dispatch
 
     torch.manual_seed(0)
     dy = torch.randn(512, 384, device="cuda").to(torch.bfloat16)
     w = torch.randn(384, 256, device="cuda").to(torch.bfloat16)
 
     def via_t():
-        return dy @ gemm_tune._wt(w).t()
+        return (dy.float() @ gemm_dispatch._wt(w).t().float())
 
-    assert torch.equal(via_t(), dy @ w)
-    t0 = gemm_tune._wt(w)
-    assert gemm_tune._wt(w) is t0  # cached
+    assert torch.equal(via_t(), dy.float() @ w.float())
+    t0 = gemm_dispatch._wt(w)
+    assert gemm_dispatch._wt(w) is t0  # cached
     w.mul_(2.0)  # torch in-place op: version bump invalidates
-    assert torch.equal(via_t(), dy @ w)
+    assert torch.equal(via_t(), dy.float() @ w.float())
     w.data.copy_(torch.randn_like(w))  # raw rewrite: no version bump ...
-    stale = via_t()
-    assert not torch.equal(stale, dy @ w)  # ... so the cache is stale until announced
-    gemm_tune.weights_changed()
-    assert torch.equal(via_t(), dy @ w)
+    assert not torch.equal(via_t(), dy.float() @ w.float())  # ... so the cache is stale until announced
+    gemm_dispatch.weights_changed()
+    assert torch.equal(via_t(), dy.float() @ w.float())
 
 
 @pytest.mark.parametrize("R,C", [(768, 3072), (50304, 768), (64, 128), (2304, 768)])
 def test_transpose_bf16(kernels, R, C):
     """The weight-transpose kernel behind the cached K-contiguous dgrad weights."""
-    from nanosandbox_amd.ops import gemm_tune
+    from nanosandbox_amd.ops import gemm_dispatch
 
     w = torch.randn(R, C, device="cuda").to(torch.bfloat16)
-    t = gemm_tune._transpose(w)
+    t = gemm_dispatch._transpose(w)
     assert t.shape == (C, R) and t.is_contiguous()
     assert torch.equal(t, w.t())
-    t2 = gemm_tune._transpose(w * 2, out=t)  # rebuilt in place
+    t2 = gemm_dispatch._transpose(w * 2, out=t)  # rebuilt in place
     assert t2.data_ptr() == t.data_ptr() and torch.equal(t2, (w * 2).t())
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768),
-                                   (256, 256, 64), (1000, 1288, 640), (8200, 768, 3072), (4096, 768, 4608)])
-def test_nt4_matches_fp32_and_nt(kernels, M, N, K):
-    """Four-wave persistent NT kernel (gemm_nt4.hip) vs fp32 torch, and bitwise against the
-    eight-wave kernel (same accumulation order per output: one K-tile at a time, k-steps in
-    order) for the plain, GELU and GELU' epilogues; ragged M / N exercise the shifted tail
-    tiles and the drained (uncounted) epilogue, 8200 x 768 several tiles per workgroup."""
+@pytest.mark.parametrize("M,V,Vp,C", [(2048, 50304, 50304, 768), (1032, 50257, 50304, 768), (512, 65, 256, 384)])
+def test_nt4_xent_epilogue(kernels, M, V, Vp, C):
+    """Fused cross-entropy forward GEMM: E = exp(x w^T - c) (bf16, padding columns 0) and the
+    half-tile row sums, against fp32."""
     from nanosandbox_amd.ops import gemm
-    torch.manual_seed(0)
-    x = torch.randn(M, K, device=DEV).to(BF)
-    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
-    y4 = gemm.nt(x, w, w4=True)
-    assert rel(y4, x.float() @ w.float().t()) < 1e-2
-    u4, g4 = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, w4=True)
-    assert torch.equal(u4, y4)
-    assert rel(g4, F.gelu(u4.float())) < 1e-2
-    for st in (1, 2):
-        assert torch.equal(gemm.nt(x, w, var=st, w4=True), y4)
-    u = torch.randn(M, N, device=DEV).to(BF)
-    d4 = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u, w4=True)
-    uf = u.float()
-    gp = 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
-    assert rel(d4, y4.float() * gp) < 1e-2
+    torch.manual_seed(2)
+    x = torch.randn(M, C, device=DEV).to(BF)
+    w = torch.zeros(Vp, C, device=DEV, dtype=BF)
+    w[:V] = (torch.randn(V, C, device=DEV) * 0.05).to(BF)
+    crow = torch.randn(M, device=DEV)
+    slots = 2 * (-(-Vp // 256))
+    part = torch.full((slots, M), NAN, device=DEV)
+    e = gemm.nt_xent(x, w, crow, part, V, out=nanbuf(M, Vp))
+    ref = torch.exp(x.float() @ w.float().t() - crow[:, None])
+    ref[:, V:] = 0
+    check(e, ref, ref.abs() * 2 ** -12, rel=2 ** -7, name="E")
+    S = part.sum(0)
+    assert torch.isfinite(part).all()
+    assert torch.allclose(S, ref.sum(1), rtol=1e-4)
 
 
-def test_nt4_asymmetric_identity(kernels):
-    """A = I with an asymmetric B through the four-wave kernel: a row/column swap or a wrong
-    column permutation of the staged B image shows up exactly (guide §3)."""
+@pytest.mark.parametrize("M,K,N", [(2048, 50304, 768), (1032, 50304, 1024)])
+def test_nt4_xdx_epilogue(kernels, M, K, N):
+    """Fused cross-entropy input-gradient GEMM: cs * (E W) - cw * Wrows, fp32 subtraction."""
     from nanosandbox_amd.ops import gemm
-    n = 512
-    eye = torch.eye(n, device=DEV).to(BF)
-    b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(251).to(BF)
-    assert torch.equal(gemm.nt(eye, b, w4=True).float(), b.float().t())
-    assert torch.equal(gemm.nt(b, eye, w4=True).float(), b.float())
+    torch.manual_seed(3)
+    e = torch.rand(M, K, device=DEV).to(BF)
+    wt = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    wrows = torch.randn(M, N, device=DEV).to(BF)
+    coef = torch.rand(M, 2, device=DEV)
+    coef[::7] = 0  # ignored rows
+    d = gemm.nt_xdx(e, wt, wrows, coef, out=nanbuf(M, N))
+    prod = e.float() @ wt.float().t()
+    ref = coef[:, :1] * prod - coef[:, 1:] * wrows.float()
+    absab = coef[:, :1] * (e.float().abs() @ wt.float().abs().t()) + coef[:, 1:] * wrows.float().abs()
+    check(d, ref, absab, name="xdx")

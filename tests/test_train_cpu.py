@@ -72,20 +72,26 @@ def test_cpu_smoke_train_resume_sample(cfg, tmp_path, capsys):
     assert outs[0].startswith("KING:") and len(outs[0]) == len("KING:") + 20
 
 
-def test_fault_injection_and_auto_resume(cfg, tmp_path):
+def test_fault_injection_and_auto_resume(cfg, tmp_path, monkeypatch):
     from nanosandbox_amd.train import Trainer
 
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job-a")
     c = dict(cfg, fault_inject_iter=8, fault_inject_rank=0, auto_resume=True)
     with pytest.raises(RuntimeError, match="injected fault"):
         Trainer(c).fit()
     assert (tmp_path / "out" / "ckpt.pt").exists()  # saved at iter 6
-    assert (tmp_path / "out" / ".fault_injected_rank0").exists()
+    assert (tmp_path / "out" / ".fault_injected_rank0.job-a").exists()
     # the same job configuration restarted (what torchrun --max-restarts / a k8s restart
     # does): the fault fired once per job, so the restart resumes at 6 and runs through
     tr = Trainer(c)
     assert tr.iter_num == 6
     tr.fit()
     assert tr.iter_num == 13
+    # a later job reusing the out_dir gets its own fault (the marker is keyed to the job)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job-b")
+    c2 = dict(c, fault_inject_iter=14, max_iters=20)
+    with pytest.raises(RuntimeError, match="injected fault at iter 14"):
+        Trainer(c2).fit()
 
 
 def test_eval_only(cfg, capsys):
@@ -131,3 +137,49 @@ def test_graph_capture_policy(monkeypatch):
     assert not ok and "one micro-step" in why
     ok, why = graph_capture_supported("cuda:0", 0.0, 2, "torch", 4)
     assert not ok and "torch DDP" in why
+
+
+def test_dtype_key_contract():
+    """nanoGPT's dtype key: bfloat16 / float16 / float32 accepted (anything else refused
+    loudly); the CPU computes in fp32 whatever the key (nanoGPT's nullcontext)."""
+    import torch
+
+    from nanosandbox_amd.train import _compute_dtype
+
+    assert _compute_dtype("cuda", "bfloat16") == torch.bfloat16
+    assert _compute_dtype("cuda", "float16") == torch.float16
+    assert _compute_dtype("cuda", "float32") == torch.float32
+    for d in ("bfloat16", "float16", "float32"):
+        assert _compute_dtype("cpu", d) == torch.float32
+    with pytest.raises(ValueError, match="dtype must be one of"):
+        _compute_dtype("cuda", "fp8")
+
+
+def test_dynamic_loss_scale_policy():
+    """GradScaler's policy: back off x0.5 and count a skip on overflow, grow x2 after
+    growth_interval clean steps."""
+    from nanosandbox_amd.optim.loss_scale import DynamicLossScale
+
+    s = DynamicLossScale(init_scale=1024.0, growth_interval=3)
+    assert not s.finite(float("inf")) and not s.finite(float("nan")) and s.finite(3.0)
+    s.update(True)
+    assert s.scale == 512.0 and s.skipped == 1
+    for _ in range(2):
+        s.update(False)
+    assert s.scale == 512.0
+    s.update(False)
+    assert s.scale == 1024.0
+    sd = s.state_dict()
+    s2 = DynamicLossScale()
+    s2.load_state_dict(sd)
+    assert s2.scale == 1024.0
+
+
+def test_cpu_trainer_accepts_float16_key(cfg):
+    """--dtype=float16 on the CPU trains in fp32 without a scaler (nanoGPT: GradScaler is
+    disabled off CUDA)."""
+    from nanosandbox_amd.train import Trainer
+
+    tr = Trainer(dict(cfg, dtype="float16", max_iters=2))
+    assert tr.scaler is None
+    tr.fit()

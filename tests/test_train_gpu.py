@@ -158,3 +158,50 @@ def test_deterministic_training_is_bitwise_reproducible(kernels, tmp_path):
             assert err < 5e-2, (k, err)
     finally:
         ops.set_deterministic(False)
+
+
+@pytest.mark.parametrize("dtype", ["float16", "float32"])
+def test_train_dtype_contract(kernels, tmp_path, dtype):
+    """nanoGPT's --dtype on the GPU: float16 (with the dynamic loss scale) and
+    float32 run the torch reference ops and learn like bf16; compile=True falls back to
+    eager micro-steps for them."""
+    import json
+
+    from nanosandbox_amd.train import Trainer
+
+    tr = Trainer(_cfg(tmp_path, dtype=dtype, max_iters=20, eval_interval=1000, compile=True,
+                      tensorboard_dir=""))
+    assert tr.raw_model.compute_dtype == {"float16": torch.float16, "float32": torch.float32}[dtype]
+    assert not tr.use_graph
+    assert (tr.scaler is not None) == (dtype == "float16")
+    tr.fit()
+    recs = [json.loads(l) for l in open(os.path.join(tmp_path, "metrics.jsonl"))]
+    train = [r for r in recs if r["kind"] == "train"]
+    assert all(r["loss"] == r["loss"] for r in train)  # finite
+    assert train[-1]["loss"] < 0.85 * train[0]["loss"]
+    if dtype == "float16":
+        assert tr.scaler.scale > 0
+
+
+def test_fp16_loss_scale_skips_overflowing_steps(kernels, tmp_path):
+    """An absurd initial loss scale overflows fp16 gradients: the step is skipped (weights
+    unchanged) and the scale backs off until steps go through (GradScaler semantics)."""
+    from nanosandbox_amd.train import Trainer
+
+    tr = Trainer(_cfg(tmp_path, dtype="float16", max_iters=5, eval_interval=1000, compile=False,
+                      tensorboard_dir=""))
+    tr.scaler.scale = 2.0 ** 60
+    w0 = tr.store.master.clone()
+    X, Y = tr.batches.get_batch("train")
+    for g in tr.optimizer.param_groups:
+        g["lr"] = 1e-3
+    tr.train_step(X, Y)
+    assert tr.scaler.skipped == 1 and tr.scaler.scale == 2.0 ** 59
+    assert torch.equal(tr.store.master, w0)
+    for _ in range(60):  # every overflow halves the scale: 2^59 -> ~2^20 in ~40 skipped steps
+        X, Y = tr.batches.get_batch("train")
+        tr.train_step(X, Y)
+        if not torch.equal(tr.store.master, w0):
+            break
+    assert not torch.equal(tr.store.master, w0)  # a step went through once the scale fit
+    assert tr.scaler.scale < 2.0 ** 59 and tr.scaler.skipped >= 1
