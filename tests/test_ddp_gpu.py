@@ -221,3 +221,38 @@ def test_ddp_gpu_compile_graph_with_reducer(tmp_path):
         assert abs(a - b) < 2e-2 * abs(b), (g[0]["losses"], e[0]["losses"])
     d = (g[0]["final"] - e[0]["final"]).abs()
     assert d.max() < 4 * 3e-3 and d.mean() < 2e-5
+
+
+def _worker_fit(rank, world, port, out_dir, cfg):
+    """Trainer.fit() under DDP (flat reducer over gloo, one GPU): rank 0 evaluates alone at
+    iteration 0 and at the eval interval while the other rank trains on; nothing may pair
+    up wrongly or hang (no collective outside the reducer's ordered buckets)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NSA_REHEARSAL_ONE_GPU="1")
+    from nanosandbox_amd.train import Trainer
+
+    torch.manual_seed(0)
+    tr = Trainer(dict(cfg, out_dir=os.path.join(out_dir, f"fit_r{rank}")))
+    tr.fit()
+    torch.cuda.synchronize()
+    torch.save({"final": tr.store.master.detach().cpu().clone(), "iter": tr.iter_num},
+               os.path.join(out_dir, f"fit_rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_gpu_fit_with_rank0_eval(tmp_path):
+    from nanosandbox_amd.config import TRAIN_DEFAULTS
+    from nanosandbox_amd.data.prepare import synthetic_corpus, write_char_dataset
+
+    write_char_dataset(str(tmp_path / "data" / "chars"), synthetic_corpus(200_000))
+    cfg = dict(TRAIN_DEFAULTS)
+    cfg.update(dataset="chars", data_dir=str(tmp_path / "data"), n_layer=2, n_head=4, n_embd=256, block_size=256,
+               batch_size=4, gradient_accumulation_steps=4, max_iters=6, eval_interval=3, eval_iters=2,
+               log_interval=1, device="cuda", backend="nccl", dropout=0.0, bias=True, seed=1234, compile=False,
+               ddp_impl="flat", ddp_bucket_mb=1, tensorboard_dir="", always_save_checkpoint=False)
+    port = _free_port()
+    mp.spawn(_worker_fit, args=(2, port, str(tmp_path), cfg), nprocs=2, join=True)
+    res = [torch.load(os.path.join(tmp_path, f"fit_rank{r}.pt"), weights_only=True) for r in range(2)]
+    assert res[0]["iter"] == res[1]["iter"] == 7
+    assert torch.equal(res[0]["final"], res[1]["final"]), "ranks diverged"

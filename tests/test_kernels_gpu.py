@@ -337,7 +337,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
@@ -362,8 +362,8 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3"])
-@pytest.mark.parametrize("pattern", ["rising", "falling", "spikes"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4"])
+@pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
 
@@ -390,9 +390,11 @@ def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     elif pattern == "falling":
         ramp = torch.linspace(1, 0, T, device=DEV)
         k = k + (ramp * 40.0)[None, :, None, None] * u
-    else:
+    elif pattern == "spikes":
         idx = torch.randint(0, T, (24,), device=DEV)
         k[:, idx] += 30.0 * u
+    else:  # every logit far below zero (the first tile must still set the max: no underflow)
+        k = k - 60.0 * u
     qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(BF).requires_grad_(True)
     y = ops.attention(qkv, H, 0.0, True)
     dy = torch.randn(B, T, C, device=DEV).to(BF)
@@ -451,6 +453,28 @@ def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
         torch.cuda.synchronize()
     e = rel_err(outs["v3"], outs["v1"])
     assert e < 5e-3, f"v3 vs v1 rel err {e}"
+
+
+@pytest.mark.parametrize("T", [384, 1024, 200])
+def test_flash_fwd_v4_matches_v1(kernels, flash_variant, T):
+    """Forward v4 (max shift and row sum on the MFMA pipe, Q pre-scaled) against v1: output
+    and the saved LSE (what the backward recomputes P from)."""
+    from nanosandbox_amd.ops import _lib
+
+    torch.manual_seed(0)
+    B, H, D = 2, 3, 64
+    C = H * D
+    qkv = torch.randn(B, T, 3 * C, device=DEV).to(BF)
+    outs = {}
+    for ver in ("v1", "v4"):
+        flash_variant(fwd=ver)
+        y = torch.empty(B, T, C, device=DEV, dtype=BF)
+        lse = torch.empty(B, H, T, device=DEV)
+        _lib.call("nsa_flash_fwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, D, 1.0 / math.sqrt(D), 0.0, 0,
+                  _lib.stream())
+        outs[ver] = (y.float(), lse)
+    assert rel_err(outs["v4"][0], outs["v1"][0]) < 5e-3
+    assert (outs["v4"][1] - outs["v1"][1]).abs().max().item() < 2e-2
 
 
 def test_flash_variant_is_resolved_once(kernels, monkeypatch):
