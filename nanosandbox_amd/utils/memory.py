@@ -117,7 +117,7 @@ def choose_micro_batch(n_layer: int, n_embd: int, n_head: int, vocab_size: int, 
     resident in ``hbm_bytes`` next to the model state; if even a one-sequence micro-step
     would not fit, the largest divisor whose checkpointed activations fit, with grad_ckpt.
     Larger micro-steps amortise the per-launch costs; resident beats checkpointed at any
-    micro-batch (GPT-2 1.5B: 60 resident 5025-5124 ms/step, 120 checkpointed 6779)."""
+    micro-batch (GPT-2 1.5B: 60 resident 4592 ms/step in round 3, 120 checkpointed 6779 in round 2)."""
     budget = headroom * (hbm_bytes - model_state_bytes(n_layer, n_embd, vocab_size, block_size) - RUNTIME_RESERVE)
     divisors = [d for d in range(min(cap, per_rank_seqs), 0, -1) if per_rank_seqs % d == 0]
     kw = dict(n_layer=n_layer, n_embd=n_embd, n_head=n_head, vocab_size=vocab_size, fp32_residual=fp32_residual)

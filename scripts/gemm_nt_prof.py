@@ -18,8 +18,7 @@ ap.add_argument("--k", type=int, default=50304)
 ap.add_argument("--probe", type=int, default=0)
 ap.add_argument("--var", type=int, default=0)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--lib", action="store_true", help="time hipBLASLt instead")
-ap.add_argument("--w4", action="store_true", help="the four-wave kernel (gemm_nt4.hip)")
+ap.add_argument("--lib", action="store_true", help="torch matmul (hipBLASLt) as a yardstick")
 a = ap.parse_args()
 x = (torch.rand(a.m, a.k, device="cuda") * 2 - 1).to(torch.bfloat16)
 w = ((torch.rand(a.n, a.k, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
@@ -27,6 +26,6 @@ for _ in range(a.iters):
     if a.lib:
         y = x @ w.t()
     else:
-        y = gemm.nt(x, w, probe=a.probe, var=a.var, w4=a.w4)
+        y = gemm.nt(x, w, probe=a.probe, var=a.var)
 torch.cuda.synchronize()
 print("done", y.shape)

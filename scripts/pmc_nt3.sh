@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# PMC groups (scripts/pmc_nt.sh) for the NT kernel, its no-DMA probe and hipBLASLt on one shape.
+# PMC groups (scripts/pmc_nt.sh) for the NT kernel, its no-DMA probe and torch's matmul (yardstick) on one shape.
 # usage: scripts/pmc_nt3.sh <outdir> <gemm_nt_prof.py shape args...>
 set -u
 out="$1"; shift
