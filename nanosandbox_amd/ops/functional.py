@@ -736,7 +736,8 @@ GEMV_MAX_ROWS = int(os.environ.get("NSA_GEMV_MAX_ROWS", "1"))
 # decode batches of 2..SKINNY_MAX_ROWS rows: the MFMA weight-streaming kernel (nsa_skinny_gemm).
 # HIP-graph decode, ms/token (GPT-2 124M / 1.5B): batch 8 0.685 / 4.24 with the library GEMM,
 # 0.549 / 3.24 with this kernel; batch 64 0.938 / 5.45 vs 0.946 / 6.62 (every 16-column
-# workgroup re-reads the whole 64-row X, 4x its weight bytes), so the library keeps M > 16.
+# workgroup re-reads the whole 64-row X, 4x its weight bytes), so M > 16 goes to ``linear``
+# (round 2 measured against the library GEMM; ``linear`` now runs our small-tile / NT kernels).
 SKINNY_MAX_ROWS = int(os.environ.get("NSA_SKINNY_MAX_ROWS", "16"))
 # residual add + LayerNorm recomputed in the skinny GEMM's prologue (nsa_skinny_ln_gemm) up to
 # this many rows; HIP-graph decode ms/token, 124M / 1.5B: batch 8 0.532 / 3.34 unfused vs
