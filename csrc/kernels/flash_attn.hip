@@ -113,11 +113,11 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3: D = 64 forward kernel; auto = v3
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4 | v5: D = 64 forward kernel; auto = v3
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -129,6 +129,7 @@ FlashConfig& flash_config() {
       d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1
               : (e[0] == 'v' && e[1] == '3') ? FWD_V3
               : (e[0] == 'v' && e[1] == '4') ? FWD_V4
+              : (e[0] == 'v' && e[1] == '5') ? FWD_V5
                                              : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
@@ -908,6 +909,205 @@ __global__ __launch_bounds__(256, 2) void flash_fwd4_kernel(const bf16_t* __rest
       }
       if (h == 0) lse_out[(int64_t)bh * T + qp] = (mu[blk] + __log2f(l)) * 0.6931471805599453f;
     }
+  }
+}
+
+// =============================================================================
+// forward v5 (D = 64, no dropout): eight-wave ping-pong.  One workgroup = 8 waves x 32
+// queries = 256 queries of one (b, h); waves w and w + 4 share a SIMD.  Each wave's tile
+// step is cut into a matrix phase M(j) = {O^T += V_{j-1}^T P_{j-1}^T, S_j^T = K_j Q^T}
+// (16 MFMAs, their LDS reads) and a vector phase V(j) = the online softmax of S_j
+// (max, exp, sum, bf16 pack; 32 scores per lane).  Waves 0-3 run M(j) while waves 4-7
+// run V(j - 1), and the other way round, with one s_barrier per phase, so every SIMD
+// pairs one wave's MFMA stream with its partner's softmax VALU (cdna_hip_programming.md
+// §5.5 / MI355X_MICROARCH.md "Two waves per SIMD"; v3 leaves that pairing to chance and
+// runs at ~25 % MFMA busy with both waves often in the same phase).
+// K/V tiles of 64 keys arrive by LDS-DMA into a 4-slot ring, two pieces per wave per
+// tile: tile t is issued at global phase 2t - 4 (into the slot of tile t - 4, whose last
+// reader, waves 4-7's M(t - 3), ran at phase 2t - 5), and waited for (vmcnt(2): tile t + 1
+// may stay in flight) at the end of phase 2t - 1, before the barrier that opens waves
+// 0-3's M(t).  Numerics are v3's (exp2 of S·c - m·c in fp32, deferred rescale, fp32 l).
+// =============================================================================
+__device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev, const bf16x8 (&qf)[4],
+                                            const bf16x8 (&pf)[2][2], f32x16 (&o)[2], f32x16 (&st)[2], bool prev,
+                                            bool cur, int h, int r, int lane) {
+  constexpr int D = 64;
+  if (prev) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt_prev, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
+      }
+  }
+  if (cur) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      st[sb] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
+    }
+  }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void fwd5_softmax(f32x16 (&st)[2], bf16x8 (&pf)[2][2], f32x16 (&o)[2], float& m_i,
+                                             float& l_i, int kv0, int qpos, int h, float scale_log2) {
+  float mt = -INFINITY;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (MASK) {
+        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
+      }
+      mt = fmaxf(mt, st[sb][i]);
+    }
+  mt = half_swap_max(mt);
+  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
+  if (__builtin_amdgcn_ballot_w64(grow)) {
+    const float m_new = grow ? mt : m_i;
+    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
+    l_i *= alpha;
+    m_i = m_new;
+    o[0] *= alpha;
+    o[1] *= alpha;
+  }
+  const float mc = m_i * scale_log2;
+  float rs = 0.0f;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = fast_exp2(st[sb][i] * scale_log2 - mc);
+      rs += p;
+      pf[sb][i >> 3][i & 7] = (__bf16)p;
+    }
+  l_i += half_swap_sum(rs);
+}
+
+// one phase boundary: nothing of either phase may be scheduled across it
+__device__ __forceinline__ void fwd5_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse_out, int B, int T, int H,
+                                                            float scale_log2) {
+  constexpr int D = 64;
+  constexpr int BN = 64;
+  constexpr int NS = 4;
+  constexpr int TILE_BYTES = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 255) / 256;
+  int bh, qt;
+  attn_order(n_qt, BH, 0, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: every per-wave test is scalar
+  const bool second = wv >= 4;                               // waves 4-7: half a tile step behind
+  const int h = lane >> 5, r = lane & 31;
+  const int q0 = qt * 256;
+  const int q0w = q0 + 32 * wv;  // this wave's queries q0w .. q0w + 31
+  const int qpos = q0w + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+
+  bf16x8 qf[4];
+  {
+    const int qc = qpos < T ? qpos : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
+  }
+  f32x16 o[2] = {f32x16{}, f32x16{}}, st[2];
+  bf16x8 pf[2][2];
+  float m_i = -1e30f, l_i = 0.0f;
+
+  const int kv_end = min(T, q0 + 256);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+  // DMA geometry: a tile is 64 rows x 128 B of K and of V = 16 pieces of 1 KiB (8 rows);
+  // wave wv fills K rows 8 wv .. 8 wv + 7 and V rows 8 wv .. 8 wv + 7
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int prow = 8 * wv + (lane >> 3);
+  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const uint32_t koff = (uint32_t)((prow * (int)row_stride + pch * 8) * 2);
+  auto issue = [&](int jt) {  // wave-uniform; tiles past the end are not fetched
+    if (jt >= n_tiles) return;
+    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
+    uint32_t o0 = koff;
+    if (jt * BN + BN > T) {
+      const int r0 = min(jt * BN + prow, T - 1) - jt * BN;
+      o0 = (uint32_t)((r0 * (int)row_stride + pch * 8) * 2);
+    }
+    const uint32_t kb = lds0 + (uint32_t)((jt % NS) * TILE_BYTES + 8 * wv * 128);
+    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
+    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(kb + NS * TILE_BYTES));
+  };
+  // "tile t landed": tile t + 1's two pieces may stay in flight when it was issued
+  auto wait_tile = [&](int t) {
+    if (t + 1 < n_tiles) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // Q landed before the DMA
+  if (second) __builtin_amdgcn_s_setprio(1);  // the younger half loses VALU arbitration otherwise
+  issue(0);
+  issue(1);
+  wait_tile(0);
+  fwd5_barrier();
+  if (second) {  // global phase 0: waves 0-3 run M(0)
+    issue(2);
+    fwd5_barrier();
+  }
+  for (int j = 0; j <= n_tiles; ++j) {
+    // ---- M(j): PV of tile j - 1, S of tile j
+    if (!second) issue(j + 2);
+    const int kvp = (j - 1) * BN, kv0 = j * BN;
+    const bool prev = j > 0 && kvp <= q0w + 31;
+    const bool cur = j < n_tiles && kv0 <= q0w + 31;
+    fwd5_matrix(smem + (j % NS) * TILE_BYTES, smem + (NS + (j + NS - 1) % NS) * TILE_BYTES, qf, pf, o, st, prev, cur,
+                h, r, lane);
+    if (second) wait_tile(j + 1);  // for waves 0-3's M(j + 1) after the next barrier
+    fwd5_barrier();
+    // ---- V(j): softmax of tile j
+    if (second) issue(j + 3);
+    if (cur) {
+      if (kv0 + BN - 1 <= q0w)
+        fwd5_softmax<false>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
+      else
+        fwd5_softmax<true>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
+    }
+    if (!second) wait_tile(j + 1);
+    if (j < n_tiles || !second) fwd5_barrier();
+  }
+
+  if (qpos < T) {
+    const float inv_l = 1.0f / l_i;
+    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = pack2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
+        u.y = pack2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
+        *reinterpret_cast<uint2*>(orow + d) = u;
+      }
+    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
   }
 }
 
@@ -1865,6 +2065,11 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
+    if (sel == FWD_V5 && !th) {
+      flash_fwd5_kernel<<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+                                                      scale * kLog2e);
+      return hipGetLastError();
+    }
     if (sel == FWD_V4 && !th) {
       flash_fwd4_kernel<4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                           scale * kLog2e);
@@ -2004,7 +2209,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
