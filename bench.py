@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--bias", action="store_true",
+                    help="Linear / LayerNorm biases (nanoGPT bias=True, the GPT-2 checkpoints' layout)")
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible step: fixed-order split-K weight gradients, sorted embedding "
                          "backward, ordered LayerNorm dW/db (no fp32 atomics)")
@@ -135,7 +137,7 @@ def main():
             dataset = args.real_data
     cfg.update(dataset=dataset, data_dir=data_dir, batch_size=args.micro_batch, block_size=args.block_size,
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
-               dropout=0.0, bias=False, compile=False, device=args.device, dtype="bfloat16",
+               dropout=0.0, bias=args.bias, compile=False, device=args.device, dtype="bfloat16",
                backend="nccl" if cuda else "gloo",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
                fp32_residual=not args.bf16_residual, deterministic=args.deterministic,
@@ -218,7 +220,8 @@ def main():
                        "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
                        "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
                        "residual_dtype": "bf16" if args.bf16_residual else "fp32",
-                       "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt)},
+                       "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt),
+                       "bias": args.bias},
             "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1) if cuda else None,
             "mfu_vs_2.5PF": round(mfu, 4),
             "loss": round(lossf, 4),

@@ -117,7 +117,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -130,6 +130,7 @@ FlashConfig& flash_config() {
               : (e[0] == 'v' && e[1] == '3') ? FWD_V3
               : (e[0] == 'v' && e[1] == '4') ? FWD_V4
               : (e[0] == 'v' && e[1] == '5') ? FWD_V5
+              : (e[0] == 'v' && e[1] == '6') ? FWD_V6
                                              : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
@@ -922,15 +923,31 @@ __global__ __launch_bounds__(256, 2) void flash_fwd4_kernel(const bf16_t* __rest
 // pairs one wave's MFMA stream with its partner's softmax VALU (cdna_hip_programming.md
 // §5.5 / MI355X_MICROARCH.md "Two waves per SIMD"; v3 leaves that pairing to chance and
 // runs at ~25 % MFMA busy with both waves often in the same phase).
-// K/V tiles of 64 keys arrive by LDS-DMA into a 4-slot ring, two pieces per wave per
-// tile: tile t is issued at global phase 2t - 4 (into the slot of tile t - 4, whose last
-// reader, waves 4-7's M(t - 3), ran at phase 2t - 5), and waited for (vmcnt(2): tile t + 1
-// may stay in flight) at the end of phase 2t - 1, before the barrier that opens waves
-// 0-3's M(t).  Numerics are v3's (exp2 of S·c - m·c in fp32, deferred rescale, fp32 l).
+// K/V tiles of 64 keys arrive by LDS-DMA into an NS-slot ring (NS = 8: 128 KB), two
+// pieces per wave per tile: tile t is issued at global phase 2 (t - NS + 2) (into the
+// slot of tile t - NS, whose last reader, waves 4-7's M(t - NS + 1), ran one phase
+// earlier) and waited for (tiles t + 1 .. t + NS - 3 may stay in flight) at the end of
+// phase 2t - 1, before the barrier that opens waves 0-3's M(t).  A 4-slot ring (the
+// fetch two phases ahead) measured 506 us against v3's 361: the DMA latency under load
+// outlasts two short phases.  Numerics are v3's (exp2 of S·c - m·c in fp32, deferred
+// rescale, fp32 l).
 // =============================================================================
-__device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev, const bf16x8 (&qf)[4],
-                                            const bf16x8 (&pf)[2][2], f32x16 (&o)[2], f32x16 (&st)[2], bool prev,
-                                            bool cur, int h, int r, int lane) {
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
+__device__ __forceinline__ void vm_wait(int n) {
+#define NSA_VMW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
+    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+#undef NSA_VMW
+}
+
+template <bool VPRE>
+__device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev, const bf16x8 (&vfr)[2][2][2],
+                                            const bf16x8 (&qf)[4], const bf16x8 (&pf)[2][2], f32x16 (&o)[2],
+                                            f32x16 (&st)[2], bool prev, bool cur, int h, int r, int lane) {
   constexpr int D = 64;
   if (prev) {
 #pragma unroll
@@ -939,7 +956,8 @@ __device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev,
       for (int s = 0; s < 2; ++s) {
         const int r0 = 32 * sb + 16 * s + 4 * h;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt_prev, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = mfma(VPRE ? vfr[sb][s][dt] : tr_frag<D>(vt_prev, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
       }
   }
   if (cur) {
@@ -951,6 +969,20 @@ __device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev,
         st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
     }
   }
+}
+
+// V_j^T fragments of the P·V product, read at the end of the softmax phase V(j) (tile j
+// is visible since the barrier that opened M(j)) so that M(j + 1) starts on MFMAs
+__device__ __forceinline__ void fwd5_vload(const char* vt, bf16x8 (&vfr)[2][2][2], int h, int lane) {
+  constexpr int D = 64;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) vfr[sb][s][dt] = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
+    }
 }
 
 template <bool MASK>
@@ -996,12 +1028,16 @@ __device__ __forceinline__ void fwd5_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifndef NSA_FWD5_NS
+#define NSA_FWD5_NS 8
+#endif
+template <bool VPRE>
 __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
                                                             float scale_log2) {
   constexpr int D = 64;
   constexpr int BN = 64;
-  constexpr int NS = 4;
+  constexpr int NS = NSA_FWD5_NS;  // ring slots: tile t is fetched 2 (NS - 2) phases ahead
   constexpr int TILE_BYTES = BN * D * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
 
@@ -1032,7 +1068,7 @@ __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __rest
       qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
   }
   f32x16 o[2] = {f32x16{}, f32x16{}}, st[2];
-  bf16x8 pf[2][2];
+  bf16x8 pf[2][2], vfr[2][2][2];
   float m_i = -1e30f, l_i = 0.0f;
 
   const int kv_end = min(T, q0 + 256);
@@ -1056,39 +1092,38 @@ __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __rest
     glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
     glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(kb + NS * TILE_BYTES));
   };
-  // "tile t landed": tile t + 1's two pieces may stay in flight when it was issued
-  auto wait_tile = [&](int t) {
-    if (t + 1 < n_tiles) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
+  // "tile t landed": at the end of phase 2t - 1 tiles t + 1 .. t + NS - 3 were issued
+  // after it (those inside the sequence), two pieces each, and may stay in flight
+  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_tiles - 1 - t))); };
 
   asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // Q landed before the DMA
   if (second) __builtin_amdgcn_s_setprio(1);  // the younger half loses VALU arbitration otherwise
-  issue(0);
-  issue(1);
+#pragma unroll
+  for (int t = 0; t < NS - 2; ++t) issue(t);  // tile t is issued at global phase 2 (t - NS + 2)
   wait_tile(0);
   fwd5_barrier();
   if (second) {  // global phase 0: waves 0-3 run M(0)
-    issue(2);
+    issue(NS - 2);
     fwd5_barrier();
   }
   for (int j = 0; j <= n_tiles; ++j) {
     // ---- M(j): PV of tile j - 1, S of tile j
-    if (!second) issue(j + 2);
+    if (!second) issue(j + NS - 2);
     const int kvp = (j - 1) * BN, kv0 = j * BN;
     const bool prev = j > 0 && kvp <= q0w + 31;
     const bool cur = j < n_tiles && kv0 <= q0w + 31;
-    fwd5_matrix(smem + (j % NS) * TILE_BYTES, smem + (NS + (j + NS - 1) % NS) * TILE_BYTES, qf, pf, o, st, prev, cur,
-                h, r, lane);
+    fwd5_matrix<VPRE>(smem + (j % NS) * TILE_BYTES, smem + (NS + (j + NS - 1) % NS) * TILE_BYTES, vfr, qf, pf, o,
+                      st, prev, cur, h, r, lane);
     if (second) wait_tile(j + 1);  // for waves 0-3's M(j + 1) after the next barrier
     fwd5_barrier();
     // ---- V(j): softmax of tile j
-    if (second) issue(j + 3);
+    if (second) issue(j + NS - 1);
     if (cur) {
       if (kv0 + BN - 1 <= q0w)
         fwd5_softmax<false>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
       else
         fwd5_softmax<true>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
+      if constexpr (VPRE) fwd5_vload(smem + (NS + j % NS) * TILE_BYTES, vfr, h, lane);
     }
     if (!second) wait_tile(j + 1);
     if (j < n_tiles || !second) fwd5_barrier();
@@ -1603,18 +1638,6 @@ __device__ __forceinline__ void slot_dispatch(int k, F& f) {
   }
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
-__device__ __forceinline__ void vm_wait(int n) {
-#define NSA_VMW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-  switch (n) {
-    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
-    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-  }
-#undef NSA_VMW
-}
-
 // one 32-query slice for one wave: S, dP for its NKB key blocks, P / dS, then dV^T, dK^T.
 // ld = this wave's copy of the slice's row constants: [0, 32) -lse/scale, [32, 64) -delta.
 template <int NKB, bool MASK, bool DROP>
@@ -2065,9 +2088,13 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if (sel == FWD_V5 && !th) {
-      flash_fwd5_kernel<<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                      scale * kLog2e);
+    if ((sel == FWD_V5 || sel == FWD_V6) && !th) {  // v6: v5 without the V-fragment prefetch (A/B)
+      if (sel == FWD_V5)
+        flash_fwd5_kernel<true><<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
+                                                              H, scale * kLog2e);
+      else
+        flash_fwd5_kernel<false><<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
+                                                               H, scale * kLog2e);
       return hipGetLastError();
     }
     if (sel == FWD_V4 && !th) {
@@ -2209,7 +2236,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;

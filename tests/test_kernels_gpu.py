@@ -455,7 +455,7 @@ def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
     assert e < 5e-3, f"v3 vs v1 rel err {e}"
 
 
-@pytest.mark.parametrize("ver", ["v4", "v5"])
+@pytest.mark.parametrize("ver", ["v4", "v5", "v6"])
 @pytest.mark.parametrize("T", [384, 1024, 200, 64, 40])
 def test_flash_fwd_variant_matches_v1(kernels, flash_variant, T, ver):
     """Forward v4 (max shift and row sum on the MFMA pipe, Q pre-scaled) and v5 (eight-wave
