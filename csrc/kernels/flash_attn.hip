@@ -113,11 +113,11 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4 | v5: D = 64 forward kernel; auto = v3
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v5 | v6: D = 64 forward kernel; auto = v3
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -128,7 +128,6 @@ FlashConfig& flash_config() {
     if (const char* e = getenv("NSA_FLASH_FWD"))
       d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1
               : (e[0] == 'v' && e[1] == '3') ? FWD_V3
-              : (e[0] == 'v' && e[1] == '4') ? FWD_V4
               : (e[0] == 'v' && e[1] == '5') ? FWD_V5
               : (e[0] == 'v' && e[1] == '6') ? FWD_V6
                                              : FWD_AUTO;
@@ -685,230 +684,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
       }
       if (h == 0)
         lse_out[(int64_t)bh * T + qp] = (m_i[blk] * scale_log2 + __log2f(l_i[blk])) * 0.6931471805599453f;
-    }
-  }
-}
-
-// =============================================================================
-// forward v4 (D = 64, no dropout): v3's geometry (two 32-query blocks per wave, 4-slot
-// LDS-DMA K/V ring) with two of the softmax's three VALU passes moved onto the matrix
-// pipe, which v3 leaves three-quarters idle (PMC: 12.6 VALU instructions per MFMA, the
-// SIMD's issue port, not the MFMA pipe, is the limit):
-//  * the max shift: Q is pre-scaled by log2(e)/sqrt(D) when it is loaded, and one extra
-//    k-step per S tile (A = e_0 "ones in column 0", B = the running max -m in row 0)
-//    makes the MFMA chain produce S·c - m directly: p = exp2(acc), no per-element fma.
-//    The shift m is kept as a bf16 value and used consistently (exp, rescale, LSE), so
-//    its rounding cancels out of P / l;
-//  * the row sum l = P·1: one extra MFMA per P fragment with an all-ones A operand
-//    accumulates l into a 32x32 tile (every row = the sum), no per-element add.
-// Per 64-key tile and wave: 44 MFMAs (32 useful), 64 v_exp, 32 v_max3, 32 v_cvt_pk
-// (v3: 32 MFMAs beside 62 fma + 64 add on top of those).  Deferred rescale as v1/v3.
-// =============================================================================
-template <bool MASK>
-__device__ __forceinline__ void fwd_tile4(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
-                                          bf16x8 (&shf)[2], const bf16x8& e0, const bf16x8 (&ones)[2],
-                                          f32x16 (&o)[2][2], f32x16& la, float (&mu)[2], bool first, int kv0,
-                                          int qposA, int h, int r, int lane) {
-  constexpr int D = 64;
-  f32x16 st[2][2];  // [block][key sub-block] = S·c - m (log2 units)
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[0][sb] = mfma(e0, shf[0], f32x16{});
-    st[1][sb] = mfma(e0, shf[1], f32x16{});
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
-      st[0][sb] = mfma(kf, qf[0][ks], st[0][sb]);
-      st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
-    }
-  }
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    float mt = -INFINITY;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if constexpr (MASK) {
-          if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) st[blk][sb][i] = -INFINITY;
-        }
-        mt = fmaxf(mt, st[blk][sb][i]);
-      }
-    }
-    mt = half_swap_max(mt);  // this tile's max relative to the shift
-    const bool grow = first || mt > kDeferLog2;
-    if (__builtin_amdgcn_ballot_w64(grow)) {
-      float dl = 0.0f;
-      if (grow) {
-        const float m_new = (float)(__bf16)(mu[blk] + mt);  // the shift stays bf16-exact
-        dl = m_new - mu[blk];
-        mu[blk] = m_new;
-        shf[blk][0] = (__bf16)(-m_new);
-      }
-      const float alpha = fast_exp2(-dl);
-      o[blk][0] *= alpha;
-      o[blk][1] *= alpha;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) la[8 * blk + i] *= alpha;  // this block's rows of the sum tile
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) st[blk][sb] -= dl;
-    }
-  }
-  // per key sub-block: P in bf16 (consumed right away: st[.][sb] dies here), O^T += V^T·P^T,
-  // and the row sums (block A into rows 0-15 of la, block B into rows 16-31)
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    bf16x8 pf[2][2];
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) pf[blk][i >> 3][i & 7] = (__bf16)fast_exp2(st[blk][sb][i]);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
-        o[0][dt] = mfma(vf, pf[0][s], o[0][dt]);
-        o[1][dt] = mfma(vf, pf[1][s], o[1][dt]);
-      }
-      la = mfma(ones[0], pf[0][s], la);
-      la = mfma(ones[1], pf[1][s], la);
-    }
-  }
-}
-
-template <int NS>
-__global__ __launch_bounds__(256, 2) void flash_fwd4_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2) {
-  static_assert(NS >= 2 && NS <= 4, "ring slots");
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int TILE_BYTES = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
-
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int h = lane >> 5, r = lane & 31;
-  const int q0 = qt * 256;
-  const int q0w = q0 + 64 * w;
-  const int qposA = q0w + r;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-
-  // Q^T fragments pre-scaled by c = log2(e)/sqrt(D) (S·c comes straight out of the MFMAs)
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qp = qposA + 32 * blk;
-    const int qc = qp < T ? qp : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const uint4 u = *reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h);
-      float f[8];
-      unpack8(u, f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qf[blk][ks][e] = (__bf16)(f[e] * scale_log2);
-    }
-  }
-  // e0: A operand with a 1 in column k = 0 of every row (the shift's k-step); ones[blk]:
-  // ones in the rows of block blk's half of the row-sum tile (rows 0-15 / 16-31), so one
-  // accumulator holds both blocks' sums (register i < 8: block A, i >= 8: block B)
-  bf16x8 e0, ones[2], shf[2];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    e0[e] = (__bf16)((h == 0 && e == 0) ? 1.0f : 0.0f);
-    ones[0][e] = (__bf16)(r < 16 ? 1.0f : 0.0f);
-    ones[1][e] = (__bf16)(r >= 16 ? 1.0f : 0.0f);
-    shf[0][e] = (__bf16)0.0f;
-    shf[1][e] = (__bf16)0.0f;
-  }
-  f32x16 o[2][2], la = f32x16{};
-  float mu[2];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    o[blk][0] = f32x16{};
-    o[blk][1] = f32x16{};
-    mu[blk] = 0.0f;
-  }
-
-  const int kv_end = min(T, q0 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int prow = 16 * w + (lane >> 3);
-  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
-  const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
-  const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
-  auto issue = [&](int jt, int buf) {
-    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
-    uint32_t o0 = koff0, o8 = koff8;
-    if (jt * BN + BN > T) {
-      const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
-      o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
-      o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
-    }
-    const uint32_t kb = lds0 + (uint32_t)(buf * TILE_BYTES + 16 * w * 128);
-    const uint32_t vb = kb + NS * TILE_BYTES;
-    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
-    glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
-    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
-    glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
-  };
-  auto wait_next = [&]() {
-    if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  };
-  asm volatile("" ::"v"(qf[0][0]), "v"(qf[0][1]), "v"(qf[0][2]), "v"(qf[0][3]), "v"(qf[1][0]), "v"(qf[1][1]),
-               "v"(qf[1][2]), "v"(qf[1][3]));  // Q landed before the DMA
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t) issue(min(t, n_tiles - 1), t);
-  wait_next();
-  __syncthreads();
-  for (int j = 0; j < n_tiles; ++j) {
-    const int cur = j % NS;
-    const int kv0 = j * BN;
-    issue(min(j + NS - 1, n_tiles - 1), (j + NS - 1) % NS);
-    const char* kt = smem + cur * TILE_BYTES;
-    const char* vt = smem + (NS + cur) * TILE_BYTES;
-    if (kv0 + BN - 1 <= q0w)
-      fwd_tile4<false>(kt, vt, qf, shf, e0, ones, o, la, mu, j == 0, kv0, qposA, h, r, lane);
-    else if (kv0 <= q0w + 63)
-      fwd_tile4<true>(kt, vt, qf, shf, e0, ones, o, la, mu, j == 0, kv0, qposA, h, r, lane);
-    wait_next();
-    __syncthreads();
-  }
-
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qp = qposA + 32 * blk;
-    if (qp < T) {
-      const float l = la[8 * blk];
-      const float inv_l = 1.0f / l;
-      bf16_t* orow = out + ((int64_t)b * T + qp) * C + hh * D;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = 32 * dt + 8 * g + 4 * h;
-          uint2 u;
-          u.x = pack2(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
-          u.y = pack2(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
-          *reinterpret_cast<uint2*>(orow + d) = u;
-        }
-      }
-      if (h == 0) lse_out[(int64_t)bh * T + qp] = (mu[blk] + __log2f(l)) * 0.6931471805599453f;
     }
   }
 }
@@ -2097,11 +1872,6 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
                                                                H, scale * kLog2e);
       return hipGetLastError();
     }
-    if (sel == FWD_V4 && !th) {
-      flash_fwd4_kernel<4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                          scale * kLog2e);
-      return hipGetLastError();
-    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -2236,7 +2006,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
