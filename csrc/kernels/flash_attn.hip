@@ -115,10 +115,11 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 // through nsa_flash_set_variant (tests / A/B scripts):
 //   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v5 | v6: D = 64 forward kernel; auto = v3
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
-//   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
+//   bwd   NSA_FLASH_BWD = v2 (default) | v1 | v3: D = 64 backward (v1 = the generic kernels,
+//         v3 = the ping-pong dQ kernel beside the v2 dK/dV kernel)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
 enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6 };
-enum { BWD_V1 = 1, BWD_V2 = 2 };
+enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
@@ -131,7 +132,8 @@ FlashConfig& flash_config() {
               : (e[0] == 'v' && e[1] == '5') ? FWD_V5
               : (e[0] == 'v' && e[1] == '6') ? FWD_V6
                                              : FWD_AUTO;
-    if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
+    if (const char* e = getenv("NSA_FLASH_BWD"))
+      d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : (e[0] == 'v' && e[1] == '3') ? BWD_V3 : BWD_V2;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
     return d;
   }();
@@ -1939,6 +1941,197 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
 // constants -delta, -lse/scale) -> the dK/dV v2 kernel, 1 key block per wave, 4 waves
 // (two independent workgroups per CU).  ws = 2 x [B, H, T] fp32.  A/B at B120 T1024 H12
 // (whole backward): v1 1307, 2 key blocks per wave 1304, 8 waves 1203, this 1189 us.
+// =============================================================================
+// dQ kernel v3 (D = 64, no dropout): the v2 dQ algebra on the forward v5's eight-wave
+// ping-pong.  One workgroup = 8 waves x 32 queries = 256 queries of one (b, h); waves w
+// and w + 4 share a SIMD and alternate
+//   M(j) = {dQ^T += K_{j-1}^T dS_{j-1}^T (8 MFMAs), S_j^T = K_j Q^T, dP_j^T = V_j dO^T (16)}
+//   V(j) = {P = exp2(c S - lse log2e), dS = P (dP - delta), bf16 pack; K_j^T fragments
+//           for the next dQ product read from LDS}
+// with one s_barrier per phase (waves 4-7 half a tile behind), so each SIMD pairs one
+// wave's matrix stream with its partner's vector work.  K / V tiles (64 keys) arrive by
+// LDS-DMA into an 8-slot ring on the forward v5 schedule (tile t issued at global phase
+// 2 (t - NS + 2), waited for at the end of phase 2t - 1).  Like v2 it forms delta and
+// the row constants for the dK/dV kernel, and writes dQ once in bf16.
+// =============================================================================
+__device__ __forceinline__ void dq3_matrix(const char* kt, const bf16x8 (&qf)[4], const bf16x8 (&gf)[4],
+                                           const f32x16& ndt, const bf16x8 (&ktr)[2][2][2],
+                                           const bf16x8 (&dsf)[2][2], f32x16 (&dq)[2], f32x16 (&st)[2],
+                                           f32x16 (&pt)[2], bool prev, bool cur, int h, int r) {
+  constexpr int D = 64;
+  if (prev) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(ktr[sb][s][dt], dsf[sb][s], dq[dt]);
+  }
+  if (cur) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      st[sb] = f32x16{};
+      pt[sb] = ndt;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
+        pt[sb] = mfma(as_frag(lds_b128(kt + DQ2_T, swz<D>(32 * sb + r, 2 * ks + h))), gf[ks], pt[sb]);
+      }
+    }
+  }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void dq3_vector(const char* kt, f32x16 (&st)[2], f32x16 (&pt)[2],
+                                           bf16x8 (&dsf)[2][2], bf16x8 (&ktr)[2][2][2], float lse2, int kv0,
+                                           int qpos, int h, int lane, float scale_log2) {
+  constexpr int D = 64;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    float dsv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
+      if constexpr (MASK) p = kv0 + 32 * sb + acc_row(i, h) > qpos ? 0.0f : p;
+      dsv[i] = p * pt[sb][i];
+    }
+    pack16(dsv, dsf[sb]);
+  }
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) ktr[sb][s][dt] = tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane);
+    }
+}
+
+#ifndef NSA_DQ3_NS
+#define NSA_DQ3_NS 8
+#endif
+__global__ __launch_bounds__(512, 1) void flash_bwd_dq3_kernel(const bf16_t* __restrict__ qkv,
+                                                               const bf16_t* __restrict__ dout,
+                                                               const bf16_t* __restrict__ o,
+                                                               const float* __restrict__ lse, float* __restrict__ nls,
+                                                               float* __restrict__ nd, bf16_t* __restrict__ dqkv,
+                                                               int B, int T, int H, float scale, float scale_log2) {
+  constexpr int D = 64;
+  constexpr int BN = 64;
+  constexpr int NS = NSA_DQ3_NS;
+  constexpr int SLOT = 2 * DQ2_T;  // K, V
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 255) / 256;
+  int bh, qt;
+  attn_order(n_qt, BH, 0, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool second = wv >= 4;
+  const int h = lane >> 5, r = lane & 31;
+  const int q0w = qt * 256 + 32 * wv;
+  const int qpos = q0w + r;
+  const int qc = qpos < T ? qpos : T - 1;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int kv_end = min(T, qt * 256 + 256);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+
+  // K / V tile t -> slot t % NS: 8 + 8 pieces of 8 rows x 128 B; wave wv copies K rows and
+  // V rows 8 wv .. 8 wv + 7, XOR swizzle on the per-lane source chunk
+  const int prow = 8 * wv + (lane >> 3);
+  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const bf16_t* kb0 = base + C + hh * D;
+  auto issue = [&](int t) {
+    if (t >= n_tiles) return;
+    int row = t * BN + prow;
+    row = row < T ? row : T - 1;  // rows past T re-read row T - 1 (their keys are masked)
+    const bf16_t* src = kb0 + (int64_t)row * row_stride + pch * 8;
+    const uint32_t sb = lds0 + (uint32_t)((t % NS) * SLOT + 8 * wv * 128);
+    glds16(src, sb);
+    glds16(src + C, sb + DQ2_T);
+  };
+  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_tiles - 1 - t))); };
+
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
+    gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
+  }
+  float dpart = 0.0f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    float fo[8], fg[8];
+    load8(o + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h, fo);
+    unpack8(__builtin_bit_cast(uint4, gf[ks]), fg);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dpart += fo[e] * fg[e];
+  }
+  const float ndl = -half_swap_sum(dpart);
+  const float lse_q = lse[(int64_t)bh * T + qc];
+  const float lse2 = lse_q * kLog2e;
+  if (h == 0 && qpos < T) {
+    nd[(int64_t)bh * T + qpos] = ndl;
+    nls[(int64_t)bh * T + qpos] = -lse_q / scale;
+  }
+  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(gf[0]), "v"(gf[1]), "v"(gf[2]),
+               "v"(gf[3]), "v"(lse2), "v"(ndl));  // retire these loads before the DMA ring
+  f32x16 ndt;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ndt[i] = ndl;
+  f32x16 dq[2] = {f32x16{}, f32x16{}}, st[2], pt[2];
+  bf16x8 dsf[2][2], ktr[2][2][2];
+
+  if (second) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int t = 0; t < NS - 2; ++t) issue(t);
+  wait_tile(0);
+  fwd5_barrier();
+  if (second) {
+    issue(NS - 2);
+    fwd5_barrier();
+  }
+  for (int j = 0; j <= n_tiles; ++j) {
+    if (!second) issue(j + NS - 2);
+    const int kv0 = j * BN;
+    const bool prev = j > 0 && (j - 1) * BN <= q0w + 31;
+    const bool cur = j < n_tiles && kv0 <= q0w + 31;
+    dq3_matrix(smem + (j % NS) * SLOT, qf, gf, ndt, ktr, dsf, dq, st, pt, prev, cur, h, r);
+    if (second) wait_tile(j + 1);
+    fwd5_barrier();
+    if (second) issue(j + NS - 1);
+    if (cur) {
+      const char* kt = smem + (j % NS) * SLOT;
+      if (kv0 + BN - 1 <= q0w)
+        dq3_vector<false>(kt, st, pt, dsf, ktr, lse2, kv0, qpos, h, lane, scale_log2);
+      else
+        dq3_vector<true>(kt, st, pt, dsf, ktr, lse2, kv0, qpos, h, lane, scale_log2);
+    }
+    if (!second) wait_tile(j + 1);
+    if (j < n_tiles || !second) fwd5_barrier();
+  }
+
+  if (qpos < T) {
+    bf16_t* qrow = dqkv + ((int64_t)b * T + qpos) * row_stride + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 u;
+        u.x = cvt2(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
+        u.y = cvt2(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(qrow + d) = u;
+      }
+  }
+}
+
 hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws, void* dqkv,
                          int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
   float* nd = (float*)ws;
@@ -1947,7 +2140,11 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_qt = (T + 127) / 128;
   const int order = attn_order_env();
-  if (th)
+  if (flash_config().bwd == BWD_V3 && !th)
+    flash_bwd_dq3_kernel<<<(T + 255) / 256 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                                 (const bf16_t*)o, (const float*)lse, nls, nd,
+                                                                 (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e);
+  else if (th)
     flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                             (const bf16_t*)o, (const float*)lse, nls, nd, (bf16_t*)dqkv,
                                                             B, T, H, scale, scale * kLog2e, th, dscale, seed, order);
@@ -1978,7 +2175,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
 NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (D == 64 && T % 32 == 0 && flash_config().bwd == BWD_V2)
+  if (D == 64 && T % 32 == 0 && (flash_config().bwd == BWD_V2 || flash_config().bwd == BWD_V3))
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
     case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
@@ -2007,7 +2204,7 @@ NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
-  if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
+  if (bwd == BWD_V1 || bwd == BWD_V2 || bwd == BWD_V3) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
 }

@@ -436,6 +436,28 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
 
 
+@pytest.mark.parametrize("T", [1024, 320, 96, 64])
+def test_flash_bwd_v3_matches_v2(kernels, flash_variant, T):
+    """The v3 backward (eight-wave ping-pong dQ kernel beside the v2 dK/dV kernel) against
+    v2: all three gradients and the row constants it hands to the dK/dV kernel."""
+    from nanosandbox_amd.ops import functional as fn
+
+    torch.manual_seed(0)
+    B, H, D = 2, 3, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
+    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
+    grads = {}
+    for ver in ("v2", "v3"):
+        flash_variant(bwd=ver)
+        x = qkv.clone().requires_grad_(True)
+        fn.attention(x, H, 0.0, True).backward(dy)
+        torch.cuda.synchronize()
+        grads[ver] = x.grad.float().view(B, T, 3, H * D)
+    for i, name in enumerate("qkv"):
+        e = rel_err(grads["v3"][:, :, i], grads["v2"][:, :, i])
+        assert e < 1e-3, f"d{name}: v3 vs v2 rel err {e}"
+
+
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
     """Forward v3 (64 queries per wave, LDS-DMA ring) against v1, with and without dropout
