@@ -116,10 +116,10 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v5 | v6: D = 64 forward kernel; auto = v3
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1 | v3: D = 64 backward (v1 = the generic kernels,
-//         v3 = the ping-pong dQ kernel beside the v2 dK/dV kernel)
+//         v3 = the ping-pong dQ kernel beside the v2 dK/dV kernel, v4 = both ping-pong)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
 enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6 };
-enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
+enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3, BWD_V4 = 4 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
@@ -133,7 +133,9 @@ FlashConfig& flash_config() {
               : (e[0] == 'v' && e[1] == '6') ? FWD_V6
                                              : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
-      d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : (e[0] == 'v' && e[1] == '3') ? BWD_V3 : BWD_V2;
+      d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : (e[0] == 'v' && e[1] == '3') ? BWD_V3
+              : (e[0] == 'v' && e[1] == '4') ? BWD_V4
+                                             : BWD_V2;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
     return d;
   }();
@@ -1942,6 +1944,190 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
 // (two independent workgroups per CU).  ws = 2 x [B, H, T] fp32.  A/B at B120 T1024 H12
 // (whole backward): v1 1307, 2 key blocks per wave 1304, 8 waves 1203, this 1189 us.
 // =============================================================================
+// dK / dV kernel v3 (D = 64, no dropout): the v2 algebra (key on the lane, row constants
+// as initial accumulators, dK^T / dV^T resident) on the eight-wave ping-pong of forward
+// v5.  One workgroup = 8 waves x 32 keys = 256 keys of one (b, h); it sweeps 32-query
+// slices, each phase pair doing for one wave
+//   M(j) = {dV^T += dO_{j-1}^T P_{j-1}, dK^T += Q_{j-1}^T dS_{j-1} (8 MFMAs),
+//           S_j = Q_j K^T - lse/scale, dP_j = dO_j V^T - delta (8 MFMAs)}
+//   V(j) = {P = exp2(c S), dS = P dP, bf16 pack; Q_j^T / dO_j^T fragments for the next
+//           M read from LDS}
+// with waves 4-7 half a slice behind waves 0-3 (one s_barrier per phase).  Slices (Q,
+// dO [32][64] tiles + per-wave row-constant copies, 10 KB) arrive by LDS-DMA into an
+// 8-slot ring on the forward v5 schedule; every wave issues two pieces per slice (waves
+// 0-3 a Q piece, waves 4-7 a dO piece, each wave its row constants).
+// =============================================================================
+constexpr int DKV3_SLOT = 2 * V2_QT + 8 * 256;
+
+__device__ __forceinline__ void dkdv3_matrix(const char* qt, const float* ld, const bf16x8 (&kf)[4],
+                                             const bf16x8 (&vf)[4], const bf16x8 (&trf)[2][2][2],
+                                             const bf16x8 (&pfr)[2], const bf16x8 (&dsfr)[2], f32x16 (&dk)[2],
+                                             f32x16 (&dv)[2], f32x16& sacc, f32x16& pacc, bool prev, bool cur,
+                                             int h, int r) {
+  constexpr int D = 64;
+  if (prev) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        dv[dt] = mfma(trf[s][dt][0], pfr[s], dv[dt]);
+        dk[dt] = mfma(trf[s][dt][1], dsfr[s], dk[dt]);
+      }
+  }
+  if (cur) {
+    sacc = row_consts(ld, h);
+    pacc = row_consts(ld + 32, h);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      sacc = mfma(as_frag(lds_b128(qt, swz<D>(r, 2 * ks + h))), kf[ks], sacc);
+      pacc = mfma(as_frag(lds_b128(qt + V2_QT, swz<D>(r, 2 * ks + h))), vf[ks], pacc);
+    }
+  }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void dkdv3_vector(const char* qt, const f32x16& sacc, const f32x16& pacc,
+                                             bf16x8 (&pfr)[2], bf16x8 (&dsfr)[2], bf16x8 (&trf)[2][2][2], int q0,
+                                             int key, int h, int lane, float scale_log2) {
+  constexpr int D = 64;
+  float pv[16], dsv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float p = fast_exp2(sacc[i] * scale_log2);
+    if constexpr (MASK) p = key > q0 + acc_row(i, h) ? 0.0f : p;
+    pv[i] = p;
+    dsv[i] = p * pacc[i];
+  }
+  pack16(pv, pfr);
+  pack16(dsv, dsfr);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int r0 = 16 * s + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      trf[s][dt][0] = tr_frag<D>(qt + V2_QT, r0, r0 + 8, 32 * dt, lane);  // dO^T
+      trf[s][dt][1] = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);          // Q^T
+    }
+  }
+}
+
+#ifndef NSA_DKV3_NS
+#define NSA_DKV3_NS 8
+#endif
+__global__ __launch_bounds__(512, 1) void flash_bwd_dkdv3_kernel(const bf16_t* __restrict__ qkv,
+                                                                 const bf16_t* __restrict__ dout,
+                                                                 const float* __restrict__ nls,
+                                                                 const float* __restrict__ nd,
+                                                                 bf16_t* __restrict__ dqkv, int B, int T, int H,
+                                                                 float scale, float scale_log2) {
+  constexpr int D = 64;
+  constexpr int KWG = 256;
+  constexpr int NS = NSA_DKV3_NS;
+  constexpr int SLOT = DKV3_SLOT;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  int bh, kbw;  // key blocks near 0 see the most queries: launched first
+  attn_order((T + KWG - 1) / KWG, BH, 0, bh, kbw);
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool second = wv >= 4;
+  const int h = lane >> 5, r = lane & 31;
+  const int k0 = kbw * KWG;
+  const int kw = k0 + 32 * wv;
+  const int key = kw + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const float* nls_bh = nls + (int64_t)bh * T;
+  const float* nd_bh = nd + (int64_t)bh * T;
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int s_first = k0 / 32;
+  const int n_mine = max(0, T / 32 - s_first);
+
+  // slice t (queries 32 (s_first + t) ..) -> slot t % NS: waves 0-3 copy Q rows 8 (wv & 3)
+  // .. +7, waves 4-7 the same dO rows; each wave its own row-constant copy
+  const int prow = 8 * (wv & 3) + (lane >> 3);
+  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const bf16_t* tsrc = second ? dout + (int64_t)b * T * C + hh * D + (int64_t)prow * C + pch * 8
+                              : base + hh * D + (int64_t)prow * row_stride + pch * 8;
+  const int64_t tstride = second ? 32 * (int64_t)C : 32 * row_stride;  // per slice
+  const float* csrc = (h == 0 ? nls_bh : nd_bh) + r;
+  auto issue = [&](int t) {
+    if (t >= n_mine) return;
+    const uint32_t sb = lds0 + (uint32_t)((t % NS) * SLOT);
+    glds16(tsrc + (int64_t)(s_first + t) * tstride, sb + (uint32_t)((second ? V2_QT : 0) + 8 * (wv & 3) * 128));
+    glds4(csrc + (s_first + t) * 32, sb + (uint32_t)(2 * V2_QT + wv * 256));
+  };
+  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_mine - 1 - t))); };
+
+  bf16x8 kf[4], vf[4];
+  {
+    const int kc = key < T ? key : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + C + hh * D + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+      vf[ks] =
+          as_frag(*reinterpret_cast<const uint4*>(base + 2 * C + hh * D + (int64_t)kc * row_stride + 16 * ks + 8 * h));
+    }
+  }
+  asm volatile("" ::"v"(kf[0]), "v"(kf[1]), "v"(kf[2]), "v"(kf[3]), "v"(vf[0]), "v"(vf[1]), "v"(vf[2]),
+               "v"(vf[3]));  // retire the fragment loads before the DMA ring (see dK/dV v2)
+  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}}, sacc, pacc;
+  bf16x8 pfr[2], dsfr[2], trf[2][2][2];
+
+  if (second) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int t = 0; t < NS - 2; ++t) issue(t);
+  wait_tile(0);
+  fwd5_barrier();
+  if (second) {
+    issue(NS - 2);
+    fwd5_barrier();
+  }
+  const int jd = wv;  // this wave's diagonal slice (keys kw .. kw + 31 = queries of slice jd)
+  for (int j = 0; j <= n_mine; ++j) {
+    if (!second) issue(j + NS - 2);
+    const bool prev = j > jd && j - 1 < n_mine;
+    const bool cur = j >= jd && j < n_mine;
+    const char* qt = smem + (j % NS) * SLOT;
+    dkdv3_matrix(qt, reinterpret_cast<const float*>(qt + 2 * V2_QT) + wv * 64, kf, vf, trf, pfr, dsfr, dk, dv,
+                 sacc, pacc, prev, cur, h, r);
+    if (second) wait_tile(j + 1);
+    fwd5_barrier();
+    if (second) issue(j + NS - 1);
+    if (cur) {
+      const int q0 = (s_first + j) * 32;
+      if (j > jd)
+        dkdv3_vector<false>(qt, sacc, pacc, pfr, dsfr, trf, q0, key, h, lane, scale_log2);
+      else
+        dkdv3_vector<true>(qt, sacc, pacc, pfr, dsfr, trf, q0, key, h, lane, scale_log2);
+    }
+    if (!second) wait_tile(j + 1);
+    if (j < n_mine || !second) fwd5_barrier();
+  }
+
+  if (key < T) {
+    bf16_t* krow = dqkv + ((int64_t)b * T + key) * row_stride + C + hh * D;
+    bf16_t* vrow = krow + C;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 uk, uv;
+        uk.x = cvt2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+        uk.y = cvt2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        uv.x = cvt2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+        uv.y = cvt2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(krow + d) = uk;
+        *reinterpret_cast<uint2*>(vrow + d) = uv;
+      }
+  }
+}
+
+// =============================================================================
 // dQ kernel v3 (D = 64, no dropout): the v2 dQ algebra on the forward v5's eight-wave
 // ping-pong.  One workgroup = 8 waves x 32 queries = 256 queries of one (b, h); waves w
 // and w + 4 share a SIMD and alternate
@@ -2140,7 +2326,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_qt = (T + 127) / 128;
   const int order = attn_order_env();
-  if (flash_config().bwd == BWD_V3 && !th)
+  if (flash_config().bwd >= BWD_V3 && !th)
     flash_bwd_dq3_kernel<<<(T + 255) / 256 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                                  (const bf16_t*)o, (const float*)lse, nls, nd,
                                                                  (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e);
@@ -2156,7 +2342,10 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int n_kb = (T + 127) / 128;
-  if (th)
+  if (flash_config().bwd == BWD_V4 && !th)
+    flash_bwd_dkdv3_kernel<<<(T + 255) / 256 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
+                                                                   (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e);
+  else if (th)
     flash_bwd_dkdv2_kernel<1, 4, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
                                                                    (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
                                                                    dscale, seed, order);
@@ -2175,7 +2364,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
 NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (D == 64 && T % 32 == 0 && (flash_config().bwd == BWD_V2 || flash_config().bwd == BWD_V3))
+  if (D == 64 && T % 32 == 0 && flash_config().bwd >= BWD_V2)
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
     case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
@@ -2204,7 +2393,7 @@ NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
-  if (bwd == BWD_V1 || bwd == BWD_V2 || bwd == BWD_V3) c.bwd = bwd;
+  if (bwd >= BWD_V1 && bwd <= BWD_V4) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
 }

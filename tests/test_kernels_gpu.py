@@ -436,10 +436,11 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
 
 
+@pytest.mark.parametrize("ver", ["v3", "v4"])
 @pytest.mark.parametrize("T", [1024, 320, 96, 64])
-def test_flash_bwd_v3_matches_v2(kernels, flash_variant, T):
-    """The v3 backward (eight-wave ping-pong dQ kernel beside the v2 dK/dV kernel) against
-    v2: all three gradients and the row constants it hands to the dK/dV kernel."""
+def test_flash_bwd_pingpong_matches_v2(kernels, flash_variant, T, ver):
+    """The ping-pong backwards against v2: v3 (eight-wave dQ kernel beside the v2 dK/dV
+    kernel) and v4 (both kernels eight-wave); all three gradients."""
     from nanosandbox_amd.ops import functional as fn
 
     torch.manual_seed(0)
@@ -447,15 +448,15 @@ def test_flash_bwd_v3_matches_v2(kernels, flash_variant, T):
     qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
     dy = torch.randn(B, T, H * D, device=DEV).to(BF)
     grads = {}
-    for ver in ("v2", "v3"):
-        flash_variant(bwd=ver)
+    for v in ("v2", ver):
+        flash_variant(bwd=v)
         x = qkv.clone().requires_grad_(True)
         fn.attention(x, H, 0.0, True).backward(dy)
         torch.cuda.synchronize()
-        grads[ver] = x.grad.float().view(B, T, 3, H * D)
+        grads[v] = x.grad.float().view(B, T, 3, H * D)
     for i, name in enumerate("qkv"):
-        e = rel_err(grads["v3"][:, :, i], grads["v2"][:, :, i])
-        assert e < 1e-3, f"d{name}: v3 vs v2 rel err {e}"
+        e = rel_err(grads[ver][:, :, i], grads["v2"][:, :, i])
+        assert e < 1e-3, f"d{name}: {ver} vs v2 rel err {e}"
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])
