@@ -167,15 +167,14 @@ __global__ __launch_bounds__(256) void xent_dw_fix_kernel(const bf16_t* __restri
   const float et = bf2f(E[(int64_t)row * lde + t]);
   const bf16_t* xr = x + (int64_t)row * ldx;
   float* gr = gW + (int64_t)t * ldg;
-  for (int c = lane * 8; c < C; c += 512) {
-    float a[8];
-    load8(xr + c, a);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float p = s * a[j];
-      const float pr = bf2f(f2bf(p));
-      atomicAdd(gr + c + j, et * (p - pr) - g * a[j]);
-    }
+  // one column per lane per step: every atomic wave-instruction covers 256 contiguous
+  // bytes of the target row (the full atomic rate; 8 columns per lane spread one
+  // instruction over 2 KB and ran ~9x slower: 2.56 ms per micro-step at 122880 rows)
+  for (int c = lane; c < C; c += 64) {
+    const float a = bf2f(xr[c]);
+    const float p = s * a;
+    const float pr = bf2f(f2bf(p));
+    atomicAdd(gr + c, et * (p - pr) - g * a);
   }
 }
 

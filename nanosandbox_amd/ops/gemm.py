@@ -149,16 +149,19 @@ WGRAD_SPLITS = int(os.environ.get("NSA_WGRAD_SPLITS", "0"))  # > 0: force a spli
 def wgrad_splits(n_out, n_in, tokens, cus=256):
     """Fixed K-split rule of the weight-gradient GEMMs (one 256 x 256 tile per workgroup).
 
-    Fewer output tiles than CUs: as many splits as fill one round of CUs (27 tiles -> 9,
-    36 -> 7, 9 -> 28).  Otherwise the fewest splits (<= 8) whose work items fill at least
-    ``WGRAD_FILL`` of their last round of CUs, else the best-filling count (the tied 124M
-    lm_head: 591 tiles x 3 = 1773 items = 99 % of 7 rounds).  These are the split counts
-    the round-3 start-up race picked on every GPT-2 shape (profiles/r3_bench_*.log)."""
+    Fewer output tiles than CUs, and one round of CUs at least 90 % busy: as many splits as
+    fit that round (27 tiles -> 9, 36 -> 7, 9 -> 28, 49 -> 5).  Otherwise the fewest
+    splits (<= 8) whose work items fill at least ``WGRAD_FILL`` of their last round of CUs,
+    else the best-filling count (the tied 124M lm_head: 591 tiles x 3 = 1773 items = 99 %
+    of 7 rounds; GPT-2 1.5B's 175-tile c_fc / mlp.c_proj dW: 7 splits = 96 % of 5 rounds,
+    where one round of 175 workgroups left 32 % of the CUs idle).  On the 124M / 350M
+    shapes these are the split counts the round-3 start-up race picked
+    (profiles/r3_bench_*.log)."""
     if WGRAD_SPLITS > 0:
         return max(1, min(WGRAD_SPLITS, max(1, tokens // BK)))
     tiles = -(-n_out // TILE) * -(-n_in // TILE)
     nkb = max(1, tokens // BK)
-    if tiles < cus:
+    if tiles < cus and tiles * min(cus // tiles, nkb) >= 0.9 * cus:
         return max(1, min(cus // tiles, nkb))
     best, best_fill = 1, -1.0
     for s in range(1, min(8, nkb) + 1):

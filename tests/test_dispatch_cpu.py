@@ -67,6 +67,11 @@ def test_wgrad_split_rule_matches_round3_race():
         assert gemm.wgrad_splits(n_out, n_in, 122880) == s, (n_out, n_in)
     # never more splits than 64-token K-tiles
     assert gemm.wgrad_splits(768, 768, 256) == 4
+    # GPT-2 1.5B (micro-batch 60 x 1024): 133 / 175 output tiles must not run as one
+    # partial round (52 % / 68 % of the CUs): 7 splits fill 91 % / 96 % of their rounds
+    for (n_out, n_in), s in {(4800, 1600): 7, (6400, 1600): 7, (1600, 6400): 7, (1600, 1600): 5,
+                             (50304, 1600): 2}.items():
+        assert gemm.wgrad_splits(n_out, n_in, 61440) == s, (n_out, n_in)
 
 
 def test_lm_head_rows_padding():
