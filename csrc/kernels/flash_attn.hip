@@ -810,6 +810,15 @@ __device__ __forceinline__ void fwd5_barrier() {
 #ifndef NSA_FWD5_NS
 #define NSA_FWD5_NS 8
 #endif
+// Diagnostic build only (-DNSA_FWD5_STAMPS=1, scripts/fwd5_stamps.py): per-wave s_memtime
+// totals of the ping-pong phases -- [total, M work, wait after M, V work, wait after V,
+// tiles] -- into a buffer of their own (no output is computed from them).
+#if NSA_FWD5_STAMPS
+__device__ unsigned long long g_fwd5_stamps[16384 * 8 * 6];
+#define FWD5_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define FWD5_T(var)
+#endif
 template <bool VPRE>
 __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
@@ -885,16 +894,23 @@ __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __rest
     issue(NS - 2);
     fwd5_barrier();
   }
+#if NSA_FWD5_STAMPS
+  unsigned long long acc[5] = {0, 0, 0, 0, 0};
+  FWD5_T(t_start);
+#endif
   for (int j = 0; j <= n_tiles; ++j) {
     // ---- M(j): PV of tile j - 1, S of tile j
+    FWD5_T(t0);
     if (!second) issue(j + NS - 2);
     const int kvp = (j - 1) * BN, kv0 = j * BN;
     const bool prev = j > 0 && kvp <= q0w + 31;
     const bool cur = j < n_tiles && kv0 <= q0w + 31;
     fwd5_matrix<VPRE>(smem + (j % NS) * TILE_BYTES, smem + (NS + (j + NS - 1) % NS) * TILE_BYTES, vfr, qf, pf, o,
                       st, prev, cur, h, r, lane);
+    FWD5_T(t1);
     if (second) wait_tile(j + 1);  // for waves 0-3's M(j + 1) after the next barrier
     fwd5_barrier();
+    FWD5_T(t2);
     // ---- V(j): softmax of tile j
     if (second) issue(j + NS - 1);
     if (cur) {
@@ -904,9 +920,28 @@ __global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __rest
         fwd5_softmax<true>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
       if constexpr (VPRE) fwd5_vload(smem + (NS + j % NS) * TILE_BYTES, vfr, h, lane);
     }
+    FWD5_T(t3);
     if (!second) wait_tile(j + 1);
     if (j < n_tiles || !second) fwd5_barrier();
+#if NSA_FWD5_STAMPS
+    FWD5_T(t4);
+    acc[0] += t1 - t0;
+    acc[1] += t2 - t1;
+    acc[2] += t3 - t2;
+    acc[3] += t4 - t3;
+    acc[4] += cur ? 1 : 0;
+#endif
   }
+#if NSA_FWD5_STAMPS
+  {
+    FWD5_T(t_end);
+    if (lane == 0) {
+      unsigned long long* g = g_fwd5_stamps + ((size_t)blockIdx.x * 8 + wv) * 6;
+      g[0] = t_end - t_start;
+      for (int k = 0; k < 5; ++k) g[1 + k] = acc[k];
+    }
+  }
+#endif
 
   if (qpos < T) {
     const float inv_l = 1.0f / l_i;
@@ -2375,6 +2410,13 @@ NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* do
 }
 
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_attn)
+
+#if NSA_FWD5_STAMPS
+NSA_API hipError_t nsa_fwd5_stamps(void* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd5_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {
