@@ -118,7 +118,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1 | v3: D = 64 backward (v1 = the generic kernels,
 //         v3 = the ping-pong dQ kernel beside the v2 dK/dV kernel, v4 = both ping-pong)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6, FWD_V7 = 7 };
 enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3, BWD_V4 = 4 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -131,6 +131,7 @@ FlashConfig& flash_config() {
               : (e[0] == 'v' && e[1] == '3') ? FWD_V3
               : (e[0] == 'v' && e[1] == '5') ? FWD_V5
               : (e[0] == 'v' && e[1] == '6') ? FWD_V6
+              : (e[0] == 'v' && e[1] == '7') ? FWD_V7
                                              : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
       d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : (e[0] == 'v' && e[1] == '3') ? BWD_V3
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
 // fragment and each transposed V fragment feeds two MFMAs).  Workgroup = 4 waves
 // = 256 queries; K/V tiles of 64 keys by LDS-DMA, double-buffered (32 KB).
 // =============================================================================
-template <bool MASK, bool DROP>
+template <bool MASK, bool DROP, bool BLK = false>
 __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
                                           f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
                                           int h, int r, int lane, float scale_log2, const DropArgs& dr) {
@@ -502,7 +503,7 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
   float mt[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
-    mt[blk] = -INFINITY;
+    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
@@ -510,10 +511,11 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
         if constexpr (MASK) {
           if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) st[blk][sb][i] = -INFINITY;
         }
-        mt[blk] = fmaxf(mt[blk], st[blk][sb][i]);
+        if constexpr (BLK) m4[i & 3] = fmaxf(m4[i & 3], st[blk][sb][i]);
+        else m4[0] = fmaxf(m4[0], st[blk][sb][i]);
       }
     }
-    mt[blk] = half_swap_max(mt[blk]);
+    mt[blk] = half_swap_max(BLK ? fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])) : m4[0]);
   }
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -528,26 +530,59 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
     }
   }
   bf16x8 pf[2][2][2];
+  if constexpr (BLK && !DROP) {
+    // independent blocks (all arguments, all exponents, 4 partial sums per block, packs)
+    // instead of per-element fma -> exp -> add chains (see fwd5_softmax)
 #pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const float mc = m_i[blk] * scale_log2;
-    float rs = 0.0f;
+    for (int blk = 0; blk < 2; ++blk) {
+      const float mc = m_i[blk] * scale_log2;
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
+      for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
-        rs += p;
-        if constexpr (DROP) {
-          const int kpos = kv0 + 32 * sb + acc_row(i, h);
-          const uint64_t id =
-              ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
-          p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
-        }
-        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
-      }
+        for (int i = 0; i < 16; ++i) st[blk][sb][i] = st[blk][sb][i] * scale_log2 - mc;
     }
-    l_i[blk] += half_swap_sum(rs);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[blk][sb][i] = fast_exp2(st[blk][sb][i]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          rs[i & 3] += st[blk][sb][i];
+          pf[blk][sb][i >> 3][i & 7] = (__bf16)st[blk][sb][i];
+        }
+      l_i[blk] += half_swap_sum((rs[0] + rs[1]) + (rs[2] + rs[3]));
+    }
+  } else {
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      const float mc = m_i[blk] * scale_log2;
+      float rs = 0.0f;
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
+          rs += p;
+          if constexpr (DROP) {
+            const int kpos = kv0 + 32 * sb + acc_row(i, h);
+            const uint64_t id =
+                ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
+            p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
+          }
+          pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
+        }
+      }
+      l_i[blk] += half_swap_sum(rs);
+    }
   }
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
@@ -567,7 +602,7 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
 // not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
-template <bool DROP, int NS>
+template <bool DROP, int NS, bool BLK = false>
 __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
                                                             float scale_log2, uint32_t drop_thresh, float drop_scale,
@@ -662,9 +697,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
     const char* kt = smem + cur * TILE_BYTES;
     const char* vt = smem + (NS + cur) * TILE_BYTES;
     if (kv0 + BN - 1 <= q0w)  // wave-uniform: every key of the tile visible to all 64 queries
-      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+      fwd_tile2<false, DROP, BLK>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
     else if (kv0 <= q0w + 63)  // the wave's diagonal tile
-      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+      fwd_tile2<true, DROP, BLK>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
     wait_next();
     __syncthreads();
   }
@@ -764,10 +799,15 @@ __device__ __forceinline__ void fwd5_vload(const char* vt, bf16x8 (&vfr)[2][2][2
     }
 }
 
+// The vector phase runs beside the partner wave's MFMA stream, so nothing else on the
+// SIMD fills its dependency stalls: the work is laid out as independent blocks (four
+// partial row maxima, all 32 exponents' arguments, the 32 exponents, four partial sums,
+// the bf16 packs) pinned by sched_barrier, instead of hipcc's per-element
+// fma -> exp -> add chains (stamps: 1600 cycles per tile, against ~700 of issue).
 template <bool MASK>
 __device__ __forceinline__ void fwd5_softmax(f32x16 (&st)[2], bf16x8 (&pf)[2][2], f32x16 (&o)[2], float& m_i,
                                              float& l_i, int kv0, int qpos, int h, float scale_log2) {
-  float mt = -INFINITY;
+  float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
@@ -775,9 +815,9 @@ __device__ __forceinline__ void fwd5_softmax(f32x16 (&st)[2], bf16x8 (&pf)[2][2]
       if constexpr (MASK) {
         if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
       }
-      mt = fmaxf(mt, st[sb][i]);
+      m4[i & 3] = fmaxf(m4[i & 3], st[sb][i]);
     }
-  mt = half_swap_max(mt);
+  const float mt = half_swap_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
   const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
   if (__builtin_amdgcn_ballot_w64(grow)) {
     const float m_new = grow ? mt : m_i;
@@ -788,16 +828,23 @@ __device__ __forceinline__ void fwd5_softmax(f32x16 (&st)[2], bf16x8 (&pf)[2][2]
     o[1] *= alpha;
   }
   const float mc = m_i * scale_log2;
-  float rs = 0.0f;
+  float x[32];
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = fast_exp2(st[sb][i] * scale_log2 - mc);
-      rs += p;
-      pf[sb][i >> 3][i & 7] = (__bf16)p;
-    }
-  l_i += half_swap_sum(rs);
+    for (int i = 0; i < 16; ++i) x[16 * sb + i] = st[sb][i] * scale_log2 - mc;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int e = 0; e < 32; ++e) x[e] = fast_exp2(x[e]);
+  __builtin_amdgcn_sched_barrier(0);
+  float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int e = 0; e < 32; ++e) rs[e & 3] += x[e];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pf[sb][i >> 3][i & 7] = (__bf16)x[16 * sb + i];
+  l_i += half_swap_sum((rs[0] + rs[1]) + (rs[2] + rs[3]));
 }
 
 // one phase boundary: nothing of either phase may be scheduled across it
@@ -1911,6 +1958,11 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
                                                                H, scale * kLog2e);
       return hipGetLastError();
     }
+    if (sel == FWD_V7 && !th) {  // v3 with the blocked softmax (A/B)
+      flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
+                                                                      B, T, H, scale * kLog2e, th, dscale, seed);
+      return hipGetLastError();
+    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -2434,7 +2486,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6 || fwd == FWD_V7) c.fwd = fwd;
   if (bwd >= BWD_V1 && bwd <= BWD_V4) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;

@@ -362,7 +362,7 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v5"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v5", "v7"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -478,7 +478,7 @@ def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
     assert e < 5e-3, f"v3 vs v1 rel err {e}"
 
 
-@pytest.mark.parametrize("ver", ["v5", "v6"])
+@pytest.mark.parametrize("ver", ["v5", "v6", "v7"])
 @pytest.mark.parametrize("T", [384, 1024, 200, 64, 40])
 def test_flash_fwd_variant_matches_v1(kernels, flash_variant, T, ver):
     """Forward v5 (eight-wave ping-pong; v6 = without the V-fragment prefetch) against v1:
