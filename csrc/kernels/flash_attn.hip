@@ -113,30 +113,20 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v5 | v6: D = 64 forward kernel; auto = v3
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3: D = 64 forward kernel; auto = v3
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
-//   bwd   NSA_FLASH_BWD = v2 (default) | v1 | v3: D = 64 backward (v1 = the generic kernels,
-//         v3 = the ping-pong dQ kernel beside the v2 dK/dV kernel, v4 = both ping-pong)
+//   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5, FWD_V6 = 6, FWD_V7 = 7 };
-enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3, BWD_V4 = 4 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3 };
+enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
 FlashConfig& flash_config() {
   static FlashConfig c = [] {
     FlashConfig d{FWD_AUTO, BWD_V2, ATTN_ORDER_DEFAULT};
-    if (const char* e = getenv("NSA_FLASH_FWD"))
-      d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1
-              : (e[0] == 'v' && e[1] == '3') ? FWD_V3
-              : (e[0] == 'v' && e[1] == '5') ? FWD_V5
-              : (e[0] == 'v' && e[1] == '6') ? FWD_V6
-              : (e[0] == 'v' && e[1] == '7') ? FWD_V7
-                                             : FWD_AUTO;
-    if (const char* e = getenv("NSA_FLASH_BWD"))
-      d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : (e[0] == 'v' && e[1] == '3') ? BWD_V3
-              : (e[0] == 'v' && e[1] == '4') ? BWD_V4
-                                             : BWD_V2;
+    if (const char* e = getenv("NSA_FLASH_FWD")) d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1 : (e[0] == 'v' && e[1] == '3') ? FWD_V3 : FWD_AUTO;
+    if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
     return d;
   }();
@@ -483,7 +473,7 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
 // fragment and each transposed V fragment feeds two MFMAs).  Workgroup = 4 waves
 // = 256 queries; K/V tiles of 64 keys by LDS-DMA, double-buffered (32 KB).
 // =============================================================================
-template <bool MASK, bool DROP, bool BLK = false>
+template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
                                           f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
                                           int h, int r, int lane, float scale_log2, const DropArgs& dr) {
@@ -503,7 +493,7 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
   float mt[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
-    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    mt[blk] = -INFINITY;
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
@@ -511,11 +501,10 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
         if constexpr (MASK) {
           if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) st[blk][sb][i] = -INFINITY;
         }
-        if constexpr (BLK) m4[i & 3] = fmaxf(m4[i & 3], st[blk][sb][i]);
-        else m4[0] = fmaxf(m4[0], st[blk][sb][i]);
+        mt[blk] = fmaxf(mt[blk], st[blk][sb][i]);
       }
     }
-    mt[blk] = half_swap_max(BLK ? fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])) : m4[0]);
+    mt[blk] = half_swap_max(mt[blk]);
   }
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -530,59 +519,26 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
     }
   }
   bf16x8 pf[2][2][2];
-  if constexpr (BLK && !DROP) {
-    // independent blocks (all arguments, all exponents, 4 partial sums per block, packs)
-    // instead of per-element fma -> exp -> add chains (see fwd5_softmax)
 #pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      const float mc = m_i[blk] * scale_log2;
+  for (int blk = 0; blk < 2; ++blk) {
+    const float mc = m_i[blk] * scale_log2;
+    float rs = 0.0f;
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
+    for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) st[blk][sb][i] = st[blk][sb][i] * scale_log2 - mc;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk)
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) st[blk][sb][i] = fast_exp2(st[blk][sb][i]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          rs[i & 3] += st[blk][sb][i];
-          pf[blk][sb][i >> 3][i & 7] = (__bf16)st[blk][sb][i];
+      for (int i = 0; i < 16; ++i) {
+        float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
+        rs += p;
+        if constexpr (DROP) {
+          const int kpos = kv0 + 32 * sb + acc_row(i, h);
+          const uint64_t id =
+              ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
+          p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
         }
-      l_i[blk] += half_swap_sum((rs[0] + rs[1]) + (rs[2] + rs[3]));
-    }
-  } else {
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      const float mc = m_i[blk] * scale_log2;
-      float rs = 0.0f;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
-          rs += p;
-          if constexpr (DROP) {
-            const int kpos = kv0 + 32 * sb + acc_row(i, h);
-            const uint64_t id =
-                ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
-            p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
-          }
-          pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
-        }
+        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
       }
-      l_i[blk] += half_swap_sum(rs);
     }
+    l_i[blk] += half_swap_sum(rs);
   }
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
@@ -602,7 +558,7 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
 // not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
-template <bool DROP, int NS, bool BLK = false>
+template <bool DROP, int NS>
 __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
                                                             float scale_log2, uint32_t drop_thresh, float drop_scale,
@@ -697,9 +653,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
     const char* kt = smem + cur * TILE_BYTES;
     const char* vt = smem + (NS + cur) * TILE_BYTES;
     if (kv0 + BN - 1 <= q0w)  // wave-uniform: every key of the tile visible to all 64 queries
-      fwd_tile2<false, DROP, BLK>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
     else if (kv0 <= q0w + 63)  // the wave's diagonal tile
-      fwd_tile2<true, DROP, BLK>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
     wait_next();
     __syncthreads();
   }
@@ -724,286 +680,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
       if (h == 0)
         lse_out[(int64_t)bh * T + qp] = (m_i[blk] * scale_log2 + __log2f(l_i[blk])) * 0.6931471805599453f;
     }
-  }
-}
-
-// =============================================================================
-// forward v5 (D = 64, no dropout): eight-wave ping-pong.  One workgroup = 8 waves x 32
-// queries = 256 queries of one (b, h); waves w and w + 4 share a SIMD.  Each wave's tile
-// step is cut into a matrix phase M(j) = {O^T += V_{j-1}^T P_{j-1}^T, S_j^T = K_j Q^T}
-// (16 MFMAs, their LDS reads) and a vector phase V(j) = the online softmax of S_j
-// (max, exp, sum, bf16 pack; 32 scores per lane).  Waves 0-3 run M(j) while waves 4-7
-// run V(j - 1), and the other way round, with one s_barrier per phase, so every SIMD
-// pairs one wave's MFMA stream with its partner's softmax VALU (cdna_hip_programming.md
-// §5.5 / MI355X_MICROARCH.md "Two waves per SIMD"; v3 leaves that pairing to chance and
-// runs at ~25 % MFMA busy with both waves often in the same phase).
-// K/V tiles of 64 keys arrive by LDS-DMA into an NS-slot ring (NS = 8: 128 KB), two
-// pieces per wave per tile: tile t is issued at global phase 2 (t - NS + 2) (into the
-// slot of tile t - NS, whose last reader, waves 4-7's M(t - NS + 1), ran one phase
-// earlier) and waited for (tiles t + 1 .. t + NS - 3 may stay in flight) at the end of
-// phase 2t - 1, before the barrier that opens waves 0-3's M(t).  A 4-slot ring (the
-// fetch two phases ahead) measured 506 us against v3's 361: the DMA latency under load
-// outlasts two short phases.  Numerics are v3's (exp2 of S·c - m·c in fp32, deferred
-// rescale, fp32 l).
-// =============================================================================
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
-__device__ __forceinline__ void vm_wait(int n) {
-#define NSA_VMW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-  switch (n) {
-    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
-    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-  }
-#undef NSA_VMW
-}
-
-template <bool VPRE>
-__device__ __forceinline__ void fwd5_matrix(const char* kt, const char* vt_prev, const bf16x8 (&vfr)[2][2][2],
-                                            const bf16x8 (&qf)[4], const bf16x8 (&pf)[2][2], f32x16 (&o)[2],
-                                            f32x16 (&st)[2], bool prev, bool cur, int h, int r, int lane) {
-  constexpr int D = 64;
-  if (prev) {
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = mfma(VPRE ? vfr[sb][s][dt] : tr_frag<D>(vt_prev, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
-      }
-  }
-  if (cur) {
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      st[sb] = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-    }
-  }
-}
-
-// V_j^T fragments of the P·V product, read at the end of the softmax phase V(j) (tile j
-// is visible since the barrier that opened M(j)) so that M(j + 1) starts on MFMAs
-__device__ __forceinline__ void fwd5_vload(const char* vt, bf16x8 (&vfr)[2][2][2], int h, int lane) {
-  constexpr int D = 64;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) vfr[sb][s][dt] = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
-    }
-}
-
-// The vector phase runs beside the partner wave's MFMA stream, so nothing else on the
-// SIMD fills its dependency stalls: the work is laid out as independent blocks (four
-// partial row maxima, all 32 exponents' arguments, the 32 exponents, four partial sums,
-// the bf16 packs) pinned by sched_barrier, instead of hipcc's per-element
-// fma -> exp -> add chains (stamps: 1600 cycles per tile, against ~700 of issue).
-template <bool MASK>
-__device__ __forceinline__ void fwd5_softmax(f32x16 (&st)[2], bf16x8 (&pf)[2][2], f32x16 (&o)[2], float& m_i,
-                                             float& l_i, int kv0, int qpos, int h, float scale_log2) {
-  float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if constexpr (MASK) {
-        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
-      }
-      m4[i & 3] = fmaxf(m4[i & 3], st[sb][i]);
-    }
-  const float mt = half_swap_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
-  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
-  if (__builtin_amdgcn_ballot_w64(grow)) {
-    const float m_new = grow ? mt : m_i;
-    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
-    l_i *= alpha;
-    m_i = m_new;
-    o[0] *= alpha;
-    o[1] *= alpha;
-  }
-  const float mc = m_i * scale_log2;
-  float x[32];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[16 * sb + i] = st[sb][i] * scale_log2 - mc;
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int e = 0; e < 32; ++e) x[e] = fast_exp2(x[e]);
-  __builtin_amdgcn_sched_barrier(0);
-  float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int e = 0; e < 32; ++e) rs[e & 3] += x[e];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) pf[sb][i >> 3][i & 7] = (__bf16)x[16 * sb + i];
-  l_i += half_swap_sum((rs[0] + rs[1]) + (rs[2] + rs[3]));
-}
-
-// one phase boundary: nothing of either phase may be scheduled across it
-__device__ __forceinline__ void fwd5_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-#ifndef NSA_FWD5_NS
-#define NSA_FWD5_NS 8
-#endif
-// Diagnostic build only (-DNSA_FWD5_STAMPS=1, scripts/fwd5_stamps.py): per-wave s_memtime
-// totals of the ping-pong phases -- [total, M work, wait after M, V work, wait after V,
-// tiles] -- into a buffer of their own (no output is computed from them).
-#if NSA_FWD5_STAMPS
-__device__ unsigned long long g_fwd5_stamps[16384 * 8 * 6];
-#define FWD5_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
-#else
-#define FWD5_T(var)
-#endif
-template <bool VPRE>
-__global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2) {
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int NS = NSA_FWD5_NS;  // ring slots: tile t is fetched 2 (NS - 2) phases ahead
-  constexpr int TILE_BYTES = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
-
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: every per-wave test is scalar
-  const bool second = wv >= 4;                               // waves 4-7: half a tile step behind
-  const int h = lane >> 5, r = lane & 31;
-  const int q0 = qt * 256;
-  const int q0w = q0 + 32 * wv;  // this wave's queries q0w .. q0w + 31
-  const int qpos = q0w + r;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-
-  bf16x8 qf[4];
-  {
-    const int qc = qpos < T ? qpos : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
-  }
-  f32x16 o[2] = {f32x16{}, f32x16{}}, st[2];
-  bf16x8 pf[2][2], vfr[2][2][2];
-  float m_i = -1e30f, l_i = 0.0f;
-
-  const int kv_end = min(T, q0 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-  // DMA geometry: a tile is 64 rows x 128 B of K and of V = 16 pieces of 1 KiB (8 rows);
-  // wave wv fills K rows 8 wv .. 8 wv + 7 and V rows 8 wv .. 8 wv + 7
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int prow = 8 * wv + (lane >> 3);
-  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const uint32_t koff = (uint32_t)((prow * (int)row_stride + pch * 8) * 2);
-  auto issue = [&](int jt) {  // wave-uniform; tiles past the end are not fetched
-    if (jt >= n_tiles) return;
-    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
-    uint32_t o0 = koff;
-    if (jt * BN + BN > T) {
-      const int r0 = min(jt * BN + prow, T - 1) - jt * BN;
-      o0 = (uint32_t)((r0 * (int)row_stride + pch * 8) * 2);
-    }
-    const uint32_t kb = lds0 + (uint32_t)((jt % NS) * TILE_BYTES + 8 * wv * 128);
-    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
-    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(kb + NS * TILE_BYTES));
-  };
-  // "tile t landed": at the end of phase 2t - 1 tiles t + 1 .. t + NS - 3 were issued
-  // after it (those inside the sequence), two pieces each, and may stay in flight
-  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_tiles - 1 - t))); };
-
-  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // Q landed before the DMA
-  if (second) __builtin_amdgcn_s_setprio(1);  // the younger half loses VALU arbitration otherwise
-#pragma unroll
-  for (int t = 0; t < NS - 2; ++t) issue(t);  // tile t is issued at global phase 2 (t - NS + 2)
-  wait_tile(0);
-  fwd5_barrier();
-  if (second) {  // global phase 0: waves 0-3 run M(0)
-    issue(NS - 2);
-    fwd5_barrier();
-  }
-#if NSA_FWD5_STAMPS
-  unsigned long long acc[5] = {0, 0, 0, 0, 0};
-  FWD5_T(t_start);
-#endif
-  for (int j = 0; j <= n_tiles; ++j) {
-    // ---- M(j): PV of tile j - 1, S of tile j
-    FWD5_T(t0);
-    if (!second) issue(j + NS - 2);
-    const int kvp = (j - 1) * BN, kv0 = j * BN;
-    const bool prev = j > 0 && kvp <= q0w + 31;
-    const bool cur = j < n_tiles && kv0 <= q0w + 31;
-    fwd5_matrix<VPRE>(smem + (j % NS) * TILE_BYTES, smem + (NS + (j + NS - 1) % NS) * TILE_BYTES, vfr, qf, pf, o,
-                      st, prev, cur, h, r, lane);
-    FWD5_T(t1);
-    if (second) wait_tile(j + 1);  // for waves 0-3's M(j + 1) after the next barrier
-    fwd5_barrier();
-    FWD5_T(t2);
-    // ---- V(j): softmax of tile j
-    if (second) issue(j + NS - 1);
-    if (cur) {
-      if (kv0 + BN - 1 <= q0w)
-        fwd5_softmax<false>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
-      else
-        fwd5_softmax<true>(st, pf, o, m_i, l_i, kv0, qpos, h, scale_log2);
-      if constexpr (VPRE) fwd5_vload(smem + (NS + j % NS) * TILE_BYTES, vfr, h, lane);
-    }
-    FWD5_T(t3);
-    if (!second) wait_tile(j + 1);
-    if (j < n_tiles || !second) fwd5_barrier();
-#if NSA_FWD5_STAMPS
-    FWD5_T(t4);
-    acc[0] += t1 - t0;
-    acc[1] += t2 - t1;
-    acc[2] += t3 - t2;
-    acc[3] += t4 - t3;
-    acc[4] += cur ? 1 : 0;
-#endif
-  }
-#if NSA_FWD5_STAMPS
-  {
-    FWD5_T(t_end);
-    if (lane == 0) {
-      unsigned long long* g = g_fwd5_stamps + ((size_t)blockIdx.x * 8 + wv) * 6;
-      g[0] = t_end - t_start;
-      for (int k = 0; k < 5; ++k) g[1 + k] = acc[k];
-    }
-  }
-#endif
-
-  if (qpos < T) {
-    const float inv_l = 1.0f / l_i;
-    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 u;
-        u.x = pack2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
-        u.y = pack2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
-        *reinterpret_cast<uint2*>(orow + d) = u;
-      }
-    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
   }
 }
 
@@ -1499,6 +1175,18 @@ __device__ __forceinline__ void slot_dispatch(int k, F& f) {
   }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
+__device__ __forceinline__ void vm_wait(int n) {
+#define NSA_VMW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
+    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+#undef NSA_VMW
+}
+
 // one 32-query slice for one wave: S, dP for its NKB key blocks, P / dS, then dV^T, dK^T.
 // ld = this wave's copy of the slice's row constants: [0, 32) -lse/scale, [32, 64) -delta.
 template <int NKB, bool MASK, bool DROP>
@@ -1949,20 +1637,6 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if ((sel == FWD_V5 || sel == FWD_V6) && !th) {  // v6: v5 without the V-fragment prefetch (A/B)
-      if (sel == FWD_V5)
-        flash_fwd5_kernel<true><<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
-                                                              H, scale * kLog2e);
-      else
-        flash_fwd5_kernel<false><<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
-                                                               H, scale * kLog2e);
-      return hipGetLastError();
-    }
-    if (sel == FWD_V7 && !th) {  // v3 with the blocked softmax (A/B)
-      flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
-                                                                      B, T, H, scale * kLog2e, th, dscale, seed);
-      return hipGetLastError();
-    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -2030,381 +1704,6 @@ hipError_t bwd_launch(const void* qkv, const void* o, const void* dout, const vo
 // constants -delta, -lse/scale) -> the dK/dV v2 kernel, 1 key block per wave, 4 waves
 // (two independent workgroups per CU).  ws = 2 x [B, H, T] fp32.  A/B at B120 T1024 H12
 // (whole backward): v1 1307, 2 key blocks per wave 1304, 8 waves 1203, this 1189 us.
-// =============================================================================
-// dK / dV kernel v3 (D = 64, no dropout): the v2 algebra (key on the lane, row constants
-// as initial accumulators, dK^T / dV^T resident) on the eight-wave ping-pong of forward
-// v5.  One workgroup = 8 waves x 32 keys = 256 keys of one (b, h); it sweeps 32-query
-// slices, each phase pair doing for one wave
-//   M(j) = {dV^T += dO_{j-1}^T P_{j-1}, dK^T += Q_{j-1}^T dS_{j-1} (8 MFMAs),
-//           S_j = Q_j K^T - lse/scale, dP_j = dO_j V^T - delta (8 MFMAs)}
-//   V(j) = {P = exp2(c S), dS = P dP, bf16 pack; Q_j^T / dO_j^T fragments for the next
-//           M read from LDS}
-// with waves 4-7 half a slice behind waves 0-3 (one s_barrier per phase).  Slices (Q,
-// dO [32][64] tiles + per-wave row-constant copies, 10 KB) arrive by LDS-DMA into an
-// 8-slot ring on the forward v5 schedule; every wave issues two pieces per slice (waves
-// 0-3 a Q piece, waves 4-7 a dO piece, each wave its row constants).
-// =============================================================================
-constexpr int DKV3_SLOT = 2 * V2_QT + 8 * 256;
-
-__device__ __forceinline__ void dkdv3_matrix(const char* qt, const float* ld, const bf16x8 (&kf)[4],
-                                             const bf16x8 (&vf)[4], const bf16x8 (&trf)[2][2][2],
-                                             const bf16x8 (&pfr)[2], const bf16x8 (&dsfr)[2], f32x16 (&dk)[2],
-                                             f32x16 (&dv)[2], f32x16& sacc, f32x16& pacc, bool prev, bool cur,
-                                             int h, int r) {
-  constexpr int D = 64;
-  if (prev) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        dv[dt] = mfma(trf[s][dt][0], pfr[s], dv[dt]);
-        dk[dt] = mfma(trf[s][dt][1], dsfr[s], dk[dt]);
-      }
-  }
-  if (cur) {
-    sacc = row_consts(ld, h);
-    pacc = row_consts(ld + 32, h);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      sacc = mfma(as_frag(lds_b128(qt, swz<D>(r, 2 * ks + h))), kf[ks], sacc);
-      pacc = mfma(as_frag(lds_b128(qt + V2_QT, swz<D>(r, 2 * ks + h))), vf[ks], pacc);
-    }
-  }
-}
-
-template <bool MASK>
-__device__ __forceinline__ void dkdv3_vector(const char* qt, const f32x16& sacc, const f32x16& pacc,
-                                             bf16x8 (&pfr)[2], bf16x8 (&dsfr)[2], bf16x8 (&trf)[2][2][2], int q0,
-                                             int key, int h, int lane, float scale_log2) {
-  constexpr int D = 64;
-  float pv[16], dsv[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    float p = fast_exp2(sacc[i] * scale_log2);
-    if constexpr (MASK) p = key > q0 + acc_row(i, h) ? 0.0f : p;
-    pv[i] = p;
-    dsv[i] = p * pacc[i];
-  }
-  pack16(pv, pfr);
-  pack16(dsv, dsfr);
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int r0 = 16 * s + 4 * h;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      trf[s][dt][0] = tr_frag<D>(qt + V2_QT, r0, r0 + 8, 32 * dt, lane);  // dO^T
-      trf[s][dt][1] = tr_frag<D>(qt, r0, r0 + 8, 32 * dt, lane);          // Q^T
-    }
-  }
-}
-
-#ifndef NSA_DKV3_NS
-#define NSA_DKV3_NS 8
-#endif
-__global__ __launch_bounds__(512, 1) void flash_bwd_dkdv3_kernel(const bf16_t* __restrict__ qkv,
-                                                                 const bf16_t* __restrict__ dout,
-                                                                 const float* __restrict__ nls,
-                                                                 const float* __restrict__ nd,
-                                                                 bf16_t* __restrict__ dqkv, int B, int T, int H,
-                                                                 float scale, float scale_log2) {
-  constexpr int D = 64;
-  constexpr int KWG = 256;
-  constexpr int NS = NSA_DKV3_NS;
-  constexpr int SLOT = DKV3_SLOT;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  int bh, kbw;  // key blocks near 0 see the most queries: launched first
-  attn_order((T + KWG - 1) / KWG, BH, 0, bh, kbw);
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool second = wv >= 4;
-  const int h = lane >> 5, r = lane & 31;
-  const int k0 = kbw * KWG;
-  const int kw = k0 + 32 * wv;
-  const int key = kw + r;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const float* nls_bh = nls + (int64_t)bh * T;
-  const float* nd_bh = nd + (int64_t)bh * T;
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int s_first = k0 / 32;
-  const int n_mine = max(0, T / 32 - s_first);
-
-  // slice t (queries 32 (s_first + t) ..) -> slot t % NS: waves 0-3 copy Q rows 8 (wv & 3)
-  // .. +7, waves 4-7 the same dO rows; each wave its own row-constant copy
-  const int prow = 8 * (wv & 3) + (lane >> 3);
-  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const bf16_t* tsrc = second ? dout + (int64_t)b * T * C + hh * D + (int64_t)prow * C + pch * 8
-                              : base + hh * D + (int64_t)prow * row_stride + pch * 8;
-  const int64_t tstride = second ? 32 * (int64_t)C : 32 * row_stride;  // per slice
-  const float* csrc = (h == 0 ? nls_bh : nd_bh) + r;
-  auto issue = [&](int t) {
-    if (t >= n_mine) return;
-    const uint32_t sb = lds0 + (uint32_t)((t % NS) * SLOT);
-    glds16(tsrc + (int64_t)(s_first + t) * tstride, sb + (uint32_t)((second ? V2_QT : 0) + 8 * (wv & 3) * 128));
-    glds4(csrc + (s_first + t) * 32, sb + (uint32_t)(2 * V2_QT + wv * 256));
-  };
-  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_mine - 1 - t))); };
-
-  bf16x8 kf[4], vf[4];
-  {
-    const int kc = key < T ? key : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + C + hh * D + (int64_t)kc * row_stride + 16 * ks + 8 * h));
-      vf[ks] =
-          as_frag(*reinterpret_cast<const uint4*>(base + 2 * C + hh * D + (int64_t)kc * row_stride + 16 * ks + 8 * h));
-    }
-  }
-  asm volatile("" ::"v"(kf[0]), "v"(kf[1]), "v"(kf[2]), "v"(kf[3]), "v"(vf[0]), "v"(vf[1]), "v"(vf[2]),
-               "v"(vf[3]));  // retire the fragment loads before the DMA ring (see dK/dV v2)
-  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}}, sacc, pacc;
-  bf16x8 pfr[2], dsfr[2], trf[2][2][2];
-
-  if (second) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int t = 0; t < NS - 2; ++t) issue(t);
-  wait_tile(0);
-  fwd5_barrier();
-  if (second) {
-    issue(NS - 2);
-    fwd5_barrier();
-  }
-  const int jd = wv;  // this wave's diagonal slice (keys kw .. kw + 31 = queries of slice jd)
-  for (int j = 0; j <= n_mine; ++j) {
-    if (!second) issue(j + NS - 2);
-    const bool prev = j > jd && j - 1 < n_mine;
-    const bool cur = j >= jd && j < n_mine;
-    const char* qt = smem + (j % NS) * SLOT;
-    dkdv3_matrix(qt, reinterpret_cast<const float*>(qt + 2 * V2_QT) + wv * 64, kf, vf, trf, pfr, dsfr, dk, dv,
-                 sacc, pacc, prev, cur, h, r);
-    if (second) wait_tile(j + 1);
-    fwd5_barrier();
-    if (second) issue(j + NS - 1);
-    if (cur) {
-      const int q0 = (s_first + j) * 32;
-      if (j > jd)
-        dkdv3_vector<false>(qt, sacc, pacc, pfr, dsfr, trf, q0, key, h, lane, scale_log2);
-      else
-        dkdv3_vector<true>(qt, sacc, pacc, pfr, dsfr, trf, q0, key, h, lane, scale_log2);
-    }
-    if (!second) wait_tile(j + 1);
-    if (j < n_mine || !second) fwd5_barrier();
-  }
-
-  if (key < T) {
-    bf16_t* krow = dqkv + ((int64_t)b * T + key) * row_stride + C + hh * D;
-    bf16_t* vrow = krow + C;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 uk, uv;
-        uk.x = cvt2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
-        uk.y = cvt2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
-        uv.x = cvt2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
-        uv.y = cvt2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
-        *reinterpret_cast<uint2*>(krow + d) = uk;
-        *reinterpret_cast<uint2*>(vrow + d) = uv;
-      }
-  }
-}
-
-// =============================================================================
-// dQ kernel v3 (D = 64, no dropout): the v2 dQ algebra on the forward v5's eight-wave
-// ping-pong.  One workgroup = 8 waves x 32 queries = 256 queries of one (b, h); waves w
-// and w + 4 share a SIMD and alternate
-//   M(j) = {dQ^T += K_{j-1}^T dS_{j-1}^T (8 MFMAs), S_j^T = K_j Q^T, dP_j^T = V_j dO^T (16)}
-//   V(j) = {P = exp2(c S - lse log2e), dS = P (dP - delta), bf16 pack; K_j^T fragments
-//           for the next dQ product read from LDS}
-// with one s_barrier per phase (waves 4-7 half a tile behind), so each SIMD pairs one
-// wave's matrix stream with its partner's vector work.  K / V tiles (64 keys) arrive by
-// LDS-DMA into an 8-slot ring on the forward v5 schedule (tile t issued at global phase
-// 2 (t - NS + 2), waited for at the end of phase 2t - 1).  Like v2 it forms delta and
-// the row constants for the dK/dV kernel, and writes dQ once in bf16.
-// =============================================================================
-__device__ __forceinline__ void dq3_matrix(const char* kt, const bf16x8 (&qf)[4], const bf16x8 (&gf)[4],
-                                           const f32x16& ndt, const bf16x8 (&ktr)[2][2][2],
-                                           const bf16x8 (&dsf)[2][2], f32x16 (&dq)[2], f32x16 (&st)[2],
-                                           f32x16 (&pt)[2], bool prev, bool cur, int h, int r) {
-  constexpr int D = 64;
-  if (prev) {
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(ktr[sb][s][dt], dsf[sb][s], dq[dt]);
-  }
-  if (cur) {
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      st[sb] = f32x16{};
-      pt[sb] = ndt;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-        pt[sb] = mfma(as_frag(lds_b128(kt + DQ2_T, swz<D>(32 * sb + r, 2 * ks + h))), gf[ks], pt[sb]);
-      }
-    }
-  }
-}
-
-template <bool MASK>
-__device__ __forceinline__ void dq3_vector(const char* kt, f32x16 (&st)[2], f32x16 (&pt)[2],
-                                           bf16x8 (&dsf)[2][2], bf16x8 (&ktr)[2][2][2], float lse2, int kv0,
-                                           int qpos, int h, int lane, float scale_log2) {
-  constexpr int D = 64;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    float dsv[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
-      if constexpr (MASK) p = kv0 + 32 * sb + acc_row(i, h) > qpos ? 0.0f : p;
-      dsv[i] = p * pt[sb][i];
-    }
-    pack16(dsv, dsf[sb]);
-  }
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) ktr[sb][s][dt] = tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane);
-    }
-}
-
-#ifndef NSA_DQ3_NS
-#define NSA_DQ3_NS 8
-#endif
-__global__ __launch_bounds__(512, 1) void flash_bwd_dq3_kernel(const bf16_t* __restrict__ qkv,
-                                                               const bf16_t* __restrict__ dout,
-                                                               const bf16_t* __restrict__ o,
-                                                               const float* __restrict__ lse, float* __restrict__ nls,
-                                                               float* __restrict__ nd, bf16_t* __restrict__ dqkv,
-                                                               int B, int T, int H, float scale, float scale_log2) {
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int NS = NSA_DQ3_NS;
-  constexpr int SLOT = 2 * DQ2_T;  // K, V
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool second = wv >= 4;
-  const int h = lane >> 5, r = lane & 31;
-  const int q0w = qt * 256 + 32 * wv;
-  const int qpos = q0w + r;
-  const int qc = qpos < T ? qpos : T - 1;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int kv_end = min(T, qt * 256 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-
-  // K / V tile t -> slot t % NS: 8 + 8 pieces of 8 rows x 128 B; wave wv copies K rows and
-  // V rows 8 wv .. 8 wv + 7, XOR swizzle on the per-lane source chunk
-  const int prow = 8 * wv + (lane >> 3);
-  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const bf16_t* kb0 = base + C + hh * D;
-  auto issue = [&](int t) {
-    if (t >= n_tiles) return;
-    int row = t * BN + prow;
-    row = row < T ? row : T - 1;  // rows past T re-read row T - 1 (their keys are masked)
-    const bf16_t* src = kb0 + (int64_t)row * row_stride + pch * 8;
-    const uint32_t sb = lds0 + (uint32_t)((t % NS) * SLOT + 8 * wv * 128);
-    glds16(src, sb);
-    glds16(src + C, sb + DQ2_T);
-  };
-  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(NS - 3, n_tiles - 1 - t))); };
-
-  bf16x8 qf[4], gf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qf[ks] = as_frag(*reinterpret_cast<const uint4*>(base + (int64_t)qc * row_stride + hh * D + 16 * ks + 8 * h));
-    gf[ks] = as_frag(*reinterpret_cast<const uint4*>(dout + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h));
-  }
-  float dpart = 0.0f;
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    float fo[8], fg[8];
-    load8(o + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h, fo);
-    unpack8(__builtin_bit_cast(uint4, gf[ks]), fg);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dpart += fo[e] * fg[e];
-  }
-  const float ndl = -half_swap_sum(dpart);
-  const float lse_q = lse[(int64_t)bh * T + qc];
-  const float lse2 = lse_q * kLog2e;
-  if (h == 0 && qpos < T) {
-    nd[(int64_t)bh * T + qpos] = ndl;
-    nls[(int64_t)bh * T + qpos] = -lse_q / scale;
-  }
-  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]), "v"(gf[0]), "v"(gf[1]), "v"(gf[2]),
-               "v"(gf[3]), "v"(lse2), "v"(ndl));  // retire these loads before the DMA ring
-  f32x16 ndt;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) ndt[i] = ndl;
-  f32x16 dq[2] = {f32x16{}, f32x16{}}, st[2], pt[2];
-  bf16x8 dsf[2][2], ktr[2][2][2];
-
-  if (second) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int t = 0; t < NS - 2; ++t) issue(t);
-  wait_tile(0);
-  fwd5_barrier();
-  if (second) {
-    issue(NS - 2);
-    fwd5_barrier();
-  }
-  for (int j = 0; j <= n_tiles; ++j) {
-    if (!second) issue(j + NS - 2);
-    const int kv0 = j * BN;
-    const bool prev = j > 0 && (j - 1) * BN <= q0w + 31;
-    const bool cur = j < n_tiles && kv0 <= q0w + 31;
-    dq3_matrix(smem + (j % NS) * SLOT, qf, gf, ndt, ktr, dsf, dq, st, pt, prev, cur, h, r);
-    if (second) wait_tile(j + 1);
-    fwd5_barrier();
-    if (second) issue(j + NS - 1);
-    if (cur) {
-      const char* kt = smem + (j % NS) * SLOT;
-      if (kv0 + BN - 1 <= q0w)
-        dq3_vector<false>(kt, st, pt, dsf, ktr, lse2, kv0, qpos, h, lane, scale_log2);
-      else
-        dq3_vector<true>(kt, st, pt, dsf, ktr, lse2, kv0, qpos, h, lane, scale_log2);
-    }
-    if (!second) wait_tile(j + 1);
-    if (j < n_tiles || !second) fwd5_barrier();
-  }
-
-  if (qpos < T) {
-    bf16_t* qrow = dqkv + ((int64_t)b * T + qpos) * row_stride + hh * D;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 u;
-        u.x = cvt2(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
-        u.y = cvt2(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(qrow + d) = u;
-      }
-  }
-}
-
 hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws, void* dqkv,
                          int B, int T, int H, float scale, float p, uint64_t seed, hipStream_t s) {
   float* nd = (float*)ws;
@@ -2413,11 +1712,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int n_qt = (T + 127) / 128;
   const int order = attn_order_env();
-  if (flash_config().bwd >= BWD_V3 && !th)
-    flash_bwd_dq3_kernel<<<(T + 255) / 256 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                                 (const bf16_t*)o, (const float*)lse, nls, nd,
-                                                                 (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e);
-  else if (th)
+  if (th)
     flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                             (const bf16_t*)o, (const float*)lse, nls, nd, (bf16_t*)dqkv,
                                                             B, T, H, scale, scale * kLog2e, th, dscale, seed, order);
@@ -2429,10 +1724,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int n_kb = (T + 127) / 128;
-  if (flash_config().bwd == BWD_V4 && !th)
-    flash_bwd_dkdv3_kernel<<<(T + 255) / 256 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
-                                                                   (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e);
-  else if (th)
+  if (th)
     flash_bwd_dkdv2_kernel<1, 4, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
                                                                    (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
                                                                    dscale, seed, order);
@@ -2451,7 +1743,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
 NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (D == 64 && T % 32 == 0 && flash_config().bwd >= BWD_V2)
+  if (D == 64 && T % 32 == 0 && flash_config().bwd == BWD_V2)
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
     case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
@@ -2462,13 +1754,6 @@ NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* do
 }
 
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_attn)
-
-#if NSA_FWD5_STAMPS
-NSA_API hipError_t nsa_fwd5_stamps(void* host, int64_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd5_stamps), (size_t)n * sizeof(unsigned long long), 0,
-                             hipMemcpyDeviceToHost);
-}
-#endif
 
 NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {
@@ -2486,8 +1771,8 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5 || fwd == FWD_V6 || fwd == FWD_V7) c.fwd = fwd;
-  if (bwd >= BWD_V1 && bwd <= BWD_V4) c.bwd = bwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3) c.fwd = fwd;
+  if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
 }

@@ -337,7 +337,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v5", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
@@ -362,7 +362,7 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v5", "v7"])
+@pytest.mark.parametrize("fwd", ["v1", "v3"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -436,29 +436,6 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
 
 
-@pytest.mark.parametrize("ver", ["v3", "v4"])
-@pytest.mark.parametrize("T", [1024, 320, 96, 64])
-def test_flash_bwd_pingpong_matches_v2(kernels, flash_variant, T, ver):
-    """The ping-pong backwards against v2: v3 (eight-wave dQ kernel beside the v2 dK/dV
-    kernel) and v4 (both kernels eight-wave); all three gradients."""
-    from nanosandbox_amd.ops import functional as fn
-
-    torch.manual_seed(0)
-    B, H, D = 2, 3, 64
-    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
-    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
-    grads = {}
-    for v in ("v2", ver):
-        flash_variant(bwd=v)
-        x = qkv.clone().requires_grad_(True)
-        fn.attention(x, H, 0.0, True).backward(dy)
-        torch.cuda.synchronize()
-        grads[v] = x.grad.float().view(B, T, 3, H * D)
-    for i, name in enumerate("qkv"):
-        e = rel_err(grads[ver][:, :, i], grads["v2"][:, :, i])
-        assert e < 1e-3, f"d{name}: {ver} vs v2 rel err {e}"
-
-
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
     """Forward v3 (64 queries per wave, LDS-DMA ring) against v1, with and without dropout
@@ -476,30 +453,6 @@ def test_flash_fwd_v3_matches_v1(kernels, flash_variant, p):
         torch.cuda.synchronize()
     e = rel_err(outs["v3"], outs["v1"])
     assert e < 5e-3, f"v3 vs v1 rel err {e}"
-
-
-@pytest.mark.parametrize("ver", ["v5", "v6", "v7"])
-@pytest.mark.parametrize("T", [384, 1024, 200, 64, 40])
-def test_flash_fwd_variant_matches_v1(kernels, flash_variant, T, ver):
-    """Forward v5 (eight-wave ping-pong; v6 = without the V-fragment prefetch) against v1:
-    output and the saved LSE (what the backward recomputes P from).
-    T = 64 / 40: one key tile (the ping-pong's no-prefetch tail from the start)."""
-    from nanosandbox_amd.ops import _lib
-
-    torch.manual_seed(0)
-    B, H, D = 2, 3, 64
-    C = H * D
-    qkv = torch.randn(B, T, 3 * C, device=DEV).to(BF)
-    outs = {}
-    for v in ("v1", ver):
-        flash_variant(fwd=v)
-        y = torch.empty(B, T, C, device=DEV, dtype=BF)
-        lse = torch.empty(B, H, T, device=DEV)
-        _lib.call("nsa_flash_fwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, D, 1.0 / math.sqrt(D), 0.0, 0,
-                  _lib.stream())
-        outs[v] = (y.float(), lse)
-    assert rel_err(outs[ver][0], outs["v1"][0]) < 5e-3
-    assert (outs[ver][1] - outs["v1"][1]).abs().max().item() < 2e-2
 
 
 def test_flash_variant_is_resolved_once(kernels, monkeypatch):
