@@ -39,6 +39,13 @@ def parse(spec):
 def with_env(env, fn):
     from nanosandbox_amd.ops.functional import flash_variant
 
+    if any(v.isdigit() for v in env.values()):  # raw selector codes (variant libraries, NSA_KERNEL_LIB)
+        code = lambda k: int(env[k]) if k in env else -1  # noqa: E731
+        prev = _lib.call_ret("nsa_flash_set_variant", code("fwd"), code("bwd"), code("order"))
+        try:
+            return fn()
+        finally:
+            _lib.call_ret("nsa_flash_set_variant", prev & 0xF, (prev >> 4) & 0xF, (prev >> 8) & 0xF)
     with flash_variant(fwd=env.get("fwd"), bwd=env.get("bwd"),
                        order=int(env["order"]) if "order" in env else None):
         return fn()
