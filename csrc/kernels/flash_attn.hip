@@ -476,7 +476,8 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
                                           f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
-                                          int h, int r, int lane, float scale_log2, const DropArgs& dr) {
+                                          int h, int r, int lane, float scale_log2, const DropArgs& dr,
+                                          unsigned long long* stamp = nullptr) {
   constexpr int D = 64;
   f32x16 st[2][2];  // [block][key sub-block]
 #pragma unroll
@@ -490,6 +491,9 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
       st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
     }
   }
+#if NSA_FWD3_STAMPS
+  stamp[0] = __builtin_amdgcn_s_memtime();
+#endif
   float mt[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -540,6 +544,9 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
     }
     l_i[blk] += half_swap_sum(rs);
   }
+#if NSA_FWD3_STAMPS
+  stamp[1] = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
@@ -554,6 +561,16 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
     }
   }
 }
+
+// Diagnostic build only (-DNSA_FWD3_STAMPS=1, scripts/fwd3_stamps.py): per-wave s_memtime
+// totals of the v3 tile loop -- [loop, S issue, S wait + softmax, P·V issue, DMA wait +
+// barrier, tiles] -- into a buffer of their own (no output is computed from them).
+#ifndef NSA_FWD3_STAMPS
+#define NSA_FWD3_STAMPS 0
+#endif
+#if NSA_FWD3_STAMPS
+__device__ unsigned long long g_fwd3_stamps[16384 * 4 * 6];
+#endif
 
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
@@ -644,6 +661,10 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
   for (int t = 0; t < NS - 1; ++t) issue(min(t, n_tiles - 1), t);
   wait_next();  // tile 0 landed
   __syncthreads();
+#if NSA_FWD3_STAMPS
+  unsigned long long acc3[5] = {0, 0, 0, 0, 0};
+  const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
+#endif
   for (int j = 0; j < n_tiles; ++j) {
     const int cur = j % NS;
     const int kv0 = j * BN;
@@ -652,13 +673,47 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
     issue(min(j + NS - 1, n_tiles - 1), (j + NS - 1) % NS);
     const char* kt = smem + cur * TILE_BYTES;
     const char* vt = smem + (NS + cur) * TILE_BYTES;
-    if (kv0 + BN - 1 <= q0w)  // wave-uniform: every key of the tile visible to all 64 queries
-      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
-    else if (kv0 <= q0w + 63)  // the wave's diagonal tile
-      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+#if NSA_FWD3_STAMPS
+    unsigned long long st2[2] = {0, 0};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    bool did = false;
+#else
+    unsigned long long* st2 = nullptr;
+#endif
+    if (kv0 + BN - 1 <= q0w) {  // wave-uniform: every key of the tile visible to all 64 queries
+      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr, st2);
+#if NSA_FWD3_STAMPS
+      did = true;
+#endif
+    } else if (kv0 <= q0w + 63) {  // the wave's diagonal tile
+      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr, st2);
+#if NSA_FWD3_STAMPS
+      did = true;
+#endif
+    }
+#if NSA_FWD3_STAMPS
+    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+#endif
     wait_next();
     __syncthreads();
+#if NSA_FWD3_STAMPS
+    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    if (did) {
+      acc3[0] += st2[0] - t0;  // S MFMA issue (+ K fragment reads)
+      acc3[1] += st2[1] - st2[0];  // wait for S + softmax VALU
+      acc3[2] += t3 - st2[1];  // P·V issue (+ V fragment reads)
+      acc3[4] += 1;
+    }
+    acc3[3] += t4 - t3;  // DMA wait + barrier
+#endif
   }
+#if NSA_FWD3_STAMPS
+  if (lane == 0) {
+    unsigned long long* g = g_fwd3_stamps + ((size_t)blockIdx.x * 4 + w) * 6;
+    g[0] = __builtin_amdgcn_s_memtime() - t_loop;
+    for (int k = 0; k < 5; ++k) g[1 + k] = acc3[k];
+  }
+#endif
 
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -1754,6 +1809,13 @@ NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* do
 }
 
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_attn)
+
+#if NSA_FWD3_STAMPS
+NSA_API hipError_t nsa_fwd3_stamps(void* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd3_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {
