@@ -92,6 +92,8 @@ _SIGNATURES = {
                  c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemm_wgrad4": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_void_p],
+    "nsa_gemm_wgrad4b": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "nsa_gemm_nt4": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                      c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemm_small": [c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

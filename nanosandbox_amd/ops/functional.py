@@ -97,6 +97,21 @@ def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     return _accumulate(p, g)
 
 
+def weight_bias_grad(w: torch.Tensor, b, dy2: torch.Tensor, x2: torch.Tensor):
+    """(dW, db) of one Linear: with both gradients accumulated into flat ``main_grad``
+    buffers on the GPU, one weight-grad kernel launch also forms the bias gradient from
+    the dY fragments it reads (``gemm_wg4.hip`` BG), instead of a second pass over dY."""
+    if b is None:
+        return weight_grad(w, dy2, x2), None
+    mw, mb = getattr(w, "main_grad", None), getattr(b, "main_grad", None)
+    if dy2.is_cuda and dy2.dtype == BF16 and mw is not None and mb is not None:
+        _gd.wgrad_acc(dy2.contiguous(), x2.contiguous(), mw, gb32=mb)
+        notify_grad_ready(w)
+        notify_grad_ready(b)
+        return None, None
+    return weight_grad(w, dy2, x2), bias_grad(b, dy2)
+
+
 def bias_grad(p, dy2: torch.Tensor):
     """db = dy2.sum(0) accumulated in fp32 (into ``p.main_grad`` when present): our
     column-sum kernel on MI355X."""
@@ -493,8 +508,7 @@ class LinearFn(torch.autograd.Function):
             wc = compute_weight(w, d2.dtype)
             dx = _gd.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
             dx = dx.view(*dout.shape[:-1], x2.shape[-1])
-        gw = weight_grad(w, d2, x2)
-        gb = bias_grad(b, d2)
+        gw, gb = weight_bias_grad(w, b, d2, x2)
         dres = dout if ctx.has_residual else None
         return dx, gw, gb, dres
 
@@ -512,8 +526,8 @@ class MLPFn(torch.autograd.Function):
 
     Forward: the c_fc GEMM's epilogue adds b_fc and writes both u and g = gelu(u); the
     c_proj GEMM adds b_proj.  Backward: du = (dy W_proj) * gelu'(u) from one GEMM epilogue,
-    dx = du W_fc, both weight gradients accumulated in fp32 by the split-K GEMM, bias
-    gradients by the column-sum kernel."""
+    dx = du W_fc, both weight gradients accumulated in fp32 by the split-K GEMM, the bias
+    gradients from the same kernel's dY fragments (``weight_bias_grad``)."""
 
     @staticmethod
     def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
@@ -532,11 +546,9 @@ class MLPFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, u, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        gw_proj = weight_grad(w_proj, dy2, g)
-        gb_proj = bias_grad(b_proj, dy2)
+        gw_proj, gb_proj = weight_bias_grad(w_proj, b_proj, dy2, g)
         du = _gd.dgrad_dgelu(dy2, compute_weight(w_proj, dy.dtype), u)
-        gw_fc = weight_grad(w_fc, du, x2)
-        gb_fc = bias_grad(b_fc, du)
+        gw_fc, gb_fc = weight_bias_grad(w_fc, b_fc, du, x2)
         dx = _gd.dgrad(du, compute_weight(w_fc, dy.dtype))
         return dx.view(ctx.xshape), gw_fc, gb_fc, gw_proj, gb_proj
 

@@ -174,14 +174,18 @@ def wgrad_splits(n_out, n_in, tokens, cus=256):
     return best
 
 
-def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False):
+def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False, gb32=None):
     """g32 (fp32 [N_out, K_in]) += dy2^T @ x2, reduced over the token dim in-kernel.
 
     Default: every K split adds its partial tile into g32 with fp32 atomics (arrival
     order, so the last bits vary run to run).  ``deterministic``: each split stores
     its partial to a workspace and one pass adds the splits to g32 in split order
     (bitwise reproducible; with one split the single atomic add per element is
-    already order-free)."""
+    already order-free).
+
+    ``gb32`` (fp32 [N_out], optional): the bias gradient gb32 += dy2.sum(0) as well -- fused
+    into the four-wave kernel's atomic path (column sums of the dY fragments it reads
+    anyway), else the separate column-sum pass."""
     T, N_out = dy2.shape
     K_in = x2.shape[1]
     _check(dy2, "dy")
@@ -190,6 +194,17 @@ def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False):
     if splits is None:
         splits = wgrad_splits(N_out, K_in, T)
     four = wgrad4_supported(N_out, K_in, T)
+
+    if gb32 is not None:
+        if not gb32.is_contiguous() or gb32.dtype != torch.float32 or gb32.numel() != N_out:
+            raise ValueError("bias grad must be a contiguous fp32 [N_out] tensor")
+        if four and not (deterministic and splits > 1):
+            _lib.call("nsa_gemm_wgrad4b", EPI_ATOMIC, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
+                      _lib.ptr(g32), K_in, _lib.ptr(gb32), N_out, K_in, T, splits, _lib.stream())
+            return g32
+        wgrad_acc(dy2, x2, g32, splits, deterministic)
+        bias_grad_acc(dy2, gb32, deterministic)
+        return g32
 
     def launch(epi, C):
         if four:

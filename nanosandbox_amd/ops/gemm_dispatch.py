@@ -115,16 +115,24 @@ def dgrad_dgelu(dy2, w, u):
     return _nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, op="dgrad_dgelu")
 
 
-def wgrad_acc(dy2, x2, g32):
-    """g32 += dy2^T @ x2 in fp32 (g32: a view of the flat gradient, or a fresh buffer)."""
+def wgrad_acc(dy2, x2, g32, gb32=None):
+    """g32 += dy2^T @ x2 in fp32 (g32: a view of the flat gradient, or a fresh buffer);
+    with ``gb32`` also the bias gradient gb32 += dy2.sum(0) (fused into the weight-grad
+    kernel where it can be, ``gemm.wgrad_acc``)."""
     T, N = dy2.shape
     K = x2.shape[1]
     k = kernel_for("wgrad", N, K, T) if _ok(dy2, x2) and g32.is_contiguous() else "torch"
     _used.setdefault(("wgrad", N, K, T), k if k == "torch" else f"{k}/s{_gemm.wgrad_splits(N, K, T)}")
     if k != "torch":
-        _gemm.wgrad_acc(dy2, x2, g32, deterministic=DETERMINISTIC)
+        if gb32 is not None and not (gb32.is_contiguous() and dy2.shape[1] % 8 == 0):
+            _gemm.wgrad_acc(dy2, x2, g32, deterministic=DETERMINISTIC)
+            bias_grad_acc(dy2, gb32)
+            return
+        _gemm.wgrad_acc(dy2, x2, g32, deterministic=DETERMINISTIC, gb32=gb32)
         return
     g32.add_(dy2.t().float() @ x2.float())
+    if gb32 is not None:
+        gb32.add_(dy2.float().sum(0))
 
 
 def bias_grad_acc(dy2, gb32):

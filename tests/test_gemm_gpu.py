@@ -170,6 +170,30 @@ def test_bias_grad(kernels):
         assert torch.equal(g1, g2)
 
 
+@pytest.mark.parametrize("T,N_out,K_in,splits", [(4096, 768, 768, 4), (2048, 1032, 520, 3), (1024, 3072, 768, 1),
+                                                 (2048, 264, 256, 5)])
+def test_wgrad_fused_bias_grad(kernels, T, N_out, K_in, splits):
+    """The weight-grad kernel's fused bias gradient (column sums of dY from its own A
+    fragments, the first column-block tiles only, one atomic per column and split) against
+    fp32 sums: ragged N_out (1032: the last row tile shifted back), several splits, and a
+    bias view at an odd offset of a flat buffer (no alignment assumed)."""
+    from nanosandbox_amd.ops import gemm
+    torch.manual_seed(0)
+    dy = torch.randn(T, N_out, device=DEV).to(BF)
+    x = torch.randn(T, K_in, device=DEV).to(BF)
+    g = torch.zeros(N_out, K_in, device=DEV)
+    flat = torch.full((N_out + 3,), float("nan"), device=DEV)
+    gb = flat[1:1 + N_out]
+    gb.zero_()
+    gb += 0.5
+    gemm.wgrad_acc(dy, x, g, splits=splits, gb32=gb)
+    ref_b = dy.float().sum(0) + 0.5
+    assert torch.isnan(flat[0]) and torch.isnan(flat[-2:]).all()  # nothing written outside the view
+    assert (gb - ref_b).abs().max().item() <= 1e-3 * T ** 0.5, (gb - ref_b).abs().max().item()
+    ref_w = dy.float().t() @ x.float()
+    assert ((g - ref_w).norm() / ref_w.norm()).item() < 1e-5
+
+
 def test_dispatch_records_native_kernels(kernels):
     """The fixed rule's picks as the bench JSON reports them (no library kernel)."""
     from nanosandbox_amd.ops import gemm_dispatch
