@@ -139,10 +139,13 @@ __device__ __forceinline__ float w_sum8(const bf16x8& a, float acc) {
 }
 
 // BG: the bias gradient (column sums of dY over the tokens) from the dY fragments the MFMAs
-// read anyway: in the tiles of the first column block, the wn = 0 waves add each A fragment
-// into a per-lane f32 (4 v_dot2c per fragment, in MFMA gaps) and finish with one atomic add
-// per column and split -- no second pass over dY (the separate column-sum kernel read the
-// whole dY again: 14.8 ms/step at GPT-2 124M with biases)
+// read anyway -- no second pass over dY (the separate column-sum kernel read the whole dY
+// again: 14.8 ms/step at GPT-2 124M with biases).  The work is spread so that no workgroup
+// carries much of it: K-tile kt of a split is summed by the tiles of column block
+// kt % tiles_n only, and of the two waves that read the same A fragments, wave wn takes the
+// fragments i with i % 2 == wn (4 v_dot2c per fragment, in MFMA gaps).  Each wave ends
+// with one atomic add per column it summed.  (All sums in the first column block's wn = 0
+// waves measured +16-18 % on that kernel: the slowest workgroup sets a one-round grid.)
 template <int EPI, bool BG = false>
 __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
   __shared__ __attribute__((aligned(16))) char smem[W_SMEM];
@@ -269,11 +272,12 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
     b0[f] = w_cat(w_tr(rdB[f]), w_tr(rdB[f] + 2048));
   }
 
-  const bool do_bg = BG && tn == 0 && wn == 0;  // wave-uniform
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int kc = kt0;  // BG: global index of the K-tile being multiplied
   uint32_t buf = 0;
   auto ktile = [&](auto FIRST_) {
     constexpr bool FIRST = decltype(FIRST_)::value;
+    const bool do_bg = BG && kc % g.tiles_n == tn;  // wave-uniform
     w_for<128>([&](auto I) {
       constexpr int n = decltype(I)::value;
       constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
@@ -284,7 +288,7 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
         w_mfma(acc[i][j], b1[j], a1[i]);
       }
       if constexpr (BG && j == 1) {  // the fragment the previous slot's MFMA read
-        if (do_bg) bsum[i] = w_sum8(kk == 0 ? a0[i] : a1[i], bsum[i]);
+        if (do_bg && (i & 1) == wn) bsum[i] = w_sum8(kk == 0 ? a0[i] : a1[i], bsum[i]);
       }
       // k-step 1 fragments of this buffer, one transposed read per MFMA
       if constexpr (n < 32) {
@@ -320,15 +324,18 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
     });
     buf ^= (uint32_t)W_IMG;
     cur_next();
+    ++kc;
   };
   ktile(WI<1>{});
   for (int kt = 1; kt < nk; ++kt) ktile(WI<0>{});
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   if constexpr (BG) {
-    if (do_bg) {
+    const int first = kt0 + ((tn - kt0 % g.tiles_n) + g.tiles_n) % g.tiles_n;  // first kt >= kt0 with kt % tiles_n == tn
+    if (first < kt1) {  // this workgroup summed at least one K-tile
       // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same column's token groups
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
+        if ((f & 1) != wn) continue;
         float v = bsum[f];
         v += __shfl_xor(v, 16);
         v += __shfl_xor(v, 32);
