@@ -117,7 +117,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V5 = 5 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -192,18 +192,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
   } else {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_dst) : "memory");
   }
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
-__device__ __forceinline__ void vm_wait(int n) {
-#define NSA_VMW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-  switch (n) {
-    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
-    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-  }
-#undef NSA_VMW
 }
 
 // =============================================================================
@@ -751,189 +739,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
 }
 
 // =============================================================================
-// forward v5 (D = 64, no dropout): eight waves x 32 queries (256 queries of one (b, h)),
-// the next tile's S issued BEFORE this tile's softmax (cdna_hip_programming.md T15, two S
-// tiles live): per iteration j every wave
-//   reads K_{j+1} fragments and issues S_{j+1}^T = K_{j+1} Q^T (8 MFMAs, asynchronous),
-//   runs the softmax of S_j (its VALU beside those MFMAs, in the same wave),
-//   reads V_j fragments and issues O^T += V_j^T P_j^T (8 MFMAs),
-// with ONE barrier per tile (all waves in step: v3's layout puts two 32-query blocks in a
-// wave for that overlap, at 238 VGPRs with no room for a second S tile).  K/V tiles by
-// LDS-DMA into an NS-slot ring, two pieces per wave per tile; tile t + 1 is waited for
-// before the barrier that opens iteration t, and tile t + NS - 1 is issued after it into
-// the slot tile t - 1 used (its V was read in iteration t - 1, its K in t - 2).
-// Numerics are v3's.
-// =============================================================================
-#ifndef NSA_FWD5_NS
-#define NSA_FWD5_NS 6
-#endif
-__device__ __forceinline__ void fwd5_s(const char* kt, const bf16x8 (&qf)[4], f32x16 (&st)[2], int h, int r) {
-  constexpr int D = 64;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[sb] = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-  }
-}
-
-template <bool MASK>
-__device__ __forceinline__ void fwd5_softmax_pv(const char* vt, f32x16 (&st)[2], f32x16 (&o)[2], float& m_i,
-                                                float& l_i, int kv0, int qpos, int h, int lane, float scale_log2) {
-  constexpr int D = 64;
-  float mt = -INFINITY;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if constexpr (MASK) {
-        if (kv0 + 32 * sb + acc_row(i, h) > qpos) st[sb][i] = -INFINITY;
-      }
-      mt = fmaxf(mt, st[sb][i]);
-    }
-  mt = half_swap_max(mt);
-  const bool grow = (mt - m_i) * scale_log2 > kDeferLog2;
-  if (__builtin_amdgcn_ballot_w64(grow)) {
-    const float m_new = grow ? mt : m_i;
-    const float alpha = fast_exp2((m_i - m_new) * scale_log2);
-    l_i *= alpha;
-    m_i = m_new;
-    o[0] *= alpha;
-    o[1] *= alpha;
-  }
-  const float mc = m_i * scale_log2;
-  float rs = 0.0f;
-  bf16x8 pf[2][2];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = fast_exp2(st[sb][i] * scale_log2 - mc);
-      rs += p;
-      pf[sb][i >> 3][i & 7] = (__bf16)p;
-    }
-  l_i += half_swap_sum(rs);
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
-    }
-}
-
-__global__ __launch_bounds__(512, 1) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2) {
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int NS = NSA_FWD5_NS;
-  constexpr int TILE_BYTES = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
-
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, r = lane & 31;
-  const int q0 = qt * 256;
-  const int q0w = q0 + 32 * wv;  // this wave's queries q0w .. q0w + 31
-  const int qpos = q0w + r;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-
-  bf16x8 qf[4];
-  {
-    const int qc = qpos < T ? qpos : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
-  }
-  f32x16 o[2] = {f32x16{}, f32x16{}}, sa[2], sb2[2];
-  float m_i = -1e30f, l_i = 0.0f;
-
-  const int kv_end = min(T, q0 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-  // a tile is 64 rows x 128 B of K and of V = 16 pieces of 1 KiB; wave wv copies K rows and
-  // V rows 8 wv .. 8 wv + 7
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int prow = 8 * wv + (lane >> 3);
-  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const uint32_t koff = (uint32_t)((prow * (int)row_stride + pch * 8) * 2);
-  auto issue = [&](int jt) {  // wave-uniform; tiles past the end are not fetched
-    if (jt >= n_tiles) return;
-    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
-    uint32_t o0 = koff;
-    if (jt * BN + BN > T) {
-      const int r0 = min(jt * BN + prow, T - 1) - jt * BN;
-      o0 = (uint32_t)((r0 * (int)row_stride + pch * 8) * 2);
-    }
-    const uint32_t kb = lds0 + (uint32_t)((jt % NS) * TILE_BYTES + 8 * wv * 128);
-    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
-    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(kb + NS * TILE_BYTES));
-  };
-  // "tile t landed" at the top of iteration t - 1: tiles t + 1 .. t + NS - 3 (inside the
-  // sequence) were issued after it and may stay in flight, two pieces each
-  auto wait_tile = [&](int t) { vm_wait(2 * max(0, min(t + NS - 3, n_tiles - 1) - t)); };
-  auto active = [&](int t) { return t < n_tiles && t * BN <= q0w + 31; };
-  auto kslot = [&](int t) { return smem + (t % NS) * TILE_BYTES; };
-  auto vslot = [&](int t) { return smem + (NS + t % NS) * TILE_BYTES; };
-
-  asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));  // Q landed before the DMA
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t) issue(t);
-  vm_wait(2 * min(NS - 2, n_tiles - 1));  // tile 0 landed (tiles 1 .. NS - 2 may fly)
-  __builtin_amdgcn_s_barrier();
-  if (active(0)) fwd5_s(kslot(0), qf, sa, h, r);
-  // iteration j: S_{j+1} into the other buffer, softmax + P·V of tile j
-  auto step = [&](int j, f32x16 (&scur)[2], f32x16 (&snext)[2]) {
-    wait_tile(j + 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    issue(j + NS - 1);
-    if (active(j + 1)) fwd5_s(kslot(j + 1), qf, snext, h, r);
-    if (active(j)) {
-      const int kv0 = j * BN;
-      if (kv0 + BN - 1 <= q0w)
-        fwd5_softmax_pv<false>(vslot(j), scur, o, m_i, l_i, kv0, qpos, h, lane, scale_log2);
-      else
-        fwd5_softmax_pv<true>(vslot(j), scur, o, m_i, l_i, kv0, qpos, h, lane, scale_log2);
-    }
-  };
-  int j = 0;
-  for (; j + 1 < n_tiles; j += 2) {
-    step(j, sa, sb2);
-    step(j + 1, sb2, sa);
-  }
-  if (j < n_tiles) step(j, sa, sb2);
-
-  if (qpos < T) {
-    const float inv_l = 1.0f / l_i;
-    bf16_t* orow = out + ((int64_t)b * T + qpos) * C + hh * D;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 u;
-        u.x = pack2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
-        u.y = pack2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
-        *reinterpret_cast<uint2*>(orow + d) = u;
-      }
-    if (h == 0) lse_out[(int64_t)bh * T + qpos] = (m_i * scale_log2 + __log2f(l_i)) * 0.6931471805599453f;
-  }
-}
-
-// =============================================================================
 // backward preprocessing (generic path), one pass over [B, T, C]:
 //   delta[b, h, t] = rowsum(dO * O)  (fp32)
 // =============================================================================
@@ -1425,6 +1230,18 @@ __device__ __forceinline__ void slot_dispatch(int k, F& f) {
   }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0 .. 15)
+__device__ __forceinline__ void vm_wait(int n) {
+#define NSA_VMW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    NSA_VMW(0) NSA_VMW(1) NSA_VMW(2) NSA_VMW(3) NSA_VMW(4) NSA_VMW(5) NSA_VMW(6) NSA_VMW(7)
+    NSA_VMW(8) NSA_VMW(9) NSA_VMW(10) NSA_VMW(11) NSA_VMW(12) NSA_VMW(13) NSA_VMW(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+#undef NSA_VMW
+}
+
 // one 32-query slice for one wave: S, dP for its NKB key blocks, P / dS, then dV^T, dK^T.
 // ld = this wave's copy of the slice's row constants: [0, 32) -lse/scale, [32, 64) -delta.
 template <int NKB, bool MASK, bool DROP>
@@ -1875,11 +1692,6 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if (sel == FWD_V5 && !th) {
-      flash_fwd5_kernel<<<n_qt3 * B * H, 512, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                      scale * kLog2e);
-      return hipGetLastError();
-    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -2021,7 +1833,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V5) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
