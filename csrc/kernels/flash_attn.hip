@@ -117,7 +117,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -562,82 +562,6 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
   }
 }
 
-// SUB (no dropout): the softmax and P·V per 32-key sub-block instead of per 64-key tile,
-// with every S MFMA of the tile issued first.  The max / exp / pack of sub-block 0 then run
-// while sub-block 1's S MFMAs execute, and sub-block 0's P·V MFMAs while sub-block 1's
-// softmax runs -- the tile-wide max of the plain order waits for all 16 S MFMAs and issues
-// no MFMA until the whole softmax is done.  The deferred-rescale check runs per sub-block
-// (online softmax is exact at any chunking), and P is packed 16 registers at a time.
-template <bool MASK>
-__device__ __forceinline__ void fwd_tile2_sub(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
-                                              f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
-                                              int h, int r, int lane, float scale_log2) {
-  constexpr int D = 64;
-  f32x16 st[2][2];  // [block][key sub-block]
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[0][sb] = f32x16{};
-    st[1][sb] = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
-      st[0][sb] = mfma(kf, qf[0][ks], st[0][sb]);
-      st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
-    }
-  }
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    float mt[2];
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      mt[blk] = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if constexpr (MASK) {
-          if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) st[blk][sb][i] = -INFINITY;
-        }
-        mt[blk] = fmaxf(mt[blk], st[blk][sb][i]);
-      }
-      mt[blk] = half_swap_max(mt[blk]);
-    }
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      const bool grow = (mt[blk] - m_i[blk]) * scale_log2 > kDeferLog2;
-      if (__builtin_amdgcn_ballot_w64(grow)) {
-        const float m_new = grow ? mt[blk] : m_i[blk];
-        const float alpha = fast_exp2((m_i[blk] - m_new) * scale_log2);
-        l_i[blk] *= alpha;
-        m_i[blk] = m_new;
-        o[blk][0] *= alpha;
-        o[blk][1] *= alpha;
-      }
-    }
-    bf16x8 pf[2][2];  // [block][16-key half]
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      const float mc = m_i[blk] * scale_log2;
-      float rs = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fast_exp2(st[blk][sb][i] * scale_log2 - mc);
-        rs += p;
-        pf[blk][i >> 3][i & 7] = (__bf16)p;
-      }
-      l_i[blk] += half_swap_sum(rs);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
-        o[0][dt] = mfma(vf, pf[0][s], o[0][dt]);
-        o[1][dt] = mfma(vf, pf[1][s], o[1][dt]);
-      }
-    }
-  }
-}
-
 // Diagnostic build only (-DNSA_FWD3_STAMPS=1, scripts/fwd3_stamps.py): per-wave s_memtime
 // totals of the v3 tile loop -- [loop, S issue, S wait + softmax, P·V issue, DMA wait +
 // barrier, tiles] -- into a buffer of their own (no output is computed from them).
@@ -651,7 +575,7 @@ __device__ unsigned long long g_fwd3_stamps[16384 * 4 * 6];
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
 // not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
-template <bool DROP, int NS, bool SUB = false>
+template <bool DROP, int NS>
 __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
                                                             float scale_log2, uint32_t drop_thresh, float drop_scale,
@@ -756,10 +680,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
 #else
     unsigned long long* st2 = nullptr;
 #endif
-    if (SUB && !DROP) {
-      if (kv0 + BN - 1 <= q0w) fwd_tile2_sub<false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2);
-      else if (kv0 <= q0w + 63) fwd_tile2_sub<true>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2);
-    } else if (kv0 + BN - 1 <= q0w) {  // wave-uniform: every key of the tile visible to all 64 queries
+    if (kv0 + BN - 1 <= q0w) {  // wave-uniform: every key of the tile visible to all 64 queries
       fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr, st2);
 #if NSA_FWD3_STAMPS
       did = true;
@@ -1771,11 +1692,6 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if (sel == FWD_V4 && !th) {  // v3 with the per-sub-block softmax / P·V (A/B)
-      flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
-                                                                      B, T, H, scale * kLog2e, th, dscale, seed);
-      return hipGetLastError();
-    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -1917,7 +1833,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
