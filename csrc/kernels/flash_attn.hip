@@ -117,7 +117,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
 //   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4 };
 enum { BWD_V1 = 1, BWD_V2 = 2 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -575,7 +575,7 @@ __device__ unsigned long long g_fwd3_stamps[16384 * 4 * 6];
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
 // not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
-template <bool DROP, int NS>
+template <bool DROP, int NS, bool PAIR = false>
 __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
                                                             float scale_log2, uint32_t drop_thresh, float drop_scale,
@@ -657,6 +657,33 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
   };
   asm volatile("" ::"v"(qf[0][0]), "v"(qf[0][1]), "v"(qf[0][2]), "v"(qf[0][3]), "v"(qf[1][0]), "v"(qf[1][1]),
                "v"(qf[1][2]), "v"(qf[1][3]));  // Q landed before the DMA
+  if constexpr (PAIR && NS == 4 && !DROP) {
+    // two tiles per barrier: pair (j, j + 1) is computed while tiles j + 2, j + 3 fly into
+    // the slots of j - 2, j - 1 (freed by the barrier that opens the pair)
+    issue(0, 0);
+    issue(min(1, n_tiles - 1), 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int j = 0; j < n_tiles; j += 2) {
+      issue(min(j + 2, n_tiles - 1), (j + 2) % 4);
+      issue(min(j + 3, n_tiles - 1), (j + 3) % 4);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int jj = j + u;
+        if (jj < n_tiles) {
+          const int kv0 = jj * BN;
+          const char* kt = smem + (jj % 4) * TILE_BYTES;
+          const char* vt = smem + (4 + jj % 4) * TILE_BYTES;
+          if (kv0 + BN - 1 <= q0w)
+            fwd_tile2<false, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+          else if (kv0 <= q0w + 63)
+            fwd_tile2<true, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t) issue(min(t, n_tiles - 1), t);
   wait_next();  // tile 0 landed
@@ -715,6 +742,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
   }
 #endif
 
+  }
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int qp = qposA + 32 * blk;
@@ -1692,6 +1720,11 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
+    if (sel == FWD_V4 && !th) {  // v3 with two tiles per barrier (A/B)
+      flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
+                                                                      B, T, H, scale * kLog2e, th, dscale, seed);
+      return hipGetLastError();
+    }
     const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
       if (th)
@@ -1833,7 +1866,7 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4) c.fwd = fwd;
   if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;

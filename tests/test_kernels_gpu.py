@@ -337,7 +337,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
