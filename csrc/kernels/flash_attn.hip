@@ -113,20 +113,24 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3: D = 64 forward kernel; auto = v3
-//         without dropout once the grid has >= 4096 v3 workgroups, else v1 (fwd_launch)
-//   bwd   NSA_FLASH_BWD = v2 (default) | v1: D = 64 backward (v1 = the generic kernels)
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4: D = 64 forward kernel; auto = v4
+//         (v3 with two K/V tiles per barrier) without dropout once the grid has >= 4096
+//         v3 workgroups, else v1 (fwd_launch); v3 = one tile per barrier
+//   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
+//         kernel taking two query slices per barrier; v1 = the generic kernels
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
 enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4 };
-enum { BWD_V1 = 1, BWD_V2 = 2 };
+enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
 FlashConfig& flash_config() {
   static FlashConfig c = [] {
-    FlashConfig d{FWD_AUTO, BWD_V2, ATTN_ORDER_DEFAULT};
-    if (const char* e = getenv("NSA_FLASH_FWD")) d.fwd = (e[0] == 'v' && e[1] == '1') ? FWD_V1 : (e[0] == 'v' && e[1] == '3') ? FWD_V3 : FWD_AUTO;
-    if (const char* e = getenv("NSA_FLASH_BWD")) d.bwd = (e[0] == 'v' && e[1] == '1') ? BWD_V1 : BWD_V2;
+    FlashConfig d{FWD_AUTO, BWD_V3, ATTN_ORDER_DEFAULT};
+    if (const char* e = getenv("NSA_FLASH_FWD"))
+      d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '3' || e[1] == '4')) ? e[1] - '0' : FWD_AUTO;
+    if (const char* e = getenv("NSA_FLASH_BWD"))
+      d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
     return d;
   }();
@@ -1342,7 +1346,7 @@ __device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, cons
 #define NSA_DKDV_NS 4  // LDS ring slots of the v2 dK/dV kernel (NS - 1 slices in flight)
 #endif
 
-template <int NKB, int NW, bool DROP>
+template <int NKB, int NW, bool DROP, bool PAIR = false>
 __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
     const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
@@ -1396,7 +1400,7 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
     glds4(csrc + s * 32, sb + (uint32_t)(2 * V2_QT + w * 256));
   };
 
-  for (int j = 0; j < LA && j < n_mine; ++j) issue(s_first + j, j);
+  for (int j = 0; j < (PAIR ? 2 : LA) && j < n_mine; ++j) issue(s_first + j, j);
 
   // K^T / V^T fragments (B operands of S = Q·K^T, dP = dO·V^T): K[key][16ks + 8h ..]
   bf16x8 kf[NKB][4], vf[NKB][4];
@@ -1458,15 +1462,35 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   // iterations in all: same barrier count.
   const int j_diag = min(NKB * w, n_mine);
   const int j_full = min(NKB * w + NKB, n_mine);
-  int j = 0;
-  for (; j < j_diag; ++j) open_slice(j);
-  for (; j < j_full; ++j) {
-    open_slice(j);
-    slice_diag(j);
-  }
-  for (; j < n_mine; ++j) {
-    open_slice(j);
-    slice_full(j);
+  if constexpr (PAIR && NS == 4) {
+    // two slices per barrier: pair (j, j + 1) runs while slices j + 2, j + 3 fly into the
+    // slots of j - 2, j - 1 (freed by the barrier that opens the pair)
+    for (int j = 0; j < n_mine; j += 2) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (j + 2 < n_mine) issue(s_first + j + 2, (j + 2) % NS);
+      if (j + 3 < n_mine) issue(s_first + j + 3, (j + 3) % NS);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int jj = j + u;
+        if (jj >= j_full) {
+          if (jj < n_mine) slice_full(jj);
+        } else if (jj >= j_diag) {
+          slice_diag(jj);
+        }
+      }
+    }
+  } else {
+    int j = 0;
+    for (; j < j_diag; ++j) open_slice(j);
+    for (; j < j_full; ++j) {
+      open_slice(j);
+      slice_diag(j);
+    }
+    for (; j < n_mine; ++j) {
+      open_slice(j);
+      slice_full(j);
+    }
   }
 
   // epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T -> dqkv[:, :, C + ...] and [2C + ...]
@@ -1720,14 +1744,14 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if (sel == FWD_V4 && !th) {  // v3 with two tiles per barrier (A/B)
-      flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
-                                                                      B, T, H, scale * kLog2e, th, dscale, seed);
-      return hipGetLastError();
-    }
-    const bool v3 = sel == FWD_V3 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
+    const bool v3 = sel == FWD_V3 || sel == FWD_V4 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3) {
-      if (th)
+      // v4 = v3 with two K/V tiles per barrier (auto's pick): B120 T1024 H12 335.5 vs
+      // 350.9 us (profiles/r4_attn_ab_pair.log)
+      if (sel != FWD_V3 && !th)
+        flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
+                                                                        B, T, H, scale * kLog2e, th, dscale, seed);
+      else if (th)
         flash_fwd3_kernel<true, 4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
                                                                  H, scale * kLog2e, th, dscale, seed);
       else
@@ -1812,7 +1836,13 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int n_kb = (T + 127) / 128;
-  if (th)
+  // two query slices per barrier (v3, default): B120 T1024 H12 whole backward 1151 vs 1181 us
+  // (profiles/r4_attn_ab_pair.log; the same change in the dQ kernel measured 1152)
+  if (flash_config().bwd == BWD_V3 && !th)
+    flash_bwd_dkdv2_kernel<1, 4, false, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+                                                                          nls, nd, (bf16_t*)dqkv, B, T, H, scale,
+                                                                          scale * kLog2e, th, dscale, seed, order);
+  else if (th)
     flash_bwd_dkdv2_kernel<1, 4, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd,
                                                                    (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
                                                                    dscale, seed, order);
@@ -1831,7 +1861,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
 NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (D == 64 && T % 32 == 0 && flash_config().bwd == BWD_V2)
+  if (D == 64 && T % 32 == 0 && flash_config().bwd >= BWD_V2)
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
     case 32: return bwd_launch<32>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
@@ -1860,14 +1890,14 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
   }
 }
 
-// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3, bwd 1 v1 / 2 v2, order
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4, bwd 1 v1 / 2 v2 / 3 v3, order
 // 0 / 1; a negative value keeps the current setting.  Returns the previous selection as
 // fwd | bwd << 4 | order << 8.
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4) c.fwd = fwd;
-  if (bwd == BWD_V1 || bwd == BWD_V2) c.bwd = bwd;
+  if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;
 }

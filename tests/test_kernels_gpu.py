@@ -362,7 +362,7 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -409,6 +409,29 @@ def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     for i, name in enumerate("qkv"):
         e = rel_err(g[:, :, i], gr[:, :, i])
         assert e < 4e-2, f"{pattern}: d{name} rel err {e}"
+
+
+@pytest.mark.parametrize("T", [320, 1024, 96, 64])
+@pytest.mark.parametrize("ver", ["v3"])
+def test_flash_bwd_pair_matches_v2(kernels, flash_variant, T, ver):
+    """Backward v3 (the default: the v2 dK/dV kernel with two query slices per barrier)
+    against v2 (one slice per barrier), bitwise (same per-slice arithmetic)."""
+    from nanosandbox_amd.ops import functional as fn
+
+    torch.manual_seed(0)
+    B, H, D = 2, 3, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
+    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
+    grads = {}
+    for v in ("v2", ver):
+        flash_variant(bwd=v)
+        x = qkv.clone().requires_grad_(True)
+        fn.attention(x, H, 0.0, True).backward(dy)
+        torch.cuda.synchronize()
+        grads[v] = x.grad.float().view(B, T, 3, H * D)
+    for i, name in enumerate("qkv"):
+        e = rel_err(grads[ver][:, :, i], grads["v2"][:, :, i])
+        assert e < 1e-6, f"d{name}: {ver} vs v2 rel err {e}"
 
 
 @pytest.mark.parametrize("T", [320, 1024, 96])
