@@ -191,6 +191,25 @@ __device__ __forceinline__ nsa_f32x2 nsa_gelu_grad2(nsa_f32x2 x) {
   nsa_gelu_cdf_pdf2(x, c, p);
   return c + x * p;
 }
+// gelu(x) and gelu'(x) from one erf / pdf evaluation (the c_fc GELU epilogue stores gelu'(u)
+// for the backward instead of u: see gemm_nt4.hip Q_EPI_GELU)
+__device__ __forceinline__ void nsa_gelu_and_grad2(nsa_f32x2 x, nsa_f32x2& g, nsa_f32x2& gp) {
+  nsa_f32x2 c, p;
+  nsa_gelu_cdf_pdf2(x, c, p);
+  g = x * c;
+  gp = c + x * p;
+}
+
+// fp16 pairs (gelu'(u) is stored as fp16: 2^-11 relative rounding, 4x finer than bf16)
+typedef _Float16 nsa_f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t nsa_pk_f16(float a, float b) {  // v_cvt_pk_f16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((nsa_f32x2{a, b}), nsa_f16x2));
+}
+__device__ __forceinline__ nsa_f32x2 nsa_unpk_f16(uint32_t u) {
+  return __builtin_convertvector(__builtin_bit_cast(nsa_f16x2, u), nsa_f32x2);
+}
+__device__ __forceinline__ float nsa_h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint16_t nsa_f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
 // Nontemporal streams only pay for tensors larger than the 256 MB Infinity Cache: a smaller
 // one can stay cache-resident for its next reader (shakespeare_char config, 25 MB LayerNorm

@@ -1,6 +1,7 @@
 // Persistent four-wave bf16 "NT" GEMM for gfx950: C[M,N] = A[M,K] · B[N,K]^T (both operands
 // K-contiguous, fp32 accumulate), with the same epilogues as gemm_nt.hip (bf16 store,
-// u + gelu(u) for the c_fc forward, acc * gelu'(U) for the mlp.c_proj input grad).
+// gelu'(u) (fp16) + gelu(u) for the c_fc forward, acc * U with U = gelu'(u) for the mlp.c_proj
+// input grad).
 //
 // Why a second NT kernel: the 8-wave kernel (gemm_nt.hip, 128x64 per wave) reads
 // 24 fragments (24 KiB) per wave per 64-deep K-tile for 64 MFMAs; with 8 waves that is
@@ -376,27 +377,36 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           for (int h = 0; h < 4; ++h) w[h] = q_pk(acc[i][2 * h][e], acc[i][2 * h + 1][e]);
         }
         if constexpr (EPI == Q_EPI_DGELU) {
+          // U holds gelu'(u) as fp16 pairs (written by the forward's GELU epilogue)
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            const uint32_t u = uv[i & 1][e][h];
             const nsa_f32x2 a = nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)} *
-                                nsa_gelu_grad2(nsa_f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)});
+                                nsa_unpk_f16(uv[i & 1][e][h]);
             w[h] = q_pk(a.x, a.y);
           }
         }
-        if constexpr (NOSTORE) {
+        if constexpr (EPI == Q_EPI_GELU) {
+          // u = w (bf16, as the reference's autocast c_fc output): C <- gelu'(u) as fp16 (the
+          // backward's only use of u, so its GELU' epilogue is one multiply), C2 <- gelu(u)
+          uint32_t gg[4], gp[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            nsa_f32x2 gv, dv;
+            nsa_gelu_and_grad2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)}, gv, dv);
+            gg[h] = q_pk(gv.x, gv.y);
+            gp[h] = nsa_pk_f16(dv.x, dv.y);
+          }
+          if constexpr (NOSTORE) {
+            asm volatile("" ::"v"(gp[0]), "v"(gp[1]), "v"(gp[2]), "v"(gp[3]), "v"(gg[0]), "v"(gg[1]), "v"(gg[2]),
+                         "v"(gg[3]));
+          } else {
+            q_st16<NT>(cb + off, gp[0], gp[1], gp[2], gp[3]);
+            q_st16<NT>(cb2 + off, gg[0], gg[1], gg[2], gg[3]);
+          }
+        } else if constexpr (NOSTORE) {
           asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
         } else {
           q_st16<NT>(cb + off, w[0], w[1], w[2], w[3]);
-        }
-        if constexpr (EPI == Q_EPI_GELU) {
-          uint32_t gg[4];
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const nsa_f32x2 gv = nsa_gelu2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)});
-            gg[h] = q_pk(gv.x, gv.y);
-          }
-          q_st16<NT>(cb2 + off, gg[0], gg[1], gg[2], gg[3]);
         }
       }
       if constexpr (EPI == Q_EPI_XENT) {
@@ -478,7 +488,10 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   }
 
   // piece P of K-tile cursor c into buffer buf (the pieces of an M0 group are issued in order)
-  // GLDS: per-piece VGPR offsets (row offset folded in), the tile base as an SGPR pair
+  // GLDS: per-piece VGPR offsets (row offset folded in), the tile base as an SGPR pair.  (The
+  // plain-epilogue instantiations spill a few of these: 2 x 6 VGPRs, reloaded behind a
+  // vmcnt(0) at the epilogue head.  Adding voff + soff at each issue instead (no spills)
+  // measured 2.8 ms/step slower: the 16 adds per K-tile cost more than the drain.)
   uint32_t vpA[NSA_NT4_GLDS ? 8 : 1], vpB[NSA_NT4_GLDS ? 8 : 1];
   if constexpr (NSA_NT4_GLDS) {
 #pragma unroll
@@ -647,7 +660,7 @@ bool nt4_store_nt(int stp, int64_t out_bytes) { return stp == 1 || (stp == 0 && 
 }  // namespace
 
 // C = A · B^T (bf16) with an optional bias[N] (bf16) added to every row.
-// epi: 0 bf16, 1 u + gelu(u) into C / C2, 2 acc * gelu'(U); bits 8-11 timing probe (-DNSA_PROBES
+// epi: 0 bf16, 1 gelu'(u) (fp16) / gelu(u) into C / C2, 2 acc * U (U = gelu'(u), fp16); bits 8-11 timing probe (-DNSA_PROBES
 // builds only; 1 no DMA, 4 no stores, ...); bits 12-13 store policy: 0 nontemporal above the
 // Infinity Cache, 1 always, 2 never; bits 16-23 row-blocks per tile group, 0 = automatic.
 // grid = persistent workgroups.

@@ -1,7 +1,7 @@
 // Bounds-checked bf16 "NT" GEMM for the shapes the persistent four-wave kernel (gemm_nt4.hip)
 // does not take: M or N below one 256 x 256 tile (tiny models, short prefills, test
 // configs), K not a multiple of 64, odd N.  C[M,N] = A[M,K] · B[N,K]^T, fp32 accumulate, the
-// same epilogues as gemm_nt4.hip (bf16 / + bias, u + gelu(u), acc * gelu'(U)).
+// same epilogues as gemm_nt4.hip (bf16 / + bias, gelu'(u) + gelu(u), acc * U).
 //
 // Geometry: 64 x 64 output tile per 256-thread workgroup, 4 waves as 2 x 2 of 32 x 32 (2 x 2
 // accumulators of v_mfma_f32_16x16x32_bf16), 32-deep K steps staged through LDS with
@@ -75,10 +75,15 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restric
         if (row >= M) continue;
         const int64_t o = (int64_t)row * ldc + col;
         float v = acc[i][j][e] + bcol;
-        if constexpr (EPI == S_EPI_DGELU) v = bf2f(f2bf(v)) * nsa_gelu_grad(bf2f(U[o]));
+        if constexpr (EPI == S_EPI_DGELU) v = bf2f(f2bf(v)) * nsa_h2f(U[o]);  // U = gelu'(u), fp16
         const bf16_t vb = f2bf(v);
-        C[o] = vb;
-        if constexpr (EPI == S_EPI_GELU) C2[o] = f2bf(nsa_gelu(bf2f(vb)));
+        if constexpr (EPI == S_EPI_GELU) {  // C <- gelu'(u) (fp16), C2 <- gelu(u)
+          const float uf = bf2f(vb);
+          C[o] = nsa_f2h(nsa_gelu_grad(uf));
+          C2[o] = f2bf(nsa_gelu(uf));
+        } else {
+          C[o] = vb;
+        }
       }
     }
   }
@@ -86,7 +91,8 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restric
 
 }  // namespace
 
-// Same contract as nsa_gemm_nt4 (epi 0 bf16, 1 u + gelu(u) into C / C2, 2 acc * gelu'(U);
+// Same contract as nsa_gemm_nt4 (epi 0 bf16, 1 gelu'(u) (fp16) / gelu(u) into C / C2, 2 acc * U with
+// U = gelu'(u) in fp16;
 // optional bias[N]) for any M, N >= 1 and K % 8 == 0 (lda, ldb % 8 == 0, 16-B aligned rows).
 NSA_API hipError_t nsa_gemm_small(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
                                   const void* U, const void* bias, int M, int N, int K, hipStream_t s) {

@@ -524,8 +524,9 @@ def linear(x, w, b=None, residual=None):
 class MLPFn(torch.autograd.Function):
     """c_proj(gelu(c_fc(x) + b_fc)) + b_proj as ONE autograd node.
 
-    Forward: the c_fc GEMM's epilogue adds b_fc and writes both u and g = gelu(u); the
-    c_proj GEMM adds b_proj.  Backward: du = (dy W_proj) * gelu'(u) from one GEMM epilogue,
+    Forward: the c_fc GEMM's epilogue adds b_fc and writes g = gelu(u) and gelu'(u) (fp16,
+    the backward's only use of u); the c_proj GEMM adds b_proj.  Backward: du = (dy W_proj) *
+    gelu'(u) from one GEMM epilogue (a multiply),
     dx = du W_fc, both weight gradients accumulated in fp32 by the split-K GEMM, the bias
     gradients from the same kernel's dY fragments (``weight_bias_grad``)."""
 
@@ -536,18 +537,18 @@ class MLPFn(torch.autograd.Function):
         wf = compute_weight(w_fc, x.dtype)
         bf = compute_weight(b_fc, x.dtype) if b_fc is not None else None
         bp = compute_weight(b_proj, x.dtype) if b_proj is not None else None
-        u, g = _gd.fwd_gelu(x2, wf, bf)
+        gp, g = _gd.fwd_gelu(x2, wf, bf)
         y = _gd.fwd(g, compute_weight(w_proj, x.dtype), bp)
-        ctx.save_for_backward(x2, u, g, w_fc, b_fc, w_proj, b_proj)
+        ctx.save_for_backward(x2, gp, g, w_fc, b_fc, w_proj, b_proj)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w_proj.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, u, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
+        x2, gp, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         gw_proj, gb_proj = weight_bias_grad(w_proj, b_proj, dy2, g)
-        du = _gd.dgrad_dgelu(dy2, compute_weight(w_proj, dy.dtype), u)
+        du = _gd.dgrad_dgelu(dy2, compute_weight(w_proj, dy.dtype), gp)
         gw_fc, gb_fc = weight_bias_grad(w_fc, b_fc, du, x2)
         dx = _gd.dgrad(du, compute_weight(w_fc, dy.dtype))
         return dx.view(ctx.xshape), gw_fc, gb_fc, gw_proj, gb_proj

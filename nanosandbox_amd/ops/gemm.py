@@ -4,7 +4,8 @@
                            kernel (``csrc/kernels/gemm_nt4.hip``; M, N >= 256, K % 64 == 0,
                            N % 8 == 0): every forward Y = X · W^T and, on the cached weight
                            transpose, every input grad dX = dY · W.  Epilogues: bf16 (+ bias),
-                           u + gelu(u), acc · gelu'(U); the fused cross-entropy pair
+                           gelu'(u) (fp16) + gelu(u), acc · U (U = that gelu'(u)); the fused
+                           cross-entropy pair
                            ``nt_xent`` / ``nt_xdx``.
 * ``small(a, b, ...)``     the same contract for any M, N (K % 8 == 0) on the bounds-checked
                            64 x 64 kernel (``csrc/kernels/gemm_small.hip``): tiny models, short
@@ -71,30 +72,40 @@ def wgrad_supported(n_out, n_in, tokens) -> bool:
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 
-def _out(M, N, device, out):
+def _out(M, N, device, out, dtype=BF16):
     if out is None:
-        return torch.empty(M, N, device=device, dtype=BF16)
+        return torch.empty(M, N, device=device, dtype=dtype)
     _check(out, "out")
+    if out.dtype != dtype:
+        raise ValueError(f"out must be {dtype}")
     return out
+
+
+def _check_gp(u):
+    _check(u, "u")
+    if u.dtype != torch.float16:
+        raise ValueError("u must be gelu'(u) in fp16 (the NT_EPI_GELU epilogue's first output)")
 
 
 def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, gm=0, out=None, out2=None):
     """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the four-wave kernel.
 
     ``bias`` [N] (bf16) is added in the epilogue (before the GELU).  epi NT_EPI_GELU returns
-    (u, gelu(u)); NT_EPI_DGELU returns (a @ b^T) * gelu'(u).  ``probe`` needs a library built
-    with -DNSA_PROBES (scripts/gemm_nt_ab.py)."""
+    (gelu'(u) as fp16, gelu(u) as bf16) for u = bf16(a @ b^T + bias): the backward's only use of
+    u is gelu'(u), so the forward stores that (fp16: 2^-11 relative rounding) and the
+    NT_EPI_DGELU epilogue, given it as ``u``, is a single multiply: bf16(bf16(a @ b^T) * u).
+    ``probe`` needs a library built with -DNSA_PROBES (scripts/gemm_nt_ab.py)."""
     M, K = a.shape
     N = b.shape[0]
     _check(a, "a")
     _check(b, "b")
     if bias is not None:
         _check(bias, "bias")
-    c = _out(M, N, a.device, out)
+    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else BF16)
     var = NT_VAR if var is None else var
     c2 = (_out(M, N, a.device, out2)) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
-        _check(u, "u")
+        _check_gp(u)
     _lib.call("nsa_gemm_nt4", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
               b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
               grid or num_cus(a.device), _lib.stream())
@@ -107,10 +118,10 @@ def small(a, b, epi=NT_EPI_BF16, u=None, bias=None, out=None, out2=None):
     N = b.shape[0]
     _check(a, "a")
     _check(b, "b")
-    c = _out(M, N, a.device, out)
+    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else BF16)
     c2 = _out(M, N, a.device, out2) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
-        _check(u, "u")
+        _check_gp(u)
     _lib.call("nsa_gemm_small", epi, _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), _lib.ptr(c), c.stride(0),
               _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K, _lib.stream())
     return (c, c2) if epi == NT_EPI_GELU else c

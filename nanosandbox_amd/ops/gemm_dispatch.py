@@ -80,9 +80,9 @@ def _nt(a, b, epi=_gemm.NT_EPI_BF16, u=None, bias=None, op="fwd"):
     if bias is not None:
         y = y + bias
     if epi == _gemm.NT_EPI_GELU:
-        return y, _gelu_torch(y)
+        return _gelu_grad_torch(y.float()).to(torch.float16), _gelu_torch(y)
     if epi == _gemm.NT_EPI_DGELU:
-        return (y.float() * _gelu_grad_torch(u.float())).to(y.dtype)
+        return (y.float() * u.float()).to(y.dtype)
     return y
 
 
@@ -101,7 +101,8 @@ def fwd(x2, w, b=None):
 
 
 def fwd_gelu(x2, w, b=None):
-    """(u, gelu(u)) with u = x2 @ w^T (+ b), both from one GEMM epilogue."""
+    """(gelu'(u) in fp16, gelu(u)) with u = x2 @ w^T (+ b), both from one GEMM epilogue (the
+    backward needs u only through gelu'(u); ``gemm.nt``)."""
     return _nt(x2, w, epi=_gemm.NT_EPI_GELU, bias=b, op="fwd_gelu")
 
 
@@ -110,9 +111,9 @@ def dgrad(dy2, w):
     return _nt(dy2, _wt(w), op="dgrad")
 
 
-def dgrad_dgelu(dy2, w, u):
-    """(dy2 @ w) * gelu'(u) from one GEMM epilogue."""
-    return _nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=u, op="dgrad_dgelu")
+def dgrad_dgelu(dy2, w, gp):
+    """(dy2 @ w) * gp from one GEMM epilogue, gp = gelu'(u) from ``fwd_gelu``."""
+    return _nt(dy2, _wt(w), epi=_gemm.NT_EPI_DGELU, u=gp, op="dgrad_dgelu")
 
 
 def wgrad_acc(dy2, x2, g32, gb32=None):

@@ -8,8 +8,12 @@ Timing: interleaved rounds in one process on uniform [-1, 1) operands
     python scripts/gemm_nt_ab.py [--m 122880] [--rounds 5] [--probe] [--epi] [--gms 1,4] [--vars 1,2]
 
 ``--probe`` needs a library built with -DNSA_PROBES (the structure probes: no DMA, no vmcnt
-wait, no barrier, no epilogue, no stores).
+wait, no barrier, no epilogue, no stores).  ``--alt-lib PATH`` loads a second build of the
+kernel library (e.g. ``nanosandbox_amd.build.build_variant``) beside the default one and times
+its nt4 kernel as "nt4_alt" in the same interleaved rounds.
 """
+
+import ctypes
 
 import argparse
 import json
@@ -46,7 +50,23 @@ def main():
     ap.add_argument("--epi", action="store_true", help="also time the GELU / GELU' epilogues")
     ap.add_argument("--gms", default="", help="extra tile-group sizes to time, e.g. 1,4,8")
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
+    ap.add_argument("--alt-lib", default="")
     a = ap.parse_args()
+    alt = None
+    if a.alt_lib:
+        alt = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4
+        alt.argtypes = _lib._SIGNATURES["nsa_gemm_nt4"]
+        alt.restype = ctypes.c_int
+
+    def nt_alt(x, w, epi=0, u=None):
+        M_, K_ = x.shape
+        N_ = w.shape[0]
+        c = torch.empty(M_, N_, device=x.device, dtype=torch.float16 if epi == gemm.NT_EPI_GELU else torch.bfloat16)
+        c2 = torch.empty(M_, N_, device=x.device, dtype=torch.bfloat16) if epi == gemm.NT_EPI_GELU else None
+        err = alt(epi | (gemm.NT_VAR << 12), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c),
+                  c.stride(0), _lib.ptr(c2), _lib.ptr(u), None, M_, N_, K_, gemm.num_cus(x.device), _lib.stream())
+        assert err == 0, err
+        return (c, c2) if epi == gemm.NT_EPI_GELU else c
     M = a.m
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     print(json.dumps({"device": torch.cuda.get_device_name(), "cus": gemm.num_cus()}), flush=True)
@@ -66,6 +86,9 @@ def main():
         tail = ((got[-256:].float() - x[-256:].float() @ w.float().t()).abs().max()).item()
         print(json.dumps({"check": name, "rel_err": rel(got[rows], ref), "tail_maxabs": tail}), flush=True)
         cands = {"torch_matmul": lambda: x @ w.t(), "nt4": lambda: gemm.nt(x, w)}
+        if alt is not None:
+            assert torch.equal(nt_alt(x, w), got)
+            cands["nt4_alt"] = lambda: nt_alt(x, w)
         for gm_ in [int(t) for t in a.gms.split(",") if t]:
             cands[f"nt4_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_)
         for v in [int(t) for t in a.vars.split(",") if t and t != "0"]:
@@ -76,7 +99,8 @@ def main():
             for pr, nm in ((1, "nodma"), (2, "novmwait"), (3, "nobarrier"), (4, "noepi"), (5, "nostore")):
                 cands[f"nt4_{nm}"] = lambda pr=pr: gemm.nt(x, w, probe=pr)
         if a.epi and name == "c_fc":
-            u, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+            gp, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+            u = gemm.nt(x, w)
             eg = ((g.float() - torch.nn.functional.gelu(u.float())).abs().max()).item()
             print(json.dumps({"check": name + "/gelu", "maxabs_g_vs_gelu(u)": eg}), flush=True)
 
@@ -86,12 +110,14 @@ def main():
                 _lib.call("nsa_gelu_fwd", _lib.ptr(uu), _lib.ptr(gg), uu.numel(), _lib.stream())
             cands["torch_matmul+gelu"] = split
             cands["nt4_gelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+            if alt is not None:
+                cands["nt4_alt_gelu"] = lambda: nt_alt(x, w, epi=gemm.NT_EPI_GELU)
         if a.epi and name == "mlp.c_proj.dx":
             u = uni(M, N, scale=3.0)
-            got = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u)
-            ref = (x.float() @ w.float().t()).to(torch.bfloat16).float()
             uf = u.float()
-            ref = ref * (0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) * 0.3989422804014327)
+            gp = (0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) * 0.3989422804014327).half()
+            got = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=gp)  # U = gelu'(u) in fp16 (the GELU epilogue's output)
+            ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() * gp.float()
             print(json.dumps({"check": name + "/dgelu", "rel_err": rel(got, ref)}), flush=True)
             del ref, uf
 
@@ -100,7 +126,9 @@ def main():
                 du = torch.empty_like(dg)
                 _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
             cands["torch_matmul+dgelu"] = split2
-            cands["nt4_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=u)
+            cands["nt4_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=gp)
+            if alt is not None:
+                cands["nt4_alt_dgelu"] = lambda: nt_alt(x, w, epi=gemm.NT_EPI_DGELU, u=gp)
         for fn in cands.values():
             fn()
         torch.cuda.synchronize()

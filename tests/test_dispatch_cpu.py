@@ -113,8 +113,15 @@ def test_cpu_fallbacks_match_torch():
     torch.manual_seed(0)
     x, w, b = torch.randn(5, 8), torch.randn(3, 8), torch.randn(3)
     assert torch.allclose(gemm_dispatch.fwd(x, w, b), x @ w.t() + b)
-    u, g = gemm_dispatch.fwd_gelu(x, w)
+    gp, g = gemm_dispatch.fwd_gelu(x, w)
+    u = x @ w.t()
     assert torch.allclose(g, torch.nn.functional.gelu(u))
+    assert gp.dtype == torch.float16  # gelu'(u), the backward's only use of u
+    uu = u.clone().requires_grad_(True)
+    torch.nn.functional.gelu(uu).backward(torch.ones_like(uu))
+    assert torch.allclose(gp.float(), uu.grad, rtol=2 ** -10, atol=1e-6)
+    w2, dy2 = torch.randn(4, 3), torch.randn(5, 4)  # the next layer (c_proj: 3 -> 4) and its output grad
+    assert torch.allclose(gemm_dispatch.dgrad_dgelu(dy2, w2, gp), (dy2 @ w2) * gp.float())
     gacc = torch.zeros(3, 8)
     gemm_dispatch.wgrad_acc(torch.randn(5, 3), x, gacc)
     gb = torch.zeros(3)

@@ -36,6 +36,15 @@ def gelu_grad(uf):
     return 0.5 * (1 + torch.erf(uf / 2 ** 0.5)) + uf * torch.exp(-0.5 * uf * uf) / (2 * torch.pi) ** 0.5
 
 
+def check_gelu_pair(gp, g, u, name):
+    """The GELU epilogue's outputs for the bf16 pre-activation u: gelu'(u) in fp16 (one fp16
+    rounding, 2^-11, plus the erf approximation) and gelu(u) in bf16."""
+    assert gp.dtype == torch.float16 and g.dtype == BF
+    uf = u.float()
+    check(gp, gelu_grad(uf), torch.ones_like(uf), rel=2 ** -10, name=name + " gelu'")
+    check(g, F.gelu(uf), uf.abs() + 1, rel=2 ** -7, name=name + " gelu")
+
+
 NT_SHAPES = [(512, 768, 768), (1024, 2304, 768), (264, 520, 192), (2048, 50304, 768), (256, 256, 64),
              (1000, 1288, 640), (8200, 768, 3072), (257, 264, 64), (4096, 768, 4608)]
 
@@ -55,15 +64,14 @@ def test_nt4_elementwise(kernels, M, N, K):
     check(y, ref, absab, name="plain")
     yb = gemm.nt(x, w, bias=b, out=nanbuf(M, N))
     check(yb, ref + b.float(), absab + b.float().abs(), name="bias")
-    u, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N), out2=nanbuf(M, N))
-    assert torch.equal(u, yb)
-    check(g, F.gelu(u.float()), u.float().abs() + 1, rel=2 ** -7, name="gelu")
+    gp, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N, dtype=torch.float16),
+                    out2=nanbuf(M, N))
+    check_gelu_pair(gp, g, yb, "nt4")  # u = yb, the bias epilogue's bf16 output
     for st in (1, 2):  # nontemporal / plain epilogue stores: identical results
         assert torch.equal(gemm.nt(x, w, var=st, out=nanbuf(M, N)), y)
-    uu = torch.randn(M, N, device=DEV).to(BF)
+    uu = gelu_grad(torch.randn(M, N, device=DEV) * 2).half()
     d = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=uu, out=nanbuf(M, N))
-    gp = gelu_grad(uu.float())
-    check(d, y.float() * gp, (absab * gp).abs(), rel=2 ** -7, name="dgelu")
+    assert torch.equal(d, (y.float() * uu.float()).to(BF))  # bf16(bf16(acc) * gelu'(u)), bitwise
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 1288, 640), (8200, 768, 3072), (257, 264, 64), (2048, 50304, 768)])
@@ -90,13 +98,14 @@ def test_small_kernel(kernels, M, N, K):
     ref = x.float() @ w.float().t()
     absab = x.float().abs() @ w.float().abs().t()
     check(gemm.small(x, w, out=nanbuf(M, N)), ref, absab, name="small")
-    u, g = gemm.small(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N), out2=nanbuf(M, N))
-    check(u, ref + b.float(), absab + b.float().abs(), name="small bias")
-    check(g, F.gelu(u.float()), u.float().abs() + 1, rel=2 ** -7, name="small gelu")
-    uu = torch.randn(M, N, device=DEV).to(BF)
+    yb = gemm.small(x, w, bias=b, out=nanbuf(M, N))
+    check(yb, ref + b.float(), absab + b.float().abs(), name="small bias")
+    gp, g = gemm.small(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N, dtype=torch.float16), out2=nanbuf(M, N))
+    check_gelu_pair(gp, g, yb, "small")
+    uu = gelu_grad(torch.randn(M, N, device=DEV) * 2).half()
     d = gemm.small(x, w, epi=gemm.NT_EPI_DGELU, u=uu, out=nanbuf(M, N))
-    gp = gelu_grad(uu.float())
-    check(d, ref * gp, (absab * gp).abs() + ref.abs() * gp.abs() * 2 ** -8, rel=2 ** -7, name="small dgelu")
+    y = gemm.small(x, w, out=nanbuf(M, N))
+    assert torch.equal(d, (y.float() * uu.float()).to(BF))
 
 
 @pytest.mark.parametrize("T,N,K,splits", [(1024, 768, 768, None), (4096, 2304, 768, None), (512, 520, 200, 2),
