@@ -1346,7 +1346,7 @@ __device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, cons
 #define NSA_DKDV_NS 4  // LDS ring slots of the v2 dK/dV kernel (NS - 1 slices in flight)
 #endif
 
-template <int NKB, int NW, bool DROP, bool PAIR = false>
+template <int NKB, int NW, bool DROP, int G = 1>
 __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
     const float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B, int T, int H, float scale,
@@ -1355,7 +1355,8 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   constexpr int KPW = 32 * NKB;       // keys per wave
   constexpr int KWG = KPW * NW;       // keys per workgroup
   constexpr int SLOT = V2Geo<NW>::SLOT;
-  constexpr int NS = NSA_DKDV_NS, LA = NS - 1;
+  // G > 1: G slices per barrier in a 2G-slot ring (G computed while the next G land)
+  constexpr int NS = G > 1 ? 2 * G : NSA_DKDV_NS, LA = NS - 1;
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int C = H * D;
   const int64_t row_stride = 3 * (int64_t)C;
@@ -1400,7 +1401,7 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
     glds4(csrc + s * 32, sb + (uint32_t)(2 * V2_QT + w * 256));
   };
 
-  for (int j = 0; j < (PAIR ? 2 : LA) && j < n_mine; ++j) issue(s_first + j, j);
+  for (int j = 0; j < (G > 1 ? G : LA) && j < n_mine; ++j) issue(s_first + j, j);
 
   // K^T / V^T fragments (B operands of S = Q·K^T, dP = dO·V^T): K[key][16ks + 8h ..]
   bf16x8 kf[NKB][4], vf[NKB][4];
@@ -1462,16 +1463,17 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
   // iterations in all: same barrier count.
   const int j_diag = min(NKB * w, n_mine);
   const int j_full = min(NKB * w + NKB, n_mine);
-  if constexpr (PAIR && NS == 4) {
-    // two slices per barrier: pair (j, j + 1) runs while slices j + 2, j + 3 fly into the
-    // slots of j - 2, j - 1 (freed by the barrier that opens the pair)
-    for (int j = 0; j < n_mine; j += 2) {
+  if constexpr (G > 1) {
+    // G slices per barrier: group (j .. j + G - 1) runs while slices j + G .. j + 2G - 1 fly
+    // into the slots of the previous group (freed by the barrier that opens this one)
+    for (int j = 0; j < n_mine; j += G) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (j + 2 < n_mine) issue(s_first + j + 2, (j + 2) % NS);
-      if (j + 3 < n_mine) issue(s_first + j + 3, (j + 3) % NS);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < G; ++u)
+        if (j + G + u < n_mine) issue(s_first + j + G + u, (j + G + u) % NS);
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
         const int jj = j + u;
         if (jj >= j_full) {
           if (jj < n_mine) slice_full(jj);
@@ -1838,8 +1840,9 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   const int n_kb = (T + 127) / 128;
   // two query slices per barrier (v3, default): B120 T1024 H12 whole backward 1151 vs 1181 us
   // (profiles/r4_attn_ab_pair.log; the same change in the dQ kernel measured 1152)
+  // (three slices per barrier in a 6-slot ring measured 1171 vs 1141 us: profiles/r4_attn_ab_dkdv_g3.log)
   if (flash_config().bwd == BWD_V3 && !th)
-    flash_bwd_dkdv2_kernel<1, 4, false, true><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
+    flash_bwd_dkdv2_kernel<1, 4, false, 2><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                                           nls, nd, (bf16_t*)dqkv, B, T, H, scale,
                                                                           scale * kLog2e, th, dscale, seed, order);
   else if (th)
