@@ -140,7 +140,8 @@ def test_gelu(kernels, n):
 
 
 # --------------------------------------------------------------- embedding
-@pytest.mark.parametrize("B,T,V,C", [(4, 128, 1000, 768), (3, 77, 65, 384)])
+@pytest.mark.parametrize("B,T,V,C", [(4, 128, 1000, 768), (3, 77, 65, 384),
+                                     (8, 1024, 50304, 768), (4, 1024, 65, 384)])  # >= 4096 tokens: sorted backward
 def test_embedding(kernels, B, T, V, C):
     from nanosandbox_amd import ops
 
