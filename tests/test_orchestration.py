@@ -3,6 +3,7 @@ and a local emulation of the multi-Pod topology."""
 
 import glob
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -126,8 +127,10 @@ def test_elastic_restart_resumes_through_entrypoint(tmp_path):
     digests = {}
     for line in log.splitlines():
         if "param digest rank" in line:
+            # two ranks share the pipe: another rank's output can follow on the same line
+            # ("... 9iter 7: loss ..."), so take only the leading digits of the count
             parts = line.split("param digest rank ")[1].split()
-            digests[int(parts[0].rstrip(":"))] = (parts[1], int(parts[3]))
+            digests[int(parts[0].rstrip(":"))] = (parts[1], int(re.match(r"\d+", parts[3]).group()))
     assert set(digests) == {0, 1}, log[-3000:]
     assert digests[0] == digests[1]  # identical replicas after the restart
     assert digests[0][1] == 9  # iterations 0..max_iters ran, the last one after the resume
