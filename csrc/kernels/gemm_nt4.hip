@@ -66,6 +66,18 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XDX = 4 };
 
+// GELU epilogue lookup table (built on the host by ops/gemm.py gelu_table with torch's exact-erf
+// GELU): entry i = gelu(u) as bf16 | gelu'(u) as fp16 << 16 for the bf16 u with bit pattern
+// (14208 + i % 2560) | (i >= 2560) << 15, i.e. every bf16 with 2^-16 <= |u| < 16.  The
+// epilogue stages it in LDS beside the operand buffers and looks each u up (one ds_read_b32
+// instead of an erf, an exp and a reciprocal); a row of 8 values per lane with any u outside
+// the table (zero, |u| < 2^-16, |u| >= 16, inf / NaN) takes the arithmetic path for the
+// whole wave.
+constexpr int Q_GTAB_LO = 14208, Q_GTAB_N = 2560, Q_GTAB_BYTES = 2 * Q_GTAB_N * 4;
+#ifndef NSA_NT4_GTAB
+#define NSA_NT4_GTAB 1  // 0 (A/B builds only): the arithmetic GELU for every row
+#endif
+
 // pieces a K-tile has issued when it waits for the previous K-tile's
 constexpr int Q_D0 = 15 * NSA_NT4_ER + 4;  // slot of the first piece
 constexpr int Q_ISS = (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 < 16 ? (NSA_NT4_VMS - Q_D0) / NSA_NT4_DS + 1 : 16;
@@ -84,7 +96,7 @@ struct Nt4Args {
   const bf16_t* B;
   bf16_t* C;
   bf16_t* C2;
-  const bf16_t* U;     // DGELU: the pre-activation u
+  const bf16_t* U;     // DGELU: gelu'(u) (fp16); GELU: the 5120-entry lookup table (see Q_GTAB)
   const bf16_t* bias;  // BIAS: bias[N] added before the store (and before GELU)
   // fused cross-entropy (see nsa_gemm_nt4_xent / _xdx below)
   const float* rowf;   // XENT: per-row shift c (the target logit); XDX: per-row pairs {g / S, g or 0}
@@ -279,7 +291,7 @@ __device__ __forceinline__ float q_rowsum16(float v) {
 //       i.e. (softmax - onehot) · W without a dlogits tensor (ignored rows: 1/S = 0, no W row).
 template <int EPI, bool NT, bool BIAS, bool NOSTORE = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
-                                           int lane) {
+                                           int lane, const char* tab) {
   int m0, n0, mlo, nlo;
   q_tile_coords(g, seq, m0, n0, mlo, nlo);
   const bool full = (m0 == mlo) & (n0 == nlo);
@@ -389,12 +401,33 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           // u = w (bf16, as the reference's autocast c_fc output): C <- gelu'(u) as fp16 (the
           // backward's only use of u, so its GELU' epilogue is one multiply), C2 <- gelu(u)
           uint32_t gg[4], gp[4];
+          uint32_t ia[4], ib[4];
+          bool oob = false;
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            nsa_f32x2 gv, dv;
-            nsa_gelu_and_grad2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)}, gv, dv);
-            gg[h] = q_pk(gv.x, gv.y);
-            gp[h] = nsa_pk_f16(dv.x, dv.y);
+            const uint32_t b = w[h];
+            const uint32_t t0 = (b & 0x7fffu) - (uint32_t)Q_GTAB_LO, t1 = ((b >> 16) & 0x7fffu) - (uint32_t)Q_GTAB_LO;
+            oob |= (t0 >= (uint32_t)Q_GTAB_N) | (t1 >= (uint32_t)Q_GTAB_N);
+            ia[h] = 4u * (t0 + ((b >> 15) & 1u) * (uint32_t)Q_GTAB_N);
+            ib[h] = 4u * (t1 + (b >> 31) * (uint32_t)Q_GTAB_N);
+          }
+          if (NSA_NT4_GTAB && __builtin_amdgcn_ballot_w64(oob) == 0) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const uint32_t ea = *reinterpret_cast<const uint32_t*>(tab + ia[h]);
+              const uint32_t eb = *reinterpret_cast<const uint32_t*>(tab + ib[h]);
+              gg[h] = __builtin_amdgcn_perm(eb, ea, 0x05040100u);  // the two gelu(u) halves
+              gp[h] = __builtin_amdgcn_perm(eb, ea, 0x07060302u);  // the two gelu'(u) halves
+            }
+          } else {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              nsa_f32x2 gv, dv;
+              nsa_gelu_and_grad2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)}, gv,
+                                 dv);
+              gg[h] = q_pk(gv.x, gv.y);
+              gp[h] = nsa_pk_f16(dv.x, dv.y);
+            }
           }
           if constexpr (NOSTORE) {
             asm volatile("" ::"v"(gp[0]), "v"(gp[1]), "v"(gp[2]), "v"(gp[3]), "v"(gg[0]), "v"(gg[1]), "v"(gg[2]),
@@ -433,7 +466,7 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 // arithmetic without its stores
 template <int EPI, bool NT, int PROBE, bool BIAS = false>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
-  __shared__ __attribute__((aligned(16))) char smem[Q_SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[Q_SMEM + (EPI == Q_EPI_GELU ? Q_GTAB_BYTES : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -449,6 +482,11 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + v / 8;
   }
   if (v >= g.tiles) return;
+  if constexpr (EPI == Q_EPI_GELU) {  // the GELU table into LDS (before any operand DMA is in flight)
+    const uint4* src = reinterpret_cast<const uint4*>(g.U);
+    uint4* dst = reinterpret_cast<uint4*>(smem + Q_SMEM);
+    for (int k = threadIdx.x; k < Q_GTAB_BYTES / 16; k += Q_THR) dst[k] = src[k];
+  }
 
   // ---- DMA geometry.  Wave w copies pieces P = 8 w + p (p = 0..7) of each image: image rows
   // 8 P + i, i = lane >> 3, physical 16-B chunk lane & 7, which holds logical chunk
@@ -594,7 +632,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT, BIAS, PROBE == 5>(g, acc, seq, wm, wn, lane);
+      q_epilogue<EPI, NT, BIAS, PROBE == 5>(g, acc, seq, wm, wn, lane, smem + Q_SMEM);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -684,7 +722,8 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   a.ldb = ldb;
   a.ldc = ldc;
   if (nt4_check(a, grid) != hipSuccess) return hipErrorInvalidValue;
-  if ((epi == Q_EPI_GELU && !C2) || (epi == Q_EPI_DGELU && (!U || bias)) || (bias && (uintptr_t)bias % 16))
+  if ((epi == Q_EPI_GELU && (!C2 || !U || (uintptr_t)U % 16)) || (epi == Q_EPI_DGELU && (!U || bias)) ||
+      (bias && (uintptr_t)bias % 16))
     return hipErrorInvalidValue;
   nt4_geometry(a, gmsel);
   const bool nt = nt4_store_nt(stp, (int64_t)M * N * 2 * (epi == Q_EPI_GELU ? 2 : 1));

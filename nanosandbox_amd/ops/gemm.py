@@ -81,6 +81,30 @@ def _out(M, N, device, out, dtype=BF16):
     return out
 
 
+_GTAB = {}
+GTAB_LO, GTAB_N = 14208, 2560  # csrc/kernels/gemm_nt4.hip Q_GTAB_*
+
+
+def gelu_table(device):
+    """The nt4 GELU epilogue's lookup table (cached per device): for every bf16 u with
+    2^-16 <= |u| < 16 (bit pattern (GTAB_LO + i % GTAB_N) | (i >= GTAB_N) << 15), entry i =
+    bf16(gelu(u)) | fp16(gelu'(u)) << 16, both from torch's exact-erf GELU in fp32 -- the
+    values nanoGPT's autocast nn.GELU produces for that bf16 input."""
+    key = torch.device(device)
+    t = _GTAB.get(key)
+    if t is None:
+        i = torch.arange(2 * GTAB_N, dtype=torch.int32)
+        bits = (GTAB_LO + i % GTAB_N) | ((i >= GTAB_N).to(torch.int32) << 15)
+        u = (bits << 16).view(torch.float32).to(device)  # the bf16 values, exactly, in fp32
+        g = torch.nn.functional.gelu(u).to(torch.bfloat16).view(torch.int16).to(torch.int32) & 0xFFFF
+        cdf = 0.5 * (1.0 + torch.erf(u * 0.7071067811865476))
+        gp = (cdf + u * torch.exp(-0.5 * u * u) * 0.3989422804014327).to(torch.float16)
+        gp = gp.view(torch.int16).to(torch.int32) & 0xFFFF
+        t = (g | (gp << 16)).contiguous()
+        _GTAB[key] = t
+    return t
+
+
 def _check_gp(u):
     _check(u, "u")
     if u.dtype != torch.float16:
@@ -106,6 +130,8 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, g
     c2 = (_out(M, N, a.device, out2)) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
         _check_gp(u)
+    if epi == NT_EPI_GELU:
+        u = gelu_table(a.device)  # rides in the U slot
     _lib.call("nsa_gemm_nt4", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
               b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
               grid or num_cus(a.device), _lib.stream())

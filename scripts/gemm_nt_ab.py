@@ -63,6 +63,8 @@ def main():
         N_ = w.shape[0]
         c = torch.empty(M_, N_, device=x.device, dtype=torch.float16 if epi == gemm.NT_EPI_GELU else torch.bfloat16)
         c2 = torch.empty(M_, N_, device=x.device, dtype=torch.bfloat16) if epi == gemm.NT_EPI_GELU else None
+        if epi == gemm.NT_EPI_GELU:
+            u = gemm.gelu_table(x.device)
         err = alt(epi | (gemm.NT_VAR << 12), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c),
                   c.stride(0), _lib.ptr(c2), _lib.ptr(u), None, M_, N_, K_, gemm.num_cus(x.device), _lib.stream())
         assert err == 0, err
@@ -110,8 +112,14 @@ def main():
                 _lib.call("nsa_gelu_fwd", _lib.ptr(uu), _lib.ptr(gg), uu.numel(), _lib.stream())
             cands["torch_matmul+gelu"] = split
             cands["nt4_gelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU)
+            if a.probe:  # the GELU epilogue without its stores / without any epilogue
+                cands["nt4_gelu_nostore"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU, probe=5)
+                cands["nt4_gelu_noepi"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_GELU, probe=4)
             if alt is not None:
                 cands["nt4_alt_gelu"] = lambda: nt_alt(x, w, epi=gemm.NT_EPI_GELU)
+                gp2, g2 = nt_alt(x, w, epi=gemm.NT_EPI_GELU)
+                print(json.dumps({"check": name + "/gelu_vs_alt", "g_ulp_diff_frac": (g2 != g).float().mean().item(),
+                                  "gp_maxabs": (gp2.float() - gp.float()).abs().max().item()}), flush=True)
         if a.epi and name == "mlp.c_proj.dx":
             u = uni(M, N, scale=3.0)
             uf = u.float()
@@ -127,6 +135,8 @@ def main():
                 _lib.call("nsa_gelu_bwd", _lib.ptr(dg), _lib.ptr(u), _lib.ptr(du), du.numel(), _lib.stream())
             cands["torch_matmul+dgelu"] = split2
             cands["nt4_dgelu"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=gp)
+            if a.probe:
+                cands["nt4_dgelu_nostore"] = lambda: gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=gp, probe=5)
             if alt is not None:
                 cands["nt4_alt_dgelu"] = lambda: nt_alt(x, w, epi=gemm.NT_EPI_DGELU, u=gp)
         for fn in cands.values():
