@@ -51,15 +51,27 @@ def batch_plan(world: int, micro_batch: int = 0) -> tuple[int, int]:
     return micro_batch, per_rank_seqs // micro_batch * world
 
 
-def rccl_summary(report, sweep) -> dict | None:
-    """The JSON record's RCCL block (None on one GPU)."""
-    if not report and not sweep:
+def rccl_summary(report, sweep, reducer=None, exposed=None, early=None) -> dict | None:
+    """The JSON record's RCCL block (None on one GPU).
+
+    With the flat reducer it also carries the bucket layout (sizes, which parameters share
+    the late embedding tail) and, per timed step, the exposed communication: the time the
+    compute stream waited in ``reducer.finish()`` after the last backward kernel
+    (``exposed_allreduce_ms``, max over ranks), plus how many buckets were launched while
+    the backward was still running."""
+    if not report and not sweep and reducer is None:
         return None
     report = report or {}
-    return {"backend": report.get("backend"), "preset": report.get("preset"),
-            "transport_by_rank": {str(k): v for k, v in (report.get("transport") or {}).items()},
-            "allreduce_64MiB_ms": report.get("allreduce_ms"), "allreduce_64MiB_busbw_GBps": report.get("busbw_GBps"),
-            "sweep": list(sweep or [])}
+    out = {"backend": report.get("backend"), "preset": report.get("preset"),
+           "transport_by_rank": {str(k): v for k, v in (report.get("transport") or {}).items()},
+           "allreduce_64MiB_ms": report.get("allreduce_ms"), "allreduce_64MiB_busbw_GBps": report.get("busbw_GBps"),
+           "sweep": list(sweep or [])}
+    if reducer is not None:
+        out["buckets"] = reducer.layout()
+        out["exposed_allreduce_ms"] = round(sum(exposed) / len(exposed), 3) if exposed else None
+        out["exposed_allreduce_ms_per_step"] = [round(v, 3) for v in (exposed or [])]
+        out["buckets_launched_in_backward"] = list(early or [])
+    return out
 
 
 def main():
@@ -162,6 +174,9 @@ def main():
         sync()
         if dist.is_initialized():
             dist.barrier()
+        reducer = getattr(tr, "reducer", None)
+        if reducer is not None:
+            reducer.exposed_ms(clear=True)  # drop the warm-up steps (the first one has no overlap)
         prof = None
         if args.profile and tr.info.rank == 0:
             from torch.profiler import ProfilerActivity, profile, schedule, tensorboard_trace_handler
@@ -187,6 +202,14 @@ def main():
         if dist.is_initialized():
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         dt = float(dt_t.item())
+        exposed, early = None, None
+        if reducer is not None:
+            early = list(reducer.launched_in_backward)
+            exposed = reducer.exposed_ms(clear=True)
+            ex_t = torch.tensor(exposed or [0.0], device=tr.device, dtype=torch.float64)
+            if dist.is_initialized():
+                dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)
+            exposed = [float(v) for v in ex_t.tolist()] if exposed else []
         lossf = float(loss.item()) * tr.gas
         if prof is not None:
             prof.stop()
@@ -230,7 +253,7 @@ def main():
             "gemm_kernels": gemm_kernels,
             # N > 1: RCCL's transport per rank (from its INIT log) + the 64 MiB all-reduce, and
             # the bus bandwidth by message size (docs/rccl.md bucket sizing)
-            "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep),
+            "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep, reducer, exposed, early),
         }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -12,18 +12,37 @@
 //   p *= 1 - lr*wd ; m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
 //   p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
 // where g = grad * coef and coef = grad_scale * min(1, max_norm/(norm+1e-6)).
+//
+// fp16 training (--dtype=float16) passes the dynamic loss scale's device
+// state `ls` (optim/loss_scale.py LS_* slots) to all three kernels, so GradScaler's
+// unscale / inf check / skip / scale update happen on the device with no host sync:
+//   sumsq   : squares of grad * pre / ls[SCALE] (the UNSCALED gradient: finite scaled
+//             gradients cannot overflow the sum) + a separate count of non-finite elements
+//   clip    : found_inf = any non-finite element or a non-finite sum; coef = 0 then, the
+//             scale backs off / grows by GradScaler's policy, the device step counter
+//             advances only on a good step
+//   adamw   : returns at once on a found_inf step; bias corrections from the device step
 #include "common.h"
 
 namespace {
 
 constexpr int kBlock = 256;
+// dynamic loss-scale state slots (float32), mirrored in optim/loss_scale.py
+enum { LS_SCALE = 0, LS_TRACKER = 1, LS_FOUND = 2, LS_SKIPPED = 3, LS_STEP = 4 };
 
 __global__ __launch_bounds__(kBlock) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       bf16_t* __restrict__ pb, const uint8_t* __restrict__ wd_mask,
                                                       int64_t n4, float lr, float b1, float b2, float eps, float wd,
                                                       float step_size, float inv_bc2_sqrt,
-                                                      const float* __restrict__ coef_ptr) {
+                                                      const float* __restrict__ coef_ptr,
+                                                      const float* __restrict__ ls) {
+  if (ls != nullptr) {
+    if (ls[LS_FOUND] != 0.0f) return;  // GradScaler: skip the step (wave-uniform)
+    const float t = ls[LS_STEP];        // good steps so far, this one included
+    step_size = lr / (1.0f - powf(b1, t));
+    inv_bc2_sqrt = 1.0f / sqrtf(1.0f - powf(b2, t));
+  }
   const float coef = coef_ptr[0];
   const float decay = 1.0f - lr * wd;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
@@ -56,46 +75,93 @@ __global__ __launch_bounds__(kBlock) void adamw_kernel(float* __restrict__ p, co
   }
 }
 
+// partial[b] = sum of (g * pre)^2 over block b's elements; with a loss scale, also
+// partial[nblocks + b] = the number of non-finite elements (pre is then divided by the scale)
 __global__ __launch_bounds__(kBlock) void sumsq_partial_kernel(const float* __restrict__ g, int64_t n4,
-                                                              float* __restrict__ partial) {
+                                                              float* __restrict__ partial, float pre,
+                                                              const float* __restrict__ ls) {
+  if (ls != nullptr) pre /= ls[LS_SCALE];
   float acc = 0.0f;
+  float bad = 0.0f;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
     const float4 x = reinterpret_cast<const float4*>(g)[i];
-    acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+    const float a = x.x * pre, b = x.y * pre, c = x.z * pre, d = x.w * pre;
+    acc += a * a + b * b + c * c + d * d;
+    if (ls != nullptr)
+      bad += (float)(!__builtin_isfinite(x.x)) + (float)(!__builtin_isfinite(x.y)) +
+             (float)(!__builtin_isfinite(x.z)) + (float)(!__builtin_isfinite(x.w));
   }
   acc = wave_sum(acc);
-  __shared__ float red[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if (ls != nullptr) bad = wave_sum(bad);
+  __shared__ float red[2][kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = acc;
+    red[1][threadIdx.x >> 6] = bad;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float s = 0.0f;
+    float s = 0.0f, nb = 0.0f;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+    for (int w = 0; w < kBlock / 64; ++w) {
+      s += red[0][w];
+      nb += red[1][w];
+    }
     partial[blockIdx.x] = s;
+    if (ls != nullptr) partial[gridDim.x + blockIdx.x] = nb;
   }
 }
 
+// norm = sqrt(sum of the partials) (already multiplied by the gradient scale in the
+// sumsq pass); coef = scale * min(1, max_norm / (norm + 1e-6)), scale divided by the loss
+// scale when one is given; then the loss-scale update (GradScaler's policy)
 __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict__ partial, int nparts, float scale,
                                                         float max_norm, float* __restrict__ norm_out,
-                                                        float* __restrict__ coef_out) {
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += 1024) acc += (double)partial[i];
-  __shared__ double red[1024];
-  red[threadIdx.x] = acc;
+                                                        float* __restrict__ coef_out, float* __restrict__ ls,
+                                                        float growth, float backoff, float interval) {
+  double acc = 0.0, bad = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 1024) {
+    acc += (double)partial[i];
+    if (ls != nullptr) bad += (double)partial[nparts + i];
+  }
+  __shared__ double red[2][1024];
+  red[0][threadIdx.x] = acc;
+  red[1][threadIdx.x] = bad;
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float norm = (float)sqrt(red[0]) * scale;
-    norm_out[0] = norm;
+    float norm = (float)sqrt(red[0][0]);
     float c = 1.0f;
     if (max_norm > 0.0f) {
       c = max_norm / (norm + 1e-6f);
       if (c > 1.0f) c = 1.0f;
     }
-    coef_out[0] = scale * c;
+    if (ls == nullptr) {
+      norm_out[0] = norm;
+      coef_out[0] = scale * c;
+      return;
+    }
+    const bool found = red[1][0] > 0.0 || !__builtin_isfinite(norm);
+    norm_out[0] = found ? __builtin_inff() : norm;
+    coef_out[0] = found ? 0.0f : scale / ls[LS_SCALE] * c;
+    ls[LS_FOUND] = found ? 1.0f : 0.0f;
+    if (found) {
+      ls[LS_SCALE] *= backoff;
+      ls[LS_TRACKER] = 0.0f;
+      ls[LS_SKIPPED] += 1.0f;
+    } else {
+      ls[LS_STEP] += 1.0f;
+      ls[LS_TRACKER] += 1.0f;
+      if (ls[LS_TRACKER] >= interval) {
+        ls[LS_SCALE] *= growth;
+        ls[LS_TRACKER] = 0.0f;
+      }
+    }
   }
 }
 
@@ -164,27 +230,30 @@ NSA_API hipError_t nsa_colsum_bf16_partial(const void* dy, int ld, int rows, int
 
 NSA_API hipError_t nsa_adamw_step(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask,
                                   int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,
-                                  float bc2_sqrt, const void* coef, hipStream_t s) {
+                                  float bc2_sqrt, const void* coef, const void* ls, hipStream_t s) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   int64_t grid = (n4 + kBlock - 1) / kBlock;
   if (grid > 4096) grid = 4096;
   adamw_kernel<<<(int)grid, kBlock, 0, s>>>((float*)p, (const float*)g, (float*)m, (float*)v, (bf16_t*)p_bf16,
                                             (const uint8_t*)wd_mask, n4, lr, beta1, beta2, eps, wd, lr / bc1,
-                                            1.0f / bc2_sqrt, (const float*)coef);
+                                            1.0f / bc2_sqrt, (const float*)coef, (const float*)ls);
   NSA_LAUNCH_CHECK();
 }
 
-NSA_API hipError_t nsa_sumsq_partial(const void* g, int64_t n, void* partial, int nblocks, hipStream_t s) {
+// partial holds nblocks floats, 2 * nblocks with a loss scale (ls != null)
+NSA_API hipError_t nsa_sumsq_partial(const void* g, int64_t n, void* partial, int nblocks, float pre, const void* ls,
+                                     hipStream_t s) {
   if (n % 4 != 0) return hipErrorInvalidValue;
-  sumsq_partial_kernel<<<nblocks, kBlock, 0, s>>>((const float*)g, n / 4, (float*)partial);
+  sumsq_partial_kernel<<<nblocks, kBlock, 0, s>>>((const float*)g, n / 4, (float*)partial, pre, (const float*)ls);
   NSA_LAUNCH_CHECK();
 }
 
 NSA_API hipError_t nsa_clip_coef(const void* partial, int nparts, float scale, float max_norm, void* norm_out,
-                                 void* coef_out, hipStream_t s) {
+                                 void* coef_out, void* ls, float growth, float backoff, float interval,
+                                 hipStream_t s) {
   clip_coef_kernel<<<1, 1024, 0, s>>>((const float*)partial, nparts, scale, max_norm, (float*)norm_out,
-                                      (float*)coef_out);
+                                      (float*)coef_out, (float*)ls, growth, backoff, interval);
   NSA_LAUNCH_CHECK();
 }
 

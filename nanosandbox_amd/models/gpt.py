@@ -142,6 +142,11 @@ class GPT(nn.Module):
         pad = ops.lm_head_rows(config.vocab_size)
         if pad != config.vocab_size:
             self.lm_head.weight._nsa_pad_rows = pad
+        # wte and wpe receive their last gradient contribution from the embedding backward,
+        # the final kernel of the backward pass: the flat store gives them a tail bucket of
+        # their own so no block weight waits behind them for its all-reduce
+        self.transformer.wte.weight._nsa_late_grad = True
+        self.transformer.wpe.weight._nsa_late_grad = True
 
         # init all weights
         self.apply(self._init_weights)

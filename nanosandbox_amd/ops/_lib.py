@@ -58,9 +58,10 @@ _SIGNATURES = {
     "nsa_xent_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_scale_rows_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_adamw_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                       c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p],
-    "nsa_sumsq_partial": [c_void_p, c_int64, c_void_p, c_int, c_void_p],
-    "nsa_clip_coef": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p],
+                       c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p],
+    "nsa_sumsq_partial": [c_void_p, c_int64, c_void_p, c_int, c_float, c_void_p, c_void_p],
+    "nsa_clip_coef": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
+                      c_void_p],
     "nsa_cast_f32_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "nsa_flash_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_flash_set_variant": [c_int, c_int, c_int],

@@ -930,11 +930,24 @@ def _lm_weight(w):
     cp = getattr(w, "compute_padded", None)
     if cp is not None and cp.dtype == BF16:
         return cp, getattr(w, "main_grad_padded", None)
-    wc = compute_weight(w, BF16)
     if Vp == V:
-        return wc, getattr(w, "main_grad", None)
-    wp = torch.zeros(Vp, C, device=w.device, dtype=BF16)
-    wp[:V] = wc
+        return compute_weight(w, BF16), getattr(w, "main_grad", None)
+    # no flat store (sample / eval scripts): the padded operand is cached on the weight for
+    # its current contents (generation, version, storage), so a token-by-token generate()
+    # does not allocate and copy the whole [Vpad, C] table per token; never cached while a
+    # HIP graph is being captured (the copy is then part of the graph)
+    capturing = w.is_cuda and torch.cuda.is_current_stream_capturing()
+    key = (_gd._weight_gen, w._version, w.data_ptr())
+    hit = getattr(w, "_nsa_lm_pad", None)
+    if not capturing and hit is not None and hit[0] == key:
+        return hit[1], None
+    wp = hit[1] if (hit is not None and not capturing) else torch.zeros(Vp, C, device=w.device, dtype=BF16)
+    wp[:V] = compute_weight(w, BF16)
+    if not capturing:
+        try:
+            w._nsa_lm_pad = (key, wp)
+        except (AttributeError, RuntimeError):
+            pass
     return wp, None
 
 
@@ -992,6 +1005,7 @@ class LMHeadLossFn(torch.autograd.Function):
                 slots = 2 * (-(-Vp // _gemm.TILE))
                 part = torch.empty(slots, N, device=x.device, dtype=F32)
                 e = _gemm.nt_xent(x2, wp, crow, part, V)
+                _gd.record("lm_head_xent", N, Vp, C, "nt4/xent")
                 inv_s = torch.empty(N, device=x.device, dtype=F32)
                 nfix = torch.zeros(1, device=x.device, dtype=torch.int32)
                 fixlist = torch.empty(N, device=x.device, dtype=torch.int32)
@@ -1039,6 +1053,7 @@ class LMHeadLossFn(torch.autograd.Function):
             _lib.call("nsa_xent_bwd_prep", _lib.ptr(x2), C, _lib.ptr(wp), C, _lib.ptr(t32), _lib.ptr(inv_s),
                       _lib.ptr(g), _lib.ptr(coef), _lib.ptr(wrows), _lib.ptr(xs), N, C, _lib.stream())
             dx = _gemm.nt_xdx(e, _gd._wt(wp), wrows, coef)
+            _gd.record("lm_head_xdx", N, C, Vp, "nt4/xdx")
             ret = gwp is None
             gw = torch.zeros(Vp, C, device=x2.device, dtype=F32) if ret else gwp
             _gd.wgrad_acc(e, xs, gw)

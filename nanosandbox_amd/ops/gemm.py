@@ -235,7 +235,9 @@ def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False, gb32=None):
     if gb32 is not None:
         if not gb32.is_contiguous() or gb32.dtype != torch.float32 or gb32.numel() != N_out:
             raise ValueError("bias grad must be a contiguous fp32 [N_out] tensor")
-        if four and not (deterministic and splits > 1):
+        # not in deterministic mode at any split count: the fused kernel spreads each bias
+        # column's token sum over the column blocks, each adding its own fp32 atomic
+        if four and not deterministic:
             _lib.call("nsa_gemm_wgrad4b", EPI_ATOMIC, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
                       _lib.ptr(g32), K_in, _lib.ptr(gb32), N_out, K_in, T, splits, _lib.stream())
             return g32

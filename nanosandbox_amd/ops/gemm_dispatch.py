@@ -67,6 +67,13 @@ def kernels_used() -> dict:
     return dict(_used)
 
 
+def record(op: str, M: int, N: int, K: int, kernel: str) -> None:
+    """Record a GEMM that bypasses the rule's front-ends (the fused cross-entropy pair
+    ``gemm.nt_xent`` / ``nt_xdx``, always the four-wave kernel) so ``kernels_used`` lists
+    every GEMM of the step."""
+    _used.setdefault((op, M, N, K), kernel)
+
+
 def _nt(a, b, epi=_gemm.NT_EPI_BF16, u=None, bias=None, op="fwd"):
     M, K = a.shape
     N = b.shape[0]

@@ -133,20 +133,33 @@ class FlatParamStore:
                     s.param.grad = self.param_view(self.grad, s)
 
     def buckets(self, cap_bytes: int):
-        """Contiguous [start, end) element ranges of ``grad``, cut at parameter
-        boundaries once a bucket reaches ``cap_bytes`` (fp32)."""
+        """Contiguous [start, end) element ranges of ``grad``, cut at parameter boundaries
+        so that no bucket exceeds ``cap_bytes`` (fp32) unless it holds a single parameter
+        larger than the cap, or is the late tail below.  A bucket is
+        closed *before* the parameter that would push it past the cap, so with the 64 MiB
+        default the transformer blocks of GPT-2 124M go two per bucket (54 MiB) instead of
+        three (81 MiB, the round-4 rule that closed a bucket only after it passed the cap).
+        Parameters tagged ``_nsa_late_grad`` (wte, wpe: complete only after the embedding
+        backward, the last kernel of the step) never share a bucket with earlier ones; they
+        form one tail bucket (GPT-2 124M: 150 MiB, the one all-reduce that cannot overlap
+        the backward)."""
         out = []
         start = 0
         size = 0
         members = []
+        late = False
         for s in self.slots:
-            members.append(s)
-            size += s.padded * 4
-            if size >= cap_bytes:
-                out.append((start, s.offset + s.padded, members))
-                start = s.offset + s.padded
+            nbytes = s.padded * 4
+            is_late = bool(getattr(s.param, "_nsa_late_grad", False))
+            # the late parameters all become final in the same kernel: one collective for them
+            if members and (is_late != late or (size + nbytes > cap_bytes and not is_late)):
+                out.append((start, s.offset, members))
+                start = s.offset
                 size = 0
                 members = []
+            members.append(s)
+            size += nbytes
+            late = is_late
         if members:
             out.append((start, self.numel, members))
         return out

@@ -12,7 +12,9 @@ One optimizer step is three kernels regardless of the parameter count:
    writes the bf16 compute shadow.  ~30 B/param, HBM-bound.
 
 Nothing is read back to the host (lr/betas/bias corrections are host scalars
-computed from the step counter), so the step is graph-capturable.
+computed from the step counter), so the step is graph-capturable.  With an fp16 dynamic
+loss scale attached (``attach_loss_scale``) the three kernels also run GradScaler's
+unscale / inf check / skip / scale update on the device (``optim/loss_scale.py``).
 
 Math and state layout match ``torch.optim.AdamW`` (``decoupled_weight_decay``):
 ``state_dict()`` / ``load_state_dict()`` speak torch's format — per-parameter
@@ -58,8 +60,15 @@ class FusedAdamW:
         self.grad_scale = 1.0  # set by the reducer (1/world_size when it sums)
         self._coef = torch.ones(1, dtype=torch.float32, device=dev)
         self._norm = torch.zeros(1, dtype=torch.float32, device=dev)
-        self._partial = torch.zeros(_NORM_BLOCKS, dtype=torch.float32, device=dev)
+        self._partial = torch.zeros(2 * _NORM_BLOCKS, dtype=torch.float32, device=dev)
         self._clip_pending = False
+        self.loss_scale = None  # DynamicLossScale (fp16), see attach_loss_scale
+
+    def attach_loss_scale(self, ls) -> None:
+        """Run the fp16 dynamic loss scale's policy inside the optimizer kernels: the
+        gradient multiplier divides by the device scale, a step whose gradients hold an
+        inf / NaN is skipped on the device, and AdamW's bias correction counts good steps."""
+        self.loss_scale = ls
 
     # -------------------------------------------------------------- helpers
     @property
@@ -81,12 +90,25 @@ class FusedAdamW:
 
         Returns the pre-clip total norm as a 1-element device tensor (no sync)."""
         g = self.store.grad
+        ls = self.loss_scale
         if self._is_gpu:
             from ..ops import _lib
+            lsp = _lib.ptr(ls.state) if ls is not None else None
             _lib.call("nsa_sumsq_partial", _lib.ptr(g), g.numel(), _lib.ptr(self._partial), _NORM_BLOCKS,
-                      _lib.stream())
+                      float(self.grad_scale), lsp, _lib.stream())
             _lib.call("nsa_clip_coef", _lib.ptr(self._partial), _NORM_BLOCKS, float(self.grad_scale),
-                      float(max_norm), _lib.ptr(self._norm), _lib.ptr(self._coef), _lib.stream())
+                      float(max_norm), _lib.ptr(self._norm), _lib.ptr(self._coef), lsp,
+                      ls.growth_factor if ls else 0.0, ls.backoff_factor if ls else 0.0,
+                      float(ls.growth_interval) if ls else 0.0, _lib.stream())
+        elif ls is not None:  # host reference of the kernels' loss-scale path
+            from .loss_scale import LS_SCALE
+            gs = float(self.grad_scale) / float(ls.state[LS_SCALE])
+            found = not bool(torch.isfinite(g).all())
+            norm = float("inf") if found else float((g.double() * gs).pow(2).sum().sqrt())
+            self._norm.fill_(norm)
+            c = min(1.0, max_norm / (norm + 1e-6)) if (max_norm > 0 and not found) else 1.0
+            self._coef.fill_(0.0 if found else gs * c)
+            ls.update(found)
         else:
             norm = g.double().pow(2).sum().sqrt().float() * self.grad_scale
             self._norm.copy_(norm.view(1))
@@ -98,9 +120,15 @@ class FusedAdamW:
     # ----------------------------------------------------------------- step
     @torch.no_grad()
     def step(self):
+        ls = self.loss_scale
         if not self._clip_pending:
-            self._coef.fill_(self.grad_scale)
+            if ls is not None:  # the inf check / unscale / scale update still has to run
+                self.clip_grad_norm_(0.0)
+            else:
+                self._coef.fill_(self.grad_scale)
         self._clip_pending = False
+        if ls is not None and not self._is_gpu and ls.found_inf:
+            return  # host reference: GradScaler skips the step
         self.step_count += 1
         lr, (beta1, beta2), eps, wd = self._hyper()
         t = self.step_count
@@ -113,8 +141,12 @@ class FusedAdamW:
             _lib.call("nsa_adamw_step", _lib.ptr(st.master), _lib.ptr(st.grad), _lib.ptr(self.exp_avg),
                       _lib.ptr(self.exp_avg_sq), _lib.ptr(st.compute), _lib.ptr(st.wd_mask), st.numel,
                       float(lr), float(beta1), float(beta2), float(eps), float(wd), float(bc1), float(bc2_sqrt),
-                      _lib.ptr(self._coef), _lib.stream())
+                      _lib.ptr(self._coef), _lib.ptr(ls.state) if ls is not None else None, _lib.stream())
             return
+        if ls is not None:  # bias correction counts the good steps only
+            t = ls.good_steps
+            bc1 = 1.0 - beta1 ** t
+            bc2_sqrt = math.sqrt(1.0 - beta2 ** t)
         # CPU reference (same math as the kernel, torch.optim.AdamW semantics)
         p, m, v = st.master, self.exp_avg, self.exp_avg_sq
         g = st.grad * self._coef
@@ -140,10 +172,11 @@ class FusedAdamW:
     def state_dict(self):
         st = self.store
         state = {}
+        step = self.loss_scale.good_steps if self.loss_scale is not None else self.step_count
         for i, p in enumerate(self._ordered_params()):
             s = st.slot_of(p)
             state[i] = {
-                "step": torch.tensor(float(self.step_count), dtype=torch.float32),
+                "step": torch.tensor(float(step), dtype=torch.float32),
                 "exp_avg": st.param_view(self.exp_avg, s).detach().clone(),
                 "exp_avg_sq": st.param_view(self.exp_avg_sq, s).detach().clone(),
             }
@@ -180,3 +213,6 @@ class FusedAdamW:
             steps.append(int(float(s_saved["step"])))
         if steps:
             self.step_count = max(steps)
+            if self.loss_scale is not None:
+                from .loss_scale import LS_STEP
+                self.loss_scale.state[LS_STEP] = float(self.step_count)

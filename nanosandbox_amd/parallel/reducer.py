@@ -20,7 +20,14 @@ backward-completion order (``FlatParamStore``), so a bucket is just a slice:
 * bucket size is chosen for xGMI: an MI355X has 7 point-to-point links of
   ~153 GB/s; a ring all-reduce is per-link bound, so buckets should be large
   enough that each RCCL call streams for tens of microseconds on every
-  channel (64 MiB default -> ~8 buckets for GPT-2 124M instead of DDP's 19).
+  channel.  The 64 MiB default gives GPT-2 124M five 63 MiB buckets, one 9 MiB
+  bucket and the 150 MiB wte + wpe tail (``FlatParamStore.buckets``), against
+  torch DDP's 19 buckets of 25 MiB.
+* the tail bucket (the embeddings, final only after the embedding backward) is the
+  one all-reduce that cannot overlap the backward.  ``finish()`` measures what is
+  exposed: HIP events on the compute stream before and after its waits give the
+  time the compute stream stood still for communication (``exposed_ms``, reported
+  by bench.py as ``rccl.exposed_allreduce_ms``).
 * optional bf16 compression (``grad_reduce_dtype='bfloat16'``) halves the
   bytes on the wire; the fp32 buffer is restored from the reduced bf16 copy.
 
@@ -30,6 +37,7 @@ flat fp32 master buffer.
 
 from __future__ import annotations
 
+import time
 
 import torch
 import torch.distributed as dist
@@ -38,17 +46,19 @@ from ..optim.flat import FlatParamStore
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "expected", "count", "work", "comm_buf")
+    __slots__ = ("index", "start", "end", "params", "names", "expected", "count", "work", "comm_buf", "early")
 
-    def __init__(self, index, start, end, params):
+    def __init__(self, index, start, end, params, names):
         self.index = index
         self.start = start
         self.end = end
         self.params = params
+        self.names = names
         self.expected = 0
         self.count = 0
         self.work = None
         self.comm_buf = None
+        self.early = False  # launched by a gradient hook, i.e. before the backward returned
 
 
 class FlatBucketReducer:
@@ -60,7 +70,7 @@ class FlatBucketReducer:
         self.world = dist.get_world_size(process_group)
         self.reduce_dtype = reduce_dtype
         cap = max(1, int(bucket_cap_mb * 1024 * 1024))
-        self.buckets = [_Bucket(i, s, e, [m.param for m in members])
+        self.buckets = [_Bucket(i, s, e, [m.param for m in members], [m.name for m in members])
                         for i, (s, e, members) in enumerate(store.buckets(cap))]
         self._bucket_of = {}
         for b in self.buckets:
@@ -70,8 +80,36 @@ class FlatBucketReducer:
         self.discovered = False
         self.armed = False
         self._next_launch = 0
+        self._in_finish = False
+        # per synchronised step: buckets launched during the backward, and the exposed
+        # communication (HIP event pairs on the compute stream, read lazily; host wall
+        # time on the CPU)
+        self.launched_in_backward: list[int] = []
+        self._exposed: list = []
         for s in store.slots:
             s.param._nsa_grad_hook = self._on_grad
+
+    def layout(self) -> list[dict]:
+        """Bucket layout for the bench record: size, parameter count, the first and last
+        parameter (backward-completion order), and whether it is the late embedding tail."""
+        return [{"index": b.index, "MiB": round((b.end - b.start) * 4 / 2 ** 20, 2), "n_params": len(b.params),
+                 "first": b.names[0], "last": b.names[-1],
+                 "late": any(getattr(p, "_nsa_late_grad", False) for p in b.params)} for b in self.buckets]
+
+    def exposed_ms(self, clear: bool = True) -> list[float]:
+        """Milliseconds per synchronised step between the end of the backward on the compute
+        stream and the point where every bucket's all-reduce had landed (synchronises)."""
+        out = []
+        for e in self._exposed:
+            if isinstance(e, tuple):
+                e[1].synchronize()
+                out.append(float(e[0].elapsed_time(e[1])))
+            else:
+                out.append(float(e))
+        if clear:
+            self._exposed = []
+            self.launched_in_backward = []
+        return out
 
     # --------------------------------------------------------------- setup
     @torch.no_grad()
@@ -87,6 +125,7 @@ class FlatBucketReducer:
         for b in self.buckets:
             b.count = 0
             b.work = None
+            b.early = False
         self._next_launch = 0
         if sync and not self.discovered:
             for k in self._contrib:
@@ -109,6 +148,7 @@ class FlatBucketReducer:
             if b.count < b.expected:
                 return
             self._launch(b)
+            b.early = not self._in_finish
             self._next_launch += 1
 
     def _launch(self, b: _Bucket):
@@ -124,13 +164,22 @@ class FlatBucketReducer:
         """Wait for every bucket of the synchronising micro-step (launching stragglers)."""
         if not self.armed:
             return
+        cuda = self.store.grad.is_cuda
+        if cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        else:
+            t0 = time.perf_counter()
+        self.launched_in_backward.append(sum(b.work is not None for b in self.buckets))
         if not self.discovered:
             for b in self.buckets:
                 b.expected = sum(self._contrib[id(p)] for p in b.params)
             self.discovered = True
         for b in self.buckets:
             b.count = max(b.count, b.expected)
+        self._in_finish = True
         self._launch_ready()
+        self._in_finish = False
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
@@ -138,6 +187,12 @@ class FlatBucketReducer:
                     self.store.grad[b.start:b.end].copy_(b.comm_buf)
                 b.work = None
                 b.comm_buf = None
+        if cuda:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._exposed.append((ev0, ev1))
+        else:
+            self._exposed.append((time.perf_counter() - t0) * 1000.0)
         self.armed = False
 
     @property

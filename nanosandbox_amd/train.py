@@ -77,7 +77,7 @@ class Trainer:
         self.scaler = None
         if self.compute_dtype == torch.float16:
             from .optim.loss_scale import DynamicLossScale
-            self.scaler = DynamicLossScale()
+            self.scaler = DynamicLossScale(device=self.device)
         if self.device_type == "cuda" and self.compute_dtype != torch.bfloat16 and self.master:
             print(f"dtype={c['dtype']}: torch reference ops (HIP kernels run bf16 only)"
                   + (", dynamic loss scale" if self.scaler else ""))
@@ -146,6 +146,8 @@ class Trainer:
                                     fused_grad=fused_grad)
         self.optimizer = model.configure_optimizers(c["weight_decay"], c["learning_rate"], (c["beta1"], c["beta2"]),
                                                     self.device_type, store=self.store)
+        if self.scaler is not None:
+            self.optimizer.attach_loss_scale(self.scaler)  # inf check / skip / update on the device
         if init_from == "resume" and checkpoint is not None:
             self.optimizer.load_state_dict(checkpoint["optimizer"])
         checkpoint = None  # free up memory
@@ -263,23 +265,14 @@ class Trainer:
             loss = loss / self.gas  # scale the loss to account for gradient accumulation
             # immediately async prefetch next batch while model is doing the forward pass on the GPU
             X, Y = self.batches.get_batch("train")
-            (loss * self.scaler.scale if self.scaler is not None else loss).backward()
+            # fp16: the loss times the device-resident scale (no host sync); the optimizer's
+            # kernels unscale, check for inf / NaN, skip and update the scale (loss_scale.py)
+            (loss * self.scaler.scale_t if self.scaler is not None else loss).backward()
         if self.reducer is not None:
             self.reducer.finish()
         norm = None
-        if self.scaler is not None:
-            # unscale by folding 1/scale into the optimizer's gradient multiplier
-            self.optimizer.grad_scale = self._grad_scale0 / self.scaler.scale
         if c["grad_clip"] != 0.0:
             norm = self.optimizer.clip_grad_norm_(c["grad_clip"])
-        if self.scaler is not None:
-            gn = norm if norm is not None else (self.store.grad.float().norm() * self.optimizer.grad_scale)
-            found_inf = not self.scaler.finite(gn.item())
-            self.scaler.update(found_inf)
-            if found_inf:  # GradScaler: skip the step, back the scale off
-                self.optimizer._clip_pending = False
-                self.optimizer.zero_grad(set_to_none=True)
-                return loss, norm, X, Y
         self.optimizer.step()
         self.optimizer.zero_grad(set_to_none=True)
         return loss, norm, X, Y
@@ -349,9 +342,11 @@ class Trainer:
         (shared storage: the PVC in the k8s topologies) records that it fired, and
         torchrun's ``TORCHELASTIC_RESTART_COUNT`` > 0 also suppresses it, so an elastic
         restart (``--max-restarts``) that auto-resumes from ``ckpt.pt`` runs through.  The
-        marker is keyed to the job (torchrun's ``TORCHELASTIC_RUN_ID``, else this process), so
-        a later job reusing the same out_dir still gets its fault."""
-        job = os.environ.get("TORCHELASTIC_RUN_ID") or f"pid{os.getpid()}"
+        marker is keyed to the job, so a later job reusing the same out_dir still gets its
+        fault: torchrun's ``TORCHELASTIC_RUN_ID`` when it names the job; under torchrun's
+        default ``--rdzv-id`` ("none", shared by every default launch) the elastic agent's pid
+        (the workers' parent, unchanged across that job's restarts); else this process."""
+        job = _fault_job_key()
         job = "".join(ch if ch.isalnum() or ch in "-_" else "_" for ch in job)
         marker = os.path.join(self.cfg["out_dir"], f".fault_injected_rank{self.info.rank}.{job}")
         if os.path.exists(marker) or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) > 0:
@@ -369,6 +364,16 @@ class Trainer:
                     record_shapes=True, profile_memory=True)
         p.start()
         return p
+
+
+def _fault_job_key() -> str:
+    """Job identity for the fault-injection marker (see ``Trainer._inject_fault``)."""
+    run_id = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if run_id and run_id.lower() != "none":
+        return f"run{run_id}"
+    if "TORCHELASTIC_RESTART_COUNT" in os.environ:  # under torchrun with the default rdzv id
+        return f"agent{os.getppid()}"
+    return f"pid{os.getpid()}"
 
 
 def main(argv=None):

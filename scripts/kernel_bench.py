@@ -152,7 +152,7 @@ def main():
 
         def step():
             _lib.call("nsa_adamw_step", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pb.data_ptr(),
-                      mask.data_ptr(), n, 6e-4, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.5, coef.data_ptr(), st())
+                      mask.data_ptr(), n, 6e-4, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.5, coef.data_ptr(), None, st())
 
         t = timeit(step, iters=5, rounds=3)
         out["adamw_124M"] = {"us": t * 1e6, "GBps": 30 * n / t / 1e9}

@@ -63,4 +63,9 @@ def test_multirank_record_carries_rccl_block(tmp_path):
     assert set(rc["transport_by_rank"]) == {"0", "1"}
     assert [r["MiB"] for r in rc["sweep"]] == [1, 2] and all(r["busbw_GBps"] > 0 for r in rc["sweep"])
     assert rc["allreduce_64MiB_ms"] > 0
+    # the bucket layout and the exposed all-reduce per timed step
+    assert rc["buckets"] and rc["buckets"][-1]["late"]
+    assert rc["exposed_allreduce_ms"] is not None and rc["exposed_allreduce_ms"] >= 0
+    assert len(rc["exposed_allreduce_ms_per_step"]) == 1
+    assert all(n >= 1 for n in rc["buckets_launched_in_backward"])
     assert "gemm_kernels" in rec  # per GEMM shape the kernel that ran it (empty on the CPU)

@@ -151,6 +151,60 @@ def test_bucket_layout_contiguous_reverse_order():
     assert names[0].startswith("transformer.ln_f") and names[-1] == "transformer.wte.weight"
 
 
+def test_bucket_cap_rule_gpt2_124m():
+    """a bucket is closed before the parameter that would push it past
+    the cap, so no bucket exceeds ``ddp_bucket_mb`` unless it is one oversized parameter or
+    the late embedding tail (wte + wpe, final only after the embedding backward), and the
+    tail shares no bucket with block weights."""
+    from nanosandbox_amd.models import GPT, GPTConfig
+
+    cfg = GPTConfig(n_layer=12, n_head=12, n_embd=768, block_size=1024, vocab_size=50304, bias=False)
+    store = FlatParamStore(GPT(cfg), "cpu")
+    cap = 64 << 20
+    b = store.buckets(cap)
+    for s, e, members in b:
+        late = [getattr(m.param, "_nsa_late_grad", False) for m in members]
+        assert all(late) or not any(late), "late embeddings share a bucket with block weights"
+        if (e - s) * 4 > cap:
+            assert len(members) == 1 or all(late)
+    assert {m.name for m in b[-1][2]} == {"transformer.wte.weight", "transformer.wpe.weight"}
+    sizes = [(e - s) * 4 / 2 ** 20 for s, e, _ in b]
+    assert len(b) == 7 and all(v <= 64 for v in sizes[:-1]), sizes
+
+
+def test_reducer_records_layout_and_exposure(tmp_path):
+    """The reducer's record for the bench JSON: bucket layout, buckets launched while the
+    backward ran, and the exposed wait in finish() per synchronised step (gloo, 2 ranks)."""
+    port = _free_port()
+    mp.spawn(_exposure_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    rec = torch.load(os.path.join(tmp_path, "exposure0.pt"), weights_only=True)
+    assert len(rec["layout"]) == rec["n_buckets"] > 1
+    assert rec["layout"][-1]["late"] and not any(x["late"] for x in rec["layout"][:-1])
+    assert all(x["MiB"] > 0 and x["first"] and x["last"] for x in rec["layout"])
+    assert len(rec["exposed"]) == STEPS and all(v >= 0 for v in rec["exposed"])
+    # the first step discovers contribution counts; later ones launch during the backward
+    assert rec["early"][0] == 0 and all(n >= 1 for n in rec["early"][1:])
+    assert rec["early"][1:] == [rec["n_buckets"]] * (STEPS - 1)
+
+
+def _exposure_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    gas = GLOBAL_MICRO // world
+    mine = [[b[rank * gas + i] for i in range(gas)] for b in _batches()]
+    model, store, opt = _build(seed=100)
+    red = FlatBucketReducer(store, bucket_cap_mb=0.02)
+    opt.grad_scale = red.grad_scale
+    _train(model, store, opt, mine, gas, before_backward=red.prepare, after_backward=red.finish)
+    early = list(red.launched_in_backward)
+    rec = {"layout": red.layout(), "n_buckets": len(red.buckets), "early": early, "exposed": red.exposed_ms()}
+    if rank == 0:
+        torch.save(rec, os.path.join(out_dir, "exposure0.pt"))
+    dist.destroy_process_group()
+
+
 def test_rccl_env_presets(monkeypatch):
     """RCCL presets fill only unset variables: xGMI (single node) sets the torch NCCL
     knobs; the socket preset adds the reference's TCP-only transport (README.md:101)."""

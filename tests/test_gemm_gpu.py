@@ -207,6 +207,26 @@ def test_wgrad_fused_bias_grad(kernels, T, N_out, K_in, splits):
     assert ((g - ref_w).norm() / ref_w.norm()).item() < 1e-5
 
 
+@pytest.mark.parametrize("T,N_out,K_in", [(2048, 1024, 4096), (1024, 3072, 768)])
+def test_wgrad_bias_deterministic_one_split(kernels, T, N_out, K_in):
+    """with one K split the fused bias-grad kernel still adds each bias column
+    from several column blocks (fp32 atomics in arrival order), so deterministic mode must
+    not use it: weight AND bias gradients bitwise equal across two runs at splits = 1."""
+    from nanosandbox_amd.ops import gemm
+    torch.manual_seed(1)
+    dy = torch.randn(T, N_out, device=DEV).to(BF)
+    x = torch.randn(T, K_in, device=DEV).to(BF)
+    outs = []
+    for _ in range(2):
+        g = torch.full((N_out, K_in), 0.25, device=DEV)
+        gb = torch.full((N_out,), 0.25, device=DEV)
+        gemm.wgrad_acc(dy, x, g, splits=1, deterministic=True, gb32=gb)
+        outs.append((g, gb))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref_b = dy.float().sum(0) + 0.25
+    assert (outs[0][1] - ref_b).abs().max().item() <= 1e-3 * T ** 0.5
+
+
 def test_dispatch_records_native_kernels(kernels):
     """The fixed rule's picks as the bench JSON reports them (no library kernel)."""
     from nanosandbox_amd.ops import gemm_dispatch

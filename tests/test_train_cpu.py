@@ -72,6 +72,29 @@ def test_cpu_smoke_train_resume_sample(cfg, tmp_path, capsys):
     assert outs[0].startswith("KING:") and len(outs[0]) == len("KING:") + 20
 
 
+def test_fault_job_key_default_rdzv_id(monkeypatch):
+    """torchrun's default --rdzv-id makes TORCHELASTIC_RUN_ID 'none' for every
+    job, so it cannot key the marker; two default-launched jobs (different elastic agents)
+    get different keys, while one job's restarted workers (same agent) keep theirs."""
+    import os
+
+    from nanosandbox_amd import train
+
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    monkeypatch.setattr(os, "getppid", lambda: 4242)
+    k1 = train._fault_job_key()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")  # the same job after a restart
+    assert train._fault_job_key() == k1
+    monkeypatch.setattr(os, "getppid", lambda: 4343)  # a second job: another agent
+    assert train._fault_job_key() != k1
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job-x")
+    assert train._fault_job_key() == "runjob-x"
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID")
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT")
+    assert train._fault_job_key() == f"pid{os.getpid()}"
+
+
 def test_fault_injection_and_auto_resume(cfg, tmp_path, monkeypatch):
     from nanosandbox_amd.train import Trainer
 
@@ -80,7 +103,7 @@ def test_fault_injection_and_auto_resume(cfg, tmp_path, monkeypatch):
     with pytest.raises(RuntimeError, match="injected fault"):
         Trainer(c).fit()
     assert (tmp_path / "out" / "ckpt.pt").exists()  # saved at iter 6
-    assert (tmp_path / "out" / ".fault_injected_rank0.job-a").exists()
+    assert (tmp_path / "out" / ".fault_injected_rank0.runjob-a").exists()
     # the same job configuration restarted (what torchrun --max-restarts / a k8s restart
     # does): the fault fired once per job, so the restart resumes at 6 and runs through
     tr = Trainer(c)
