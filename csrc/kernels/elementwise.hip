@@ -19,8 +19,8 @@ constexpr int kBlock = 256;
 constexpr int kUnroll = NSA_EW_UNROLL;
 
 // Grid cap: 2048 blocks = 8 per CU x 4 waves fill every wave slot (fastest alone).
-// NSA_EW_MAX_BLOCKS lowers it so a concurrent stream's GEMM workgroups can be
-// resident beside the elementwise kernel (ops/streams.py).
+// NSA_EW_MAX_BLOCKS lowers it (an A/B knob: room for another stream's workgroups; the
+// training step itself runs on one compute stream).
 inline int64_t ew_grid_cap() {
   static int64_t cap = [] {
     const char* e = getenv("NSA_EW_MAX_BLOCKS");

@@ -119,7 +119,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
 //         kernel taking two query slices per barrier; v1 = the generic kernels
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5 };
 enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -128,7 +128,7 @@ FlashConfig& flash_config() {
   static FlashConfig c = [] {
     FlashConfig d{FWD_AUTO, BWD_V3, ATTN_ORDER_DEFAULT};
     if (const char* e = getenv("NSA_FLASH_FWD"))
-      d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '3' || e[1] == '4')) ? e[1] - '0' : FWD_AUTO;
+      d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '3' || e[1] == '4' || e[1] == '5')) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
       d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
@@ -562,6 +562,246 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
         o[0][dt] = mfma(vf, pf[0][sb][s], o[0][dt]);
         o[1][dt] = mfma(vf, pf[1][sb][s], o[1][dt]);
       }
+    }
+  }
+}
+
+// =============================================================================
+// forward v5 (D = 64): v4's geometry (64 queries per wave as two 32-query blocks, two
+// K/V tiles per barrier) with the softmax's per-element instruction count cut in half.
+//
+// Scores are taken in log2 units, S' = c q·k with c = scale*log2(e) (Q pre-scaled when it is
+// loaded, or one packed multiply per score pair: NSA_FWD5_QSCALE below).  The max subtraction is then not needed for
+// correctness, only for range: O and l are sums of 2^(S' - m) for ANY per-query m, and
+// O / l does not depend on m.  While every score of a wave's queries stays within fp32 /
+// bf16 range the kernel runs with m = 0 ("fast" tiles): p = exp2(S') straight from the
+// accumulator -- no row max (34 v_max3 + exchanges), no subtract / fma per element, no
+// rescale test.  Per tile and lane: 64 v_exp_f32, 32 v_cvt_pk_bf16_f32, the row sum and
+// one range test, against v4's ~315 VALU.  The range test is exact: a tile whose row sum
+// exceeds 2^64 (or is not finite), or a query whose running l would stay below 2^-60, is
+// redone by v4's exact tile (row max, deferred rescale) and the wave stays on exact tiles
+// from then on, so extreme logits cost speed, never accuracy.
+//
+// NSA_FWD5_ROWSUM 0: row sums as fp32 adds of p; 1: v_dot2_f32_bf16 over the bf16 pairs the
+// P·V MFMAs consume (half the instructions, and l sums exactly the P that multiplies V).
+// =============================================================================
+//
+// NSA_FWD5_QSCALE 1: Q pre-scaled as above; 0: Q as loaded and the fast tiles multiply each
+// score pair by scale*log2(e) with one v_pk_mul_f32 (32 more VALU per tile, but the scores
+// are exactly v4's: the bf16 rounding of q*c costs up to a few % of p once single products
+// q_d k_d reach tens of log2 units, e.g. the test suite's +-100 logits).
+#ifndef NSA_FWD5_ROWSUM
+#define NSA_FWD5_ROWSUM 1
+#endif
+#ifndef NSA_FWD5_QSCALE
+#define NSA_FWD5_QSCALE 0
+#endif
+
+template <bool MASK>
+__device__ __forceinline__ bool fwd_tile5(const char* kt, const char* vt, const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2],
+                                          float (&l_i)[2], int kv0, int qposA, int h, int r, int lane,
+                                          float scale_log2) {
+  constexpr int D = 64;
+  f32x16 st[2][2];  // [block][key sub-block]
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[0][sb] = f32x16{};
+    st[1][sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 kf = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
+      st[0][sb] = mfma(kf, qf[0][ks], st[0][sb]);
+      st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
+    }
+  }
+  bf16x8 pf[2][2][2];
+  float rs[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    float acc[2] = {0.0f, 0.0f};  // one chain per key sub-block
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      if constexpr (!NSA_FWD5_QSCALE) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {  // one v_pk_mul_f32 per score pair
+          nsa_f32x2 v2 = nsa_f32x2{st[blk][sb][i], st[blk][sb][i + 1]} * scale_log2;
+          st[blk][sb][i] = v2.x;
+          st[blk][sb][i + 1] = v2.y;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float s = st[blk][sb][i];
+        if constexpr (MASK) {
+          if (kv0 + 32 * sb + acc_row(i, h) > qposA + 32 * blk) s = -INFINITY;
+        }
+        const float p = fast_exp2(s);
+        if constexpr (NSA_FWD5_ROWSUM == 0) acc[sb] += p;
+        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
+      }
+      if constexpr (NSA_FWD5_ROWSUM == 1) {
+        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+        const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[sb] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{pf[blk][sb][s][2 * e], pf[blk][sb][s][2 * e + 1]}, one,
+                                                      acc[sb], false);
+      }
+    }
+    rs[blk] = half_swap_sum(acc[0] + acc[1]);
+  }
+  const float lA = l_i[0] + rs[0], lB = l_i[1] + rs[1];
+  // NaN-safe: a non-finite sum fails every comparison
+  const bool ok = rs[0] <= 0x1p64f && rs[1] <= 0x1p64f && lA >= 0x1p-60f && lB >= 0x1p-60f;
+  if (__builtin_amdgcn_ballot_w64(!ok)) return false;  // wave-uniform: redo this tile exactly
+  l_i[0] = lA;
+  l_i[1] = lB;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 vf = tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane);
+        o[0][dt] = mfma(vf, pf[0][sb][s], o[0][dt]);
+        o[1][dt] = mfma(vf, pf[1][sb][s], o[1][dt]);
+      }
+    }
+  }
+  return true;
+}
+
+// Workgroup = 4 waves x 64 queries, 4-slot K/V ring filled by LDS-DMA, two tiles per
+// barrier (flash_fwd3_kernel<false, 4, true>'s schedule).  No dropout (dropout runs v1/v3).
+__global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse_out, int B, int T, int H,
+                                                            float scale_log2) {
+  constexpr int D = 64;
+  constexpr int BN = 64;
+  constexpr int NS = 4;
+  constexpr int TILE_BYTES = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
+
+  const int C = H * D;
+  const int64_t row_stride = 3 * (int64_t)C;
+  const int BH = B * H;
+  const int n_qt = (T + 255) / 256;
+  int bh, qt;
+  attn_order(n_qt, BH, 0, bh, qt);
+  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
+  const int b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int q0 = qt * 256;
+  const int q0w = q0 + 64 * w;
+  const int qposA = q0w + r;
+  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
+  const bf16_t* qbase = base + hh * D;
+  const bf16_t* kbase = base + C + hh * D;
+
+  // Q fragments, pre-scaled by scale * log2(e) (scores come out of the MFMA in log2 units)
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int qp = qposA + 32 * blk;
+    const int qc = qp < T ? qp : T - 1;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 raw = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[blk][ks][e] = NSA_FWD5_QSCALE ? (__bf16)((float)raw[e] * scale_log2) : raw[e];
+    }
+  }
+  f32x16 o[2][2];
+  float m_i[2], l_i[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    o[blk][0] = f32x16{};
+    o[blk][1] = f32x16{};
+    m_i[blk] = 0.0f;  // fast tiles: m = 0 (exact tiles take over from there)
+    l_i[blk] = 0.0f;
+  }
+  bool fast = true;  // wave-uniform
+
+  const int kv_end = min(T, q0 + 256);
+  const int n_tiles = (kv_end + BN - 1) / BN;
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+  const int prow = 16 * w + (lane >> 3);
+  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
+  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
+  const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
+  const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
+  auto issue = [&](int jt, int buf) {
+    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
+    uint32_t o0 = koff0, o8 = koff8;
+    if (jt * BN + BN > T) {
+      const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
+      o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
+      o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
+    }
+    const uint32_t kb = lds0 + (uint32_t)(buf * TILE_BYTES + 16 * w * 128);
+    const uint32_t vb = kb + NS * TILE_BYTES;
+    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
+    glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
+    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
+    glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
+  };
+  asm volatile("" ::"v"(qf[0][0]), "v"(qf[0][1]), "v"(qf[0][2]), "v"(qf[0][3]), "v"(qf[1][0]), "v"(qf[1][1]),
+               "v"(qf[1][2]), "v"(qf[1][3]));  // Q landed before the DMA
+  const DropArgs dr{0u, 1.0f, 0ull, bh, T};
+  const float sl_exact = NSA_FWD5_QSCALE ? 1.0f : scale_log2;  // the exact tiles' score multiplier
+  issue(0, 0);
+  issue(min(1, n_tiles - 1), 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int j = 0; j < n_tiles; j += 2) {
+    issue(min(j + 2, n_tiles - 1), (j + 2) % 4);
+    issue(min(j + 3, n_tiles - 1), (j + 3) % 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int jj = j + u;
+      if (jj < n_tiles) {
+        const int kv0 = jj * BN;
+        const char* kt = smem + (jj % 4) * TILE_BYTES;
+        const char* vt = smem + (4 + jj % 4) * TILE_BYTES;
+        if (kv0 + BN - 1 <= q0w) {
+          if (!(fast && fwd_tile5<false>(kt, vt, qf, o, l_i, kv0, qposA, h, r, lane, scale_log2))) {
+            fast = false;
+            fwd_tile2<false, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, sl_exact, dr);
+          }
+        } else if (kv0 <= q0w + 63) {
+          if (!(fast && fwd_tile5<true>(kt, vt, qf, o, l_i, kv0, qposA, h, r, lane, scale_log2))) {
+            fast = false;
+            fwd_tile2<true, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, sl_exact, dr);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int qp = qposA + 32 * blk;
+    if (qp < T) {
+      const float inv_l = 1.0f / l_i[blk];
+      bf16_t* orow = out + ((int64_t)b * T + qp) * C + hh * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          uint2 u;
+          u.x = pack2(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
+          u.y = pack2(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
+          *reinterpret_cast<uint2*>(orow + d) = u;
+        }
+      }
+      if (h == 0) lse_out[(int64_t)bh * T + qp] = (m_i[blk] * sl_exact + __log2f(l_i[blk])) * 0.6931471805599453f;
     }
   }
 }
@@ -1746,7 +1986,13 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
     const int n_qt3 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    const bool v3 = sel == FWD_V3 || sel == FWD_V4 || (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
+    const bool v3 = sel == FWD_V3 || sel == FWD_V4 || sel == FWD_V5 ||
+                    (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
+    if (v3 && sel == FWD_V5 && !th) {
+      flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+                                                      scale * kLog2e);
+      return hipGetLastError();
+    }
     if (v3) {
       // v4 = v3 with two K/V tiles per barrier (auto's pick): B120 T1024 H12 335.5 vs
       // 350.9 us (profiles/r4_attn_ab_pair.log)
@@ -1893,13 +2139,13 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
   }
 }
 
-// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4, bwd 1 v1 / 2 v2 / 3 v3, order
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5, bwd 1 v1 / 2 v2 / 3 v3, order
 // 0 / 1; a negative value keeps the current setting.  Returns the previous selection as
 // fwd | bwd << 4 | order << 8.
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5) c.fwd = fwd;
   if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order == 0 || order == 1) c.order = order;
   return prev;

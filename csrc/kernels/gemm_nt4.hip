@@ -1,9 +1,9 @@
 // Persistent four-wave bf16 "NT" GEMM for gfx950: C[M,N] = A[M,K] · B[N,K]^T (both operands
-// K-contiguous, fp32 accumulate), with the same epilogues as gemm_nt.hip (bf16 store,
-// gelu'(u) (fp16) + gelu(u) for the c_fc forward, acc * U with U = gelu'(u) for the mlp.c_proj
-// input grad).
+// K-contiguous, fp32 accumulate), with fused epilogues (bf16 store (+ bias), gelu'(u) (fp16)
+// + gelu(u) for the c_fc forward, acc * U with U = gelu'(u) for the mlp.c_proj input grad,
+// and the cross-entropy pair XENT / XDX for the tied lm_head).
 //
-// Why a second NT kernel: the 8-wave kernel (gemm_nt.hip, 128x64 per wave) reads
+// Why four waves: round 3's eight-wave NT kernel (128x64 per wave, since removed) read
 // 24 fragments (24 KiB) per wave per 64-deep K-tile for 64 MFMAs; with 8 waves that is
 // 192 KiB of ds_read_b128 plus 64 KiB of LDS-DMA writes per CU per K-tile, against
 // 2048 MFMA cycles per SIMD — the LDS array runs near its 256 B/clk (PMC:
@@ -35,7 +35,8 @@
 // accumulators of the 8 fragments j are 8 CONSECUTIVE columns and one store instruction
 // writes 4 rows x 256 contiguous bytes straight from the accumulators (no LDS round trip).
 //
-// Persistent: grid = #CUs, tiles walked in the XCD-grouped order of gemm_nt.hip; the DMA
+// Persistent: grid = #CUs, tiles walked in an XCD-grouped order (tile groups of row blocks
+// x every column, each XCD's workgroups on neighbouring tiles); the DMA
 // cursor runs straight on into the next tile, so the next tile's first two K-tiles load
 // while this tile's epilogue stores.  Tail tiles are shifted back inside the matrix and
 // store only their not-yet-covered rows / columns: M, N >= 256, N % 8 == 0, K % 64 == 0.

@@ -17,9 +17,9 @@ bias grad db += colsum(dY)    any                                             ``
 
 Anything outside every rule (K % 8 != 0, a side < 8, fp32 inputs) is out of the kernels'
 contract and runs as a plain torch matmul — no GPT configuration in ``config/`` reaches it
-(``tests/test_dispatch_cpu.py`` enumerates them).  The round-3 runtime race against hipBLASLt
-(``NSA_GEMM_BACKEND`` / TunableOp tables) is gone: its last library wins were 1-5 % on four
-shapes (docs/performance.md), and it made the kernel set depend on the box.
+(``tests/test_dispatch_cpu.py`` enumerates them).  Round 3's start-up race against the vendor
+library is gone: its last library wins were 1-5 % on four shapes (docs/performance.md), and it
+made the kernel set depend on the box.
 
 Env knobs for A/B experiments only: ``NSA_WGRAD_SPLITS`` (force a weight-grad split count),
 ``NSA_WGRAD_FILL`` (the split rule's round-fill threshold), ``NSA_NT_STORE`` (epilogue store

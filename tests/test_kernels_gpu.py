@@ -338,7 +338,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
@@ -356,6 +356,14 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
     yr = attn_ref(xr, H)
     yr.backward(dy.float())
     assert rel_err(y, yr) < 2e-2, rel_err(y, yr)
+    # per element: every output within a bound scaled by the absolute terms that form it
+    # (|P|·|V|, the row's weighted magnitude), not only the Frobenius ratio
+    q, k, v = xr.detach().view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    att = torch.softmax((q @ k.transpose(-1, -2) / math.sqrt(D)).masked_fill(
+        torch.ones(T, T, device=DEV, dtype=torch.bool).triu(1), float("-inf")), -1)
+    mag = (att @ v.abs()).transpose(1, 2).reshape(B, T, C)
+    assert torch.isfinite(y.float()).all()
+    assert ((y.float() - yr.detach()).abs() <= 2 ** -5 * mag + 2 ** -7 * yr.detach().abs() + 1e-4).all()
     g = qkv.grad.float().view(B, T, 3, C)
     gr = xr.grad.view(B, T, 3, C)
     for i, name in enumerate("qkv"):
@@ -363,8 +371,99 @@ def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
         assert e < 3e-2, f"d{name} rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4"])
-@pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative"])
+def _flash_fwd_raw(qkv, H, out_nan=True):
+    """nsa_flash_fwd into NaN-prefilled y / lse buffers (a row or column the kernel skips
+    stays NaN instead of whatever torch.empty held)."""
+    from nanosandbox_amd.ops import _lib
+
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    y = torch.full((B, T, C), float("nan") if out_nan else 0.0, device=DEV, dtype=BF)
+    lse = torch.full((B, H, T), float("nan"), device=DEV, dtype=torch.float32)
+    _lib.call("nsa_flash_fwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, C // H, 1.0 / math.sqrt(C // H),
+              0.0, 0, _lib.stream())
+    torch.cuda.synchronize()
+    return y, lse
+
+
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5"])
+@pytest.mark.parametrize("T,D", [(1024, 64), (320, 64), (200, 64), (64, 64), (77, 32), (192, 128), (1024, 32)])
+@pytest.mark.parametrize("layout", ["tile", "row"])
+def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
+    """Exact-structure forward: Q = 0 makes every visible score 0, so
+    P is uniform over keys 0..q, and V is one-hot -- by 64-key tile ("tile": column d holds
+    the keys of tile d % D) or by row inside the tile ("row": column d holds the keys with
+    k % 64 == d % D).  Then y[q, d] = (visible keys of that column) / (q + 1) exactly (in
+    bf16) and lse[q] = ln(q + 1): a skipped causal tile, a dropped or misplaced key row, or
+    a wrong diagonal mask shows up as a whole wrong column, and NaN-prefilled outputs catch
+    anything left unwritten."""
+    flash_variant(fwd=fwd)
+    B, H = 2, 2
+    C = H * D
+    k_idx = torch.arange(T, device=DEV)
+    col = (k_idx // 64) % D if layout == "tile" else (k_idx % 64) % D
+    v1h = torch.zeros(T, D, device=DEV)
+    v1h[k_idx, col] = 1.0
+    qkv = torch.zeros(B, T, 3, H, D, device=DEV)
+    qkv[:, :, 1] = torch.randn(B, T, H, D, device=DEV)  # K: irrelevant when Q = 0
+    qkv[:, :, 2] = v1h[None, :, None, :]
+    qkv = qkv.reshape(B, T, 3 * C).to(BF)
+    y, lse = _flash_fwd_raw(qkv, H)
+    counts = torch.cumsum(v1h, 0)  # [T, D]: visible keys per column for query q
+    ref = counts / (k_idx[:, None] + 1).float()
+    got = y.float().view(B, T, H, D)
+    assert not torch.isnan(got).any() and not torch.isnan(lse).any()
+    err = (got - ref[None, :, None, :]).abs()
+    assert (err <= 2 ** -8 * ref[None, :, None, :] + 1e-7).all(), err.max().item()
+    lref = torch.log((k_idx + 1).float())
+    assert ((lse - lref[None, None]).abs() <= 1e-5 * lref[None, None] + 1e-6).all()
+
+
+@pytest.mark.parametrize("T", [1024, 320, 96])
+def test_flash_bwd_exact_structure(kernels, flash_variant, T):
+    """Backward counterpart: Q = 0 (uniform P = 1/(q+1)), K one-hot by key tile, dO one-hot
+    by query slice, V random.  Every gradient element is compared with the fp32 reference
+    against a bound scaled by the absolute terms that form it, so a skipped query slice
+    (dK / dV) or key tile (dQ) is a whole column far outside its bound."""
+    from nanosandbox_amd.ops import functional as fn
+
+    B, H, D = 1, 2, 64
+    C = H * D
+    k_idx = torch.arange(T, device=DEV)
+    q = torch.zeros(B, T, H, D, device=DEV)
+    k = torch.zeros(B, T, H, D, device=DEV)
+    k[:, k_idx, :, (k_idx // 64) % D] = 1.0
+    v = torch.randn(B, T, H, D, device=DEV)
+    qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(BF)
+    dy = torch.zeros(B, T, H, D, device=DEV)
+    dy[:, k_idx, :, (k_idx // 32) % D] = 1.0
+    dy = dy.reshape(B, T, C).to(BF)
+    x = qkv.clone().requires_grad_(True)
+    fn.attention(x, H, 0.0, True).backward(dy)
+    g = x.grad.float().view(B, T, 3, H, D)
+    xr = qkv.float().requires_grad_(True)
+    attn_ref(xr, H).backward(dy.float())
+    gr = xr.grad.view(B, T, 3, H, D)
+    # magnitude of the terms behind each gradient element (fp32, from the same inputs)
+    qf, kf, vf = qkv.float().view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    dof = dy.float().view(B, T, H, D).transpose(1, 2)
+    mask = torch.ones(T, T, device=DEV, dtype=torch.bool).triu(1)
+    p = torch.softmax((qf @ kf.transpose(-1, -2) / math.sqrt(D)).masked_fill(mask, float("-inf")), -1)
+    dp = dof @ vf.transpose(-1, -2)
+    o = p @ vf
+    delta = (dof * o).sum(-1, keepdim=True)
+    ds_mag = p * (dp.abs() + delta.abs())
+    mags = {"q": (ds_mag @ kf.abs()) / math.sqrt(D), "k": (ds_mag.transpose(-1, -2) @ qf.abs()) / math.sqrt(D),
+            "v": p.transpose(-1, -2) @ dof.abs()}
+    for i, name in enumerate("qkv"):
+        m = mags[name].transpose(1, 2)  # [B, T, H, D]
+        err = (g[:, :, i] - gr[:, :, i]).abs()
+        assert torch.isfinite(g[:, :, i]).all()
+        assert (err <= 2 ** -6 * m + 1e-5).all(), (name, err.max().item())
+
+
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5"])
+@pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative", "overflow", "underflow"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
 
@@ -394,6 +493,10 @@ def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     elif pattern == "spikes":
         idx = torch.randint(0, T, (24,), device=DEV)
         k[:, idx] += 30.0 * u
+    elif pattern == "overflow":  # scores ~ +100 (log2 ~ 144): v5's fast tiles overflow, exact tiles take over
+        k = k + 200.0 * u
+    elif pattern == "underflow":  # scores ~ -100 (log2 ~ -144): v5's fast tiles underflow to l < 2^-60
+        k = k - 200.0 * u
     else:  # every logit far below zero (the first tile must still set the max: no underflow)
         k = k - 60.0 * u
     qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(BF).requires_grad_(True)
@@ -458,6 +561,28 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
     for i, name in enumerate("qkv"):
         e = rel_err(grads["v2"][:, :, i], grads["v1"][:, :, i])
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
+
+
+def test_flash_fwd_v5_fallback_mid_sequence(kernels, flash_variant):
+    """v5 switches a wave from fast (m = 0) to exact tiles when a later tile overflows: the
+    first tiles ran with m = 0 and are then rescaled by the exact path's max."""
+    from nanosandbox_amd.ops import functional as fn
+
+    flash_variant(fwd="v5")
+    torch.manual_seed(3)
+    B, T, H, D = 1, 1024, 2, 64
+    C = H * D
+    q = torch.randn(B, T, H, D, device=DEV)
+    k = torch.randn(B, T, H, D, device=DEV)
+    v = torch.randn(B, T, H, D, device=DEV)
+    u = torch.nn.functional.normalize(torch.randn(D, device=DEV), dim=0)
+    q = q + 4.0 * u
+    k[:, 700:760] += 220.0 * u  # keys 700..759 score ~ +110: every query >= 700 overflows there
+    qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(BF)
+    y = fn.attention(qkv, H, 0.0, True).float()
+    yr = attn_ref(qkv.float(), H)
+    assert torch.isfinite(y).all()
+    assert rel_err(y, yr) < 2e-2, rel_err(y, yr)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])
