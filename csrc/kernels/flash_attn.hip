@@ -104,6 +104,11 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
     bh = v % BH;
     return;
   }
+  if (order == 2) {  // (b, h)-major: the tiles of one (b, h) are consecutive workgroups
+    bh = v / n_tiles;
+    t = v % n_tiles;
+    return;
+  }
   const int total = n_tiles * BH;
   const int xcd = v % 8, q = total / 8, r = total % 8;
   const int u = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + v / 8;
@@ -131,7 +136,7 @@ FlashConfig& flash_config() {
       d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '3' || e[1] == '4' || e[1] == '5')) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
       d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
-    if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = e[0] == '1';
+    if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
     return d;
   }();
   return c;
@@ -674,11 +679,37 @@ __device__ __forceinline__ bool fwd_tile5(const char* kt, const char* vt, const 
   return true;
 }
 
+// Hand-over from fast tiles (m = 0) to exact tiles: O and l so far are sums of 2^(S'),
+// relative to m = 0.  The exact tiles' deferred rescale only ever RAISES m, so the hand-over
+// first moves each query to m' = log2(l) (O and l times 2^-m', l becomes ~1): a tile whose
+// scores underflowed (all far below the earlier ones) then adds ~0, one that overflowed
+// raises m from there.  A query with nothing accumulated yet (l = 0) gets m = -inf-like, so
+// its first exact tile sets the max.  m_i is in the exact tiles' units (raw scores, times
+// their multiplier sl).
+__device__ __forceinline__ void fwd5_to_exact(f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], float sl) {
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    if (l_i[blk] > 0.0f) {
+      const float mp = __log2f(l_i[blk]);
+      const float f = fast_exp2(-mp);
+      l_i[blk] *= f;
+      o[blk][0] *= f;
+      o[blk][1] *= f;
+      m_i[blk] = mp / sl;
+    } else {
+      m_i[blk] = -1e30f;
+    }
+  }
+}
+
 // Workgroup = 4 waves x 64 queries, 4-slot K/V ring filled by LDS-DMA, two tiles per
 // barrier (flash_fwd3_kernel<false, 4, true>'s schedule).  No dropout (dropout runs v1/v3).
+#ifndef NSA_PROBE_KV_SHARED
+#define NSA_PROBE_KV_SHARED 0  // probe build: every (b, h) reads (0, 0)'s K/V (wrong output; traffic probe)
+#endif
 __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2) {
+                                                            float scale_log2, int order) {
   constexpr int D = 64;
   constexpr int BN = 64;
   constexpr int NS = 4;
@@ -690,7 +721,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
   const int BH = B * H;
   const int n_qt = (T + 255) / 256;
   int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
+  attn_order(n_qt, BH, order, bh, qt);
   qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -700,7 +731,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
   const int qposA = q0w + r;
   const bf16_t* base = qkv + (int64_t)b * T * row_stride;
   const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
+  const bf16_t* kbase = NSA_PROBE_KV_SHARED ? qkv + C : base + C + hh * D;
 
   // Q fragments, pre-scaled by scale * log2(e) (scores come out of the MFMA in log2 units)
   bf16x8 qf[2][4];
@@ -770,11 +801,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
         const char* vt = smem + (4 + jj % 4) * TILE_BYTES;
         if (kv0 + BN - 1 <= q0w) {
           if (!(fast && fwd_tile5<false>(kt, vt, qf, o, l_i, kv0, qposA, h, r, lane, scale_log2))) {
+            if (fast) fwd5_to_exact(o, m_i, l_i, sl_exact);
             fast = false;
             fwd_tile2<false, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, sl_exact, dr);
           }
         } else if (kv0 <= q0w + 63) {
           if (!(fast && fwd_tile5<true>(kt, vt, qf, o, l_i, kv0, qposA, h, r, lane, scale_log2))) {
+            if (fast) fwd5_to_exact(o, m_i, l_i, sl_exact);
             fast = false;
             fwd_tile2<true, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, sl_exact, dr);
           }
@@ -1990,7 +2023,7 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
                     (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
     if (v3 && sel == FWD_V5 && !th) {
       flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                      scale * kLog2e);
+                                                      scale * kLog2e, order);
       return hipGetLastError();
     }
     if (v3) {
@@ -2147,6 +2180,6 @@ NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5) c.fwd = fwd;
   if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
-  if (order == 0 || order == 1) c.order = order;
+  if (order >= 0 && order <= 2) c.order = order;
   return prev;
 }

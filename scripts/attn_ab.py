@@ -40,7 +40,13 @@ def with_env(env, fn):
     from nanosandbox_amd.ops.functional import flash_variant
 
     if any(v.isdigit() for v in env.values()):  # raw selector codes (variant libraries, NSA_KERNEL_LIB)
-        code = lambda k: int(env[k]) if k in env else -1  # noqa: E731
+        from nanosandbox_amd.ops.functional import _FLASH_BWD, _FLASH_FWD
+        names = {"fwd": _FLASH_FWD, "bwd": _FLASH_BWD, "order": {}}
+
+        def code(k):
+            if k not in env:
+                return -1
+            return int(env[k]) if env[k].isdigit() else names[k][env[k]]
         prev = _lib.call_ret("nsa_flash_set_variant", code("fwd"), code("bwd"), code("order"))
         try:
             return fn()
