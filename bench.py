@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible step: fixed-order split-K weight gradients, sorted embedding "
                          "backward, ordered LayerNorm dW/db (no fp32 atomics)")
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"],
+                    help="compute dtype (nanoGPT's dtype key): float16 runs the fp16 instantiation of every "
+                         "kernel with the dynamic loss scale on the device (the headline is bfloat16)")
     ap.add_argument("--bf16-residual", action="store_true",
                     help="keep the residual stream and its gradient in bf16 (default fp32: nanoGPT's "
                          "autocast contract, fp32 embedding sum and fp32 + bf16 residual adds)")
@@ -149,7 +152,7 @@ def main():
             dataset = args.real_data
     cfg.update(dataset=dataset, data_dir=data_dir, batch_size=args.micro_batch, block_size=args.block_size,
                gradient_accumulation_steps=total_micro, n_layer=dims[0], n_head=dims[1], n_embd=dims[2],
-               dropout=0.0, bias=args.bias, compile=False, device=args.device, dtype="bfloat16",
+               dropout=0.0, bias=args.bias, compile=False, device=args.device, dtype=args.dtype,
                backend="nccl" if cuda else "gloo",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
                fp32_residual=not args.bf16_residual, deterministic=args.deterministic,
@@ -234,7 +237,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16" if cuda else "fp32",
+            "dtype": ({"bfloat16": "bf16", "float16": "fp16"}[args.dtype]) if cuda else "fp32",
             "data": (f"real ({dataset}); random-init weights" if args.real_data else
                      "synthetic (uniform random tokens, vocab 50304); random-init weights"),
             "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,

@@ -211,6 +211,90 @@ __device__ __forceinline__ nsa_f32x2 nsa_unpk_f16(uint32_t u) {
 __device__ __forceinline__ float nsa_h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t nsa_f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
+// ---------------------------------------------------------------------------------------
+// 16-bit element types.  The training kernels take a compile-time H: false = bf16 (the
+// default compute dtype), true = fp16 (nanoGPT's dtype='float16' with a dynamic loss scale).
+// Both are stored as raw 16-bit words (bf16_t) and moved in the same vectors; only the
+// conversions and the MFMA opcode differ (gfx950's fp16 MFMAs run at the bf16 rate).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <bool H>
+__device__ __forceinline__ float e2f(uint16_t v) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, v);
+  else return __uint_as_float(((uint32_t)v) << 16);
+}
+template <bool H>
+__device__ __forceinline__ uint16_t f2e(float f) {
+  if constexpr (H) return __builtin_bit_cast(uint16_t, (_Float16)f);
+  else return f2bf(f);
+}
+// the low / high element of a packed pair
+template <bool H>
+__device__ __forceinline__ float lo2f(uint32_t w) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+  else return __uint_as_float(w << 16);
+}
+template <bool H>
+__device__ __forceinline__ float hi2f(uint32_t w) {
+  if constexpr (H) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  else return __uint_as_float(w & 0xffff0000u);
+}
+// two f32 -> one dword of two elements (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32, RNE)
+template <bool H>
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  if constexpr (H) {
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t{lo, hi}), h2_t));
+  } else {
+    typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t{lo, hi}), b2_t));
+  }
+}
+template <bool H>
+__device__ __forceinline__ void unpack8e(uint4 u, float (&f)[8]) {
+  f[0] = lo2f<H>(u.x);
+  f[1] = hi2f<H>(u.x);
+  f[2] = lo2f<H>(u.y);
+  f[3] = hi2f<H>(u.y);
+  f[4] = lo2f<H>(u.z);
+  f[5] = hi2f<H>(u.z);
+  f[6] = lo2f<H>(u.w);
+  f[7] = hi2f<H>(u.w);
+}
+template <bool H>
+__device__ __forceinline__ void load8e(const bf16_t* p, float (&f)[8]) {
+  unpack8e<H>(*reinterpret_cast<const uint4*>(p), f);
+}
+template <bool H>
+__device__ __forceinline__ void store8e(bf16_t* p, const float (&f)[8]) {
+  uint4 u;
+  u.x = pk2<H>(f[0], f[1]);
+  u.y = pk2<H>(f[2], f[3]);
+  u.z = pk2<H>(f[4], f[5]);
+  u.w = pk2<H>(f[6], f[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+// one scalar f32 -> element (the value a cast to the element type gives)
+template <bool H>
+__device__ __forceinline__ __bf16 f2frag(float f) {
+  return __builtin_bit_cast(__bf16, f2e<H>(f));
+}
+// MFMAs on 8-element fragments held in bf16x8 containers (the bits of either type)
+template <bool H>
+__device__ __forceinline__ f32x16 mfma32e(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool H>
+__device__ __forceinline__ f32x4 mfma16e(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 // Nontemporal streams only pay for tensors larger than the 256 MB Infinity Cache: a smaller
 // one can stay cache-resident for its next reader (shakespeare_char config, 25 MB LayerNorm
 // rows: 4.78 ms/iter with nontemporal streams everywhere, 4.72-4.76 gated).  Streams of at

@@ -56,21 +56,22 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) {
     return *reinterpret_cast<const uint4*>(p);
   }
 }
-template <bool NT>
+template <bool NT, bool H = false>
 __device__ __forceinline__ void st8(bf16_t* p, const float (&f)[8]) {
   if constexpr (NT) {
     ew_u32x4 v;
-    v.x = pack2(f[0], f[1]);
-    v.y = pack2(f[2], f[3]);
-    v.z = pack2(f[4], f[5]);
-    v.w = pack2(f[6], f[7]);
+    v.x = pk2<H>(f[0], f[1]);
+    v.y = pk2<H>(f[2], f[3]);
+    v.z = pk2<H>(f[4], f[5]);
+    v.w = pk2<H>(f[6], f[7]);
     __builtin_nontemporal_store(v, reinterpret_cast<ew_u32x4*>(p));
   } else {
-    store8(p, f);
+    store8e<H>(p, f);
   }
 }
 
-template <bool NT = false>
+// H (every kernel below): the 16-bit tensors are fp16 instead of bf16
+template <bool NT = false, bool H = false>
 __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                          int64_t n) {
   const int64_t nv = n / 8;
@@ -87,19 +88,19 @@ __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const bf16_t* __restri
       const int64_t i = i0 + (int64_t)r * kBlock;
       if (i < nv) {
         float f[8];
-        unpack8(u[r], f);
+        unpack8e<H>(u[r], f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-        st8<NT>(y + i * 8, f);
+        st8<NT, H>(y + i * 8, f);
       }
     }
   }
   // scalar tail
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-    y[i] = f2bf(gelu_f(bf2f(x[i])));
+    y[i] = f2e<H>(gelu_f(e2f<H>(x[i])));
 }
 
-template <bool NT = false>
+template <bool NT = false, bool H = false>
 __global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                          bf16_t* __restrict__ dx, int64_t n) {
   const int64_t nv = n / 8;
@@ -117,33 +118,35 @@ __global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const bf16_t* __restri
       const int64_t i = i0 + (int64_t)r * kBlock;
       if (i < nv) {
         float g[8], f[8];
-        unpack8(ug[r], g);
-        unpack8(ux[r], f);
+        unpack8e<H>(ug[r], g);
+        unpack8e<H>(ux[r], f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = g[j] * gelu_grad(f[j]);
-        st8<NT>(dx + i * 8, f);
+        st8<NT, H>(dx + i * 8, f);
       }
     }
   }
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-    dx[i] = f2bf(bf2f(dy[i]) * gelu_grad(bf2f(x[i])));
+    dx[i] = f2e<H>(e2f<H>(dy[i]) * gelu_grad(e2f<H>(x[i])));
 }
 
+template <bool H = false>
 __global__ __launch_bounds__(kBlock) void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                         int64_t n, uint32_t thresh, float scale, uint64_t salt) {
   const uint64_t seed = nsa_seed(salt);
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
     float f[8];
-    load8(x + i * 8, f);
+    load8e<H>(x + i * 8, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = nsa_keep(seed, (uint64_t)(i * 8 + j), thresh) ? f[j] * scale : 0.0f;
-    store8(y + i * 8, f);
+    store8e<H>(y + i * 8, f);
   }
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-    y[i] = f2bf(nsa_keep(seed, (uint64_t)i, thresh) ? bf2f(x[i]) * scale : 0.0f);
+    y[i] = f2e<H>(nsa_keep(seed, (uint64_t)i, thresh) ? e2f<H>(x[i]) * scale : 0.0f);
 }
 
+template <bool H = false>
 __global__ __launch_bounds__(kBlock) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
                                                               int64_t n) {
   const int64_t nv = n / 8;
@@ -151,10 +154,10 @@ __global__ __launch_bounds__(kBlock) void cast_f32_bf16_kernel(const float* __re
     const float4 a = reinterpret_cast<const float4*>(x)[2 * i];
     const float4 b = reinterpret_cast<const float4*>(x)[2 * i + 1];
     float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    store8(y + i * 8, f);
+    store8e<H>(y + i * 8, f);
   }
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-    y[i] = f2bf(x[i]);
+    y[i] = f2e<H>(x[i]);
 }
 
 // dst[C][R] = src[R][C]^T for bf16 (R, C multiples of 64): the cached K-contiguous
@@ -219,20 +222,21 @@ __global__ __launch_bounds__(kBlock) void splitk_reduce_kernel(const float* __re
   }
 }
 
-// y[i] *= s[0]  (bf16 tensor scaled by a device scalar; no host sync)
+// y[i] *= s[0]  (16-bit tensor scaled by a device scalar; no host sync)
+template <bool H = false>
 __global__ __launch_bounds__(kBlock) void scale_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                            const float* __restrict__ s, int64_t n) {
   const float sc = s[0];
   const int64_t nv = n / 8;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
     float f[8];
-    load8(x + i * 8, f);
+    load8e<H>(x + i * 8, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] *= sc;
-    store8(y + i * 8, f);
+    store8e<H>(y + i * 8, f);
   }
   for (int64_t i = nv * 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
-    y[i] = f2bf(bf2f(x[i]) * sc);
+    y[i] = f2e<H>(e2f<H>(x[i]) * sc);
 }
 
 }  // namespace
@@ -257,20 +261,34 @@ NSA_API int nsa_ew_set_nt(int on) {
   return prev;
 }
 
-NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
+template <bool H>
+static hipError_t gelu_fwd_entry(const void* x, void* y, int64_t n, hipStream_t s) {
   if (ew_nt() && n * 2 >= NSA_NT_MIN_BYTES)
-    gelu_fwd_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
+    gelu_fwd_kernel<true, H><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
   else
-    gelu_fwd_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
+    gelu_fwd_kernel<false, H><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n);
   NSA_LAUNCH_CHECK();
 }
-
-NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
+template <bool H>
+static hipError_t gelu_bwd_entry(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
   if (ew_nt() && n * 2 >= NSA_NT_MIN_BYTES)
-    gelu_bwd_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
+    gelu_bwd_kernel<true, H><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
   else
-    gelu_bwd_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n);
+    gelu_bwd_kernel<false, H><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx,
+                                                                  n);
   NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
+  return gelu_fwd_entry<false>(x, y, n, s);
+}
+NSA_API hipError_t nsa_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
+  return gelu_bwd_entry<false>(dy, x, dx, n, s);
+}
+NSA_API hipError_t nsa_gelu_fwd_h(const void* x, void* y, int64_t n, hipStream_t s) {
+  return gelu_fwd_entry<true>(x, y, n, s);
+}
+NSA_API hipError_t nsa_gelu_bwd_h(const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
+  return gelu_bwd_entry<true>(dy, x, dx, n, s);
 }
 
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_ew)
@@ -278,12 +296,15 @@ NSA_API hipError_t nsa_rng_advance_emb(hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_attn(hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_emb_set(uint64_t v, hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_attn_set(uint64_t v, hipStream_t s);
+NSA_API hipError_t nsa_rng_advance_attn_h(hipStream_t s);  // the fp16 attention build's counter
+NSA_API hipError_t nsa_rng_advance_attn_h_set(uint64_t v, hipStream_t s);
 
 // set every translation unit's dropout step counter (start of a run)
 NSA_API hipError_t nsa_rng_set(uint64_t v, hipStream_t s) {
   hipError_t e = nsa_rng_advance_ew_set(v, s);
   if (e == hipSuccess) e = nsa_rng_advance_emb_set(v, s);
   if (e == hipSuccess) e = nsa_rng_advance_attn_set(v, s);
+  if (e == hipSuccess) e = nsa_rng_advance_attn_h_set(v, s);
   return e;
 }
 
@@ -292,13 +313,20 @@ NSA_API hipError_t nsa_rng_advance(hipStream_t s) {
   hipError_t e = nsa_rng_advance_ew(s);
   if (e == hipSuccess) e = nsa_rng_advance_emb(s);
   if (e == hipSuccess) e = nsa_rng_advance_attn(s);
+  if (e == hipSuccess) e = nsa_rng_advance_attn_h(s);
   return e;
 }
 
 NSA_API hipError_t nsa_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t s) {
   const float scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
-  dropout_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, nsa_drop_thresh(p), scale,
-                                                    seed);
+  dropout_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, nsa_drop_thresh(p), scale,
+                                                           seed);
+  NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_dropout_h(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t s) {
+  const float scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
+  dropout_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, nsa_drop_thresh(p), scale,
+                                                          seed);
   NSA_LAUNCH_CHECK();
 }
 
@@ -315,11 +343,19 @@ NSA_API hipError_t nsa_transpose_bf16(const void* src, void* dst, int R, int C, 
 }
 
 NSA_API hipError_t nsa_cast_f32_bf16(const void* x, void* y, int64_t n, hipStream_t s) {
-  cast_f32_bf16_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const float*)x, (bf16_t*)y, n);
+  cast_f32_bf16_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const float*)x, (bf16_t*)y, n);
+  NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_cast_f32_bf16_h(const void* x, void* y, int64_t n, hipStream_t s) {  // fp32 -> fp16
+  cast_f32_bf16_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const float*)x, (bf16_t*)y, n);
   NSA_LAUNCH_CHECK();
 }
 
 NSA_API hipError_t nsa_scale_rows_bf16(const void* x, void* y, const void* scale, int64_t n, hipStream_t s) {
-  scale_bf16_kernel<<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, (const float*)scale, n);
+  scale_bf16_kernel<false><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, (const float*)scale, n);
+  NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_scale_rows_bf16_h(const void* x, void* y, const void* scale, int64_t n, hipStream_t s) {
+  scale_bf16_kernel<true><<<grid_for(n / 8), kBlock, 0, s>>>((const bf16_t*)x, (bf16_t*)y, (const float*)scale, n);
   NSA_LAUNCH_CHECK();
 }

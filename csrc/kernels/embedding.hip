@@ -29,7 +29,7 @@ __device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
-template <typename XT>
+template <typename XT, bool H = false>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx, const bf16_t* __restrict__ wte,
                                                      const bf16_t* __restrict__ wpe, XT* __restrict__ out, int N,
                                                      int T, int C, uint32_t thresh, float scale, uint64_t salt) {
@@ -44,8 +44,8 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
   XT* o = out + (int64_t)row * C;
   for (int c = lane * 8; c < C; c += 512) {
     float fa[8], fp[8];
-    load8(a + c, fa);
-    load8(p + c, fp);
+    load8e<H>(a + c, fa);
+    load8e<H>(p + c, fp);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = fa[j] + fp[j];
@@ -169,13 +169,13 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_det_kernel(const int64_t* __r
   }
 }
 
-template <typename XT>
+template <typename XT, bool H = false>
 hipError_t launch_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T, int C, float p,
                       uint64_t seed, hipStream_t s) {
   if (C % 8 != 0) return hipErrorInvalidValue;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  emb_fwd_kernel<XT><<<(N + 3) / 4, 256, 0, s>>>((const int64_t*)idx, (const bf16_t*)wte, (const bf16_t*)wpe,
+  emb_fwd_kernel<XT, H><<<(N + 3) / 4, 256, 0, s>>>((const int64_t*)idx, (const bf16_t*)wte, (const bf16_t*)wpe,
                                                  (XT*)out, N, T, C, th, scale, seed);
   return hipGetLastError();
 }
@@ -237,6 +237,12 @@ NSA_API hipError_t nsa_embedding_fwd_x32(const void* idx, const void* wte, const
 NSA_API hipError_t nsa_embedding_bwd_x32(const void* idx, const void* dx, void* dwte, void* dwpe, int B, int T,
                                          int C, float p, uint64_t seed, hipStream_t s) {
   return launch_bwd<float>(idx, dx, dwte, dwpe, B, T, C, p, seed, s);
+}
+
+// fp16 weight shadows (dtype float16), fp32 stream; the backward reads only the fp32 stream
+NSA_API hipError_t nsa_embedding_fwd_x32_h(const void* idx, const void* wte, const void* wpe, void* out, int N, int T,
+                                           int C, float p, uint64_t seed, hipStream_t s) {
+  return launch_fwd<float, true>(idx, wte, wpe, out, N, T, C, p, seed, s);
 }
 
 // deterministic backward (order: token positions stably sorted by id, seg: [V + 1] offsets)

@@ -38,7 +38,25 @@
 
 #include <type_traits>
 
+// Element type.  This file is compiled twice: as is (bf16) and by flash_attn_f16.hip with
+// NSA_FA_F16 = 1 (fp16 Q/K/V/O/dO/dQKV and fp16 P / dS operands, nanoGPT's dtype='float16';
+// v_mfma_f32_32x32x16_f16 runs at the bf16 rate).  The fp16 build's entry points carry an
+// _h suffix and share the bf16 build's kernel selection (FlashConfig).
+#ifndef NSA_FA_F16
+#define NSA_FA_F16 0
+#endif
+#if NSA_FA_F16
+#define NSA_FA_SYM(name) name##_h
+#else
+#define NSA_FA_SYM(name) name
+#endif
+constexpr bool kFaH = NSA_FA_F16 != 0;
+
 namespace {
+
+// one f32 -> an operand-fragment element; a fragment element -> f32
+__device__ __forceinline__ __bf16 fa_elt(float v) { return f2frag<kFaH>(v); }
+__device__ __forceinline__ float fa_f(__bf16 v) { return e2f<kFaH>(__builtin_bit_cast(uint16_t, v)); }
 
 constexpr float kLog2e = 1.4426950408889634f;
 #ifndef ATTN_ORDER_DEFAULT
@@ -83,9 +101,7 @@ __device__ __forceinline__ bf16x8 cat_tr(s16x4 a, s16x4 b) {
 
 __device__ __forceinline__ bf16x8 as_frag(uint4 u) { return __builtin_bit_cast(bf16x8, u); }
 
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) { return mfma32e<kFaH>(a, b, c); }
 
 // Workgroup -> (b*H + h, tile) order; tile 0 is a kernel's heaviest (longest causal
 // range), launched first.
@@ -129,6 +145,13 @@ enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
+}  // namespace
+// one selection for both element types: the fp16 build uses the bf16 build's record
+NSA_API void* nsa_flash_config_ptr();
+namespace {
+#if NSA_FA_F16
+FlashConfig& flash_config() { return *static_cast<FlashConfig*>(nsa_flash_config_ptr()); }
+#else
 FlashConfig& flash_config() {
   static FlashConfig c = [] {
     FlashConfig d{FWD_AUTO, BWD_V3, ATTN_ORDER_DEFAULT};
@@ -141,6 +164,7 @@ FlashConfig& flash_config() {
   }();
   return c;
 }
+#endif
 int attn_order_env() { return flash_config().order; }
 
 // accumulator register i of a 32x32 tile holds row (i&3) + 8*(i>>2) + 4*h
@@ -287,7 +311,7 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
         const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
         p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
       }
-      pf[sb][i >> 3][i & 7] = (__bf16)p;
+      pf[sb][i >> 3][i & 7] = fa_elt(p);
     }
   }
   l_i += half_swap_sum(rs);
@@ -460,8 +484,8 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
       for (int g = 0; g < 4; ++g) {
         const int d = 32 * dt + 8 * g + 4 * h;
         uint2 u;
-        u.x = pack2(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
-        u.y = pack2(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
+        u.x = pk2<kFaH>(o[dt][4 * g + 0] * inv_l, o[dt][4 * g + 1] * inv_l);
+        u.y = pk2<kFaH>(o[dt][4 * g + 2] * inv_l, o[dt][4 * g + 3] * inv_l);
         *reinterpret_cast<uint2*>(orow + d) = u;
       }
     }
@@ -548,7 +572,7 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
               ((uint64_t)dr.bh * dr.T + (uint64_t)(qposA + 32 * blk)) * (uint64_t)dr.T + (uint64_t)kpos;
           p = nsa_keep(dr.seed, id, dr.thresh) ? p * dr.scale : 0.0f;
         }
-        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
+        pf[blk][sb][i >> 3][i & 7] = fa_elt(p);
       }
     }
     l_i[blk] += half_swap_sum(rs);
@@ -642,17 +666,27 @@ __device__ __forceinline__ bool fwd_tile5(const char* kt, const char* vt, const 
         }
         const float p = fast_exp2(s);
         if constexpr (NSA_FWD5_ROWSUM == 0) acc[sb] += p;
-        pf[blk][sb][i >> 3][i & 7] = (__bf16)p;
+        pf[blk][sb][i >> 3][i & 7] = fa_elt(p);
       }
       if constexpr (NSA_FWD5_ROWSUM == 1) {
-        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-        const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 2; ++s) {
+          if constexpr (kFaH) {
+            typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+            const f16x8 hv = __builtin_bit_cast(f16x8, pf[blk][sb][s]);
+            const f16x2_t one = __builtin_bit_cast(f16x2_t, 0x3C003C00u);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[sb] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{pf[blk][sb][s][2 * e], pf[blk][sb][s][2 * e + 1]}, one,
-                                                      acc[sb], false);
+            for (int e = 0; e < 4; ++e)
+              acc[sb] = __builtin_amdgcn_fdot2(f16x2_t{hv[2 * e], hv[2 * e + 1]}, one, acc[sb], false);
+          } else {
+            typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+            const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[sb] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{pf[blk][sb][s][2 * e], pf[blk][sb][s][2 * e + 1]},
+                                                        one, acc[sb], false);
+          }
+        }
       }
     }
     rs[blk] = half_swap_sum(acc[0] + acc[1]);
@@ -743,7 +777,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 raw = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
 #pragma unroll
-      for (int e = 0; e < 8; ++e) qf[blk][ks][e] = NSA_FWD5_QSCALE ? (__bf16)((float)raw[e] * scale_log2) : raw[e];
+      for (int e = 0; e < 8; ++e) qf[blk][ks][e] = NSA_FWD5_QSCALE ? fa_elt(fa_f(raw[e]) * scale_log2) : raw[e];
     }
   }
   f32x16 o[2][2];
@@ -829,8 +863,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
         for (int g = 0; g < 4; ++g) {
           const int d = 32 * dt + 8 * g + 4 * h;
           uint2 u;
-          u.x = pack2(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
-          u.y = pack2(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
+          u.x = pk2<kFaH>(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
+          u.y = pk2<kFaH>(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
           *reinterpret_cast<uint2*>(orow + d) = u;
         }
       }
@@ -1032,8 +1066,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
         for (int g = 0; g < 4; ++g) {
           const int d = 32 * dt + 8 * g + 4 * h;
           uint2 u;
-          u.x = pack2(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
-          u.y = pack2(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
+          u.x = pk2<kFaH>(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
+          u.y = pk2<kFaH>(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
           *reinterpret_cast<uint2*>(orow + d) = u;
         }
       }
@@ -1062,8 +1096,8 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
   const int t = bt % T, b = bt / T;
   const int64_t off = bt * C + hh * D + sub * 8;
   float a[8], g[8];
-  load8(o + off, a);
-  load8(dout + off, g);
+  load8e<kFaH>(o + off, a);
+  load8e<kFaH>(dout + off, g);
   float s = 0.0f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += a[j] * g[j];
@@ -1110,8 +1144,8 @@ __device__ __forceinline__ void bwd_probs(const f32x16& sacc, const f32x16& dpac
         pd = keep ? p * dr.scale : 0.0f;
         dp = keep ? dp * dr.scale : 0.0f;
       }
-      pfr[i >> 3][i & 7] = (__bf16)pd;
-      dsfr[i >> 3][i & 7] = (__bf16)(p * (dp - dlv[e]));
+      pfr[i >> 3][i & 7] = fa_elt(pd);
+      dsfr[i >> 3][i & 7] = fa_elt(p * (dp - dlv[e]));
     }
   }
 }
@@ -1270,10 +1304,10 @@ __global__ __launch_bounds__(BwdGeo<D>::NW * 64, 2) void flash_bwd_kernel(
       for (int g = 0; g < 4; ++g) {
         const int d = 32 * dt + 8 * g + 4 * h;
         uint2 uk, uv;
-        uk.x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
-        uk.y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
-        uv.x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
-        uv.y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        uk.x = pk2<kFaH>(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+        uk.y = pk2<kFaH>(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        uv.x = pk2<kFaH>(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+        uv.y = pk2<kFaH>(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
         *reinterpret_cast<uint2*>(krow + d) = uk;
         *reinterpret_cast<uint2*>(vrow + d) = uv;
       }
@@ -1327,7 +1361,7 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
         const uint64_t id = ((uint64_t)dr.bh * dr.T + (uint64_t)qpos) * (uint64_t)dr.T + (uint64_t)kpos;
         dp = nsa_keep(dr.seed, id, dr.thresh) ? dp * dr.scale : 0.0f;
       }
-      dsf[i >> 3][i & 7] = (__bf16)(p * (dp - dlt));
+      dsf[i >> 3][i & 7] = fa_elt(p * (dp - dlt));
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1438,8 +1472,8 @@ __global__ __launch_bounds__(256, NSA_DQK_OCC) void flash_bwd_dq_kernel(
       for (int g = 0; g < 4; ++g) {
         const int d = 32 * dt + 8 * g + 4 * h;
         uint2 u;
-        u.x = pack2(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
-        u.y = pack2(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
+        u.x = pk2<kFaH>(dq[dt][4 * g + 0] * scale, dq[dt][4 * g + 1] * scale);
+        u.y = pk2<kFaH>(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale);
         *reinterpret_cast<uint2*>(qrow + d) = u;
       }
     }
@@ -1490,9 +1524,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // two f32 -> one dword of two bf16 (v_cvt_pk_bf16_f32, RNE)
-__device__ __forceinline__ uint32_t cvt2(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
-}
+__device__ __forceinline__ uint32_t cvt2(float a, float b) { return pk2<kFaH>(a, b); }
 
 // 16 accumulator values -> the two bf16x8 operand fragments (k-steps 0 and 1)
 __device__ __forceinline__ void pack16(const float (&v)[16], bf16x8 (&f)[2]) {
@@ -1858,10 +1890,13 @@ __device__ __forceinline__ void dq2_tile(const char* kt, const char* vt, const b
 
 #ifndef NSA_DQ2_NS
 #define NSA_DQ2_NS 4  // LDS ring slots of the v2 dQ kernel (NS - 1 tiles in flight)
+#ifndef NSA_DQ2_OCC
+#define NSA_DQ2_OCC 2  // waves per SIMD the v2 dQ kernel is compiled for
+#endif
 #endif
 
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
+__global__ __launch_bounds__(256, NSA_DQ2_OCC) void flash_bwd_dq2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
     const float* __restrict__ lse, float* __restrict__ nls, float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B,
     int T, int H, float scale, float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
@@ -1930,8 +1965,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq2_kernel(
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     float fo[8], fg[8];
-    load8(o + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h, fo);
-    unpack8(__builtin_bit_cast(uint4, gf[ks]), fg);
+    load8e<kFaH>(o + ((int64_t)b * T + qc) * C + hh * D + 16 * ks + 8 * h, fo);
+    unpack8e<kFaH>(__builtin_bit_cast(uint4, gf[ks]), fg);
 #pragma unroll
     for (int e = 0; e < 8; ++e) dpart += fo[e] * fg[e];
   }
@@ -2021,7 +2056,7 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     const int sel = flash_config().fwd;
     const bool v3 = sel == FWD_V3 || sel == FWD_V4 || sel == FWD_V5 ||
                     (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
-    if (v3 && sel == FWD_V5 && !th) {
+    if (v3 && sel == FWD_V5 && !th && !kFaH) {  // (fp16 P cannot hold v5's m = 0 range: v4 instead)
       flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                       scale * kLog2e, order);
       return hipGetLastError();
@@ -2140,7 +2175,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
 // Backward with a 2 x [B, H, T] fp32 workspace.  D = 64 with T % 32 == 0 runs the v2
 // kernels (unless the bwd variant is v1); every other shape the generic backward with
 // ws[0] as delta.
-NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
+NSA_API hipError_t NSA_FA_SYM(nsa_flash_bwd2)(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
   if (D == 64 && T % 32 == 0 && flash_config().bwd >= BWD_V2)
@@ -2153,16 +2188,17 @@ NSA_API hipError_t nsa_flash_bwd2(const void* qkv, const void* o, const void* do
   }
 }
 
-NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_attn)
+#define NSA_FA_RNG(NAME) NSA_DEFINE_RNG_ADVANCE(NAME)
+NSA_FA_RNG(NSA_FA_SYM(nsa_rng_advance_attn))
 
-#if NSA_FWD3_STAMPS
+#if NSA_FWD3_STAMPS && !NSA_FA_F16
 NSA_API hipError_t nsa_fwd3_stamps(void* host, int64_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd3_stamps), (size_t)n * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost);
 }
 #endif
 
-NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
+NSA_API hipError_t NSA_FA_SYM(nsa_flash_fwd)(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {
   switch (D) {
     case 32: return fwd_launch<32>(qkv, out, lse, B, T, H, scale, p, seed, s);
@@ -2171,6 +2207,9 @@ NSA_API hipError_t nsa_flash_fwd(const void* qkv, void* out, void* lse, int B, i
     default: return hipErrorInvalidValue;
   }
 }
+
+#if !NSA_FA_F16
+NSA_API void* nsa_flash_config_ptr() { return &flash_config(); }
 
 // Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5, bwd 1 v1 / 2 v2 / 3 v3, order
 // 0 / 1; a negative value keeps the current setting.  Returns the previous selection as
@@ -2183,3 +2222,4 @@ NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   if (order >= 0 && order <= 2) c.order = order;
   return prev;
 }
+#endif  // !NSA_FA_F16

@@ -153,7 +153,7 @@ constexpr int R64_SLOT = 2 * R64_SLOT_A;  // A + B
 constexpr int R64_SMEM = 2 * R64_SLOT > EP_BYTES ? 2 * R64_SLOT : EP_BYTES;
 static_assert(R64_SMEM <= 163840, "LDS budget");
 
-template <int EPI>
+template <int EPI, bool H = false>
 __global__ __launch_bounds__(NTHREADS, 2) void wgrad_ring64_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[R64_SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_ring64_kernel(GemmArgs g) {
   __builtin_amdgcn_s_setprio(1);                                                              \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) {                                            \
     _Pragma("unroll") for (int j = 0; j < FN; ++j)                                            \
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BC[j], af[i], acc[i][j], 0, 0, 0);   \
+      acc[i][j] = mfma16e<H>(BC[j], af[i], acc[i][j]);                                        \
     af[i] = load_frag<BM>((TA), wm * WTM + 16 * i, (KKN), lane);                              \
     if (i < FN) BNX[i] = load_frag<BN>((TB), wn * WTN + 16 * i, (KKN), lane);                 \
   }                                                                                           \
@@ -235,8 +235,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_ring64_kernel(GemmArgs g) {
 // K split over `splits` workgroups per output tile.
 // epi: 1 = fp32 atomic add into C, 4 = split z stores its fp32 partial into C + z*M*ldc
 // (bits 8..15, the round-2 variant selector, are ignored).
-NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
-                            void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t gemm_ring64_entry(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                             void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
   (void)C2;
   (void)U;
   epi &= 0xff;
@@ -255,7 +257,18 @@ NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const v
   a.tiles_m = (M + BM - 1) / BM;
   a.tiles_n = (N + BN - 1) / BN;
   const dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  if (epi == EPI_ATOMIC_F32) wgrad_ring64_kernel<EPI_ATOMIC_F32><<<grid, NTHREADS, 0, s>>>(a);
-  else wgrad_ring64_kernel<EPI_STORE_F32><<<grid, NTHREADS, 0, s>>>(a);
+  if (epi == EPI_ATOMIC_F32) wgrad_ring64_kernel<EPI_ATOMIC_F32, H><<<grid, NTHREADS, 0, s>>>(a);
+  else wgrad_ring64_kernel<EPI_STORE_F32, H><<<grid, NTHREADS, 0, s>>>(a);
   return hipGetLastError();
+}
+}  // namespace
+
+NSA_API hipError_t nsa_gemm(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                            void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
+  return gemm_ring64_entry<false>(layout, epi, A, lda, B, ldb, C, ldc, C2, U, M, N, K, splits, s);
+}
+// fp16 A / B
+NSA_API hipError_t nsa_gemm_h(int layout, int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                              void* C2, const void* U, int M, int N, int K, int splits, hipStream_t s) {
+  return gemm_ring64_entry<true>(layout, epi, A, lda, B, ldb, C, ldc, C2, U, M, N, K, splits, s);
 }

@@ -116,12 +116,17 @@ __device__ __forceinline__ void q_for(F&& f, std::integer_sequence<int, Is...>) 
   (f(QI<Is>{}), ...);
 }
 
+// H: fp16 operands (v_mfma_f32_16x16x32_f16, the same cycles); the fragments are raw bits
+template <bool H>
 __device__ __forceinline__ void q_mfma(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // first k-step of an output tile: the accumulator starts from 0 (no zeroing pass)
+template <bool H>
 __device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+  if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
 }
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
@@ -290,7 +295,7 @@ __device__ __forceinline__ float q_rowsum16(float v) {
 //       columns into part[2 tile_n + wn][row] (plain stores, one writer per slot: no atomics);
 //  XDX  (dX = dlogits · W): out = g (acc / S_row - W[t_row]) in fp32 before the one rounding,
 //       i.e. (softmax - onehot) · W without a dlogits tensor (ignored rows: 1/S = 0, no W row).
-template <int EPI, bool NT, bool BIAS, bool NOSTORE = false>
+template <int EPI, bool NT, bool BIAS, bool NOSTORE = false, bool H = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
                                            int lane, const char* tab) {
   int m0, n0, mlo, nlo;
@@ -300,7 +305,7 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
   const int col = n0 + wn * 128 + 8 * r;
   const int row0 = m0 + wm * 128 + 4 * q;
   float bv[8];
-  if constexpr (BIAS) load8(g.bias + col, bv);
+  if constexpr (BIAS) load8e<H>(g.bias + col, bv);
   // EPI_DGELU: the U pieces of two fragment rows are in flight at a time
   q_u32x4 uv[2][4];
   auto load_u = [&](int i, q_u32x4 (&dst)[4]) {
@@ -384,18 +389,18 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           }
         } else if constexpr (BIAS) {
 #pragma unroll
-          for (int h = 0; h < 4; ++h) w[h] = q_pk(acc[i][2 * h][e] + bv[2 * h], acc[i][2 * h + 1][e] + bv[2 * h + 1]);
+          for (int h = 0; h < 4; ++h)
+            w[h] = pk2<H>(acc[i][2 * h][e] + bv[2 * h], acc[i][2 * h + 1][e] + bv[2 * h + 1]);
         } else {
 #pragma unroll
-          for (int h = 0; h < 4; ++h) w[h] = q_pk(acc[i][2 * h][e], acc[i][2 * h + 1][e]);
+          for (int h = 0; h < 4; ++h) w[h] = pk2<H>(acc[i][2 * h][e], acc[i][2 * h + 1][e]);
         }
         if constexpr (EPI == Q_EPI_DGELU) {
           // U holds gelu'(u) as fp16 pairs (written by the forward's GELU epilogue)
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            const nsa_f32x2 a = nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)} *
-                                nsa_unpk_f16(uv[i & 1][e][h]);
-            w[h] = q_pk(a.x, a.y);
+            const nsa_f32x2 a = nsa_f32x2{lo2f<H>(w[h]), hi2f<H>(w[h])} * nsa_unpk_f16(uv[i & 1][e][h]);
+            w[h] = pk2<H>(a.x, a.y);
           }
         }
         if constexpr (EPI == Q_EPI_GELU) {
@@ -412,7 +417,8 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
             ia[h] = 4u * (t0 + ((b >> 15) & 1u) * (uint32_t)Q_GTAB_N);
             ib[h] = 4u * (t1 + (b >> 31) * (uint32_t)Q_GTAB_N);
           }
-          if (NSA_NT4_GTAB && __builtin_amdgcn_ballot_w64(oob) == 0) {
+          // the table is indexed by bf16 bit patterns: fp16 outputs take the arithmetic path
+          if (NSA_NT4_GTAB && !H && __builtin_amdgcn_ballot_w64(oob) == 0) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
               const uint32_t ea = *reinterpret_cast<const uint32_t*>(tab + ia[h]);
@@ -424,9 +430,8 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
               nsa_f32x2 gv, dv;
-              nsa_gelu_and_grad2(nsa_f32x2{__uint_as_float(w[h] << 16), __uint_as_float(w[h] & 0xffff0000u)}, gv,
-                                 dv);
-              gg[h] = q_pk(gv.x, gv.y);
+              nsa_gelu_and_grad2(nsa_f32x2{lo2f<H>(w[h]), hi2f<H>(w[h])}, gv, dv);
+              gg[h] = pk2<H>(gv.x, gv.y);
               gp[h] = nsa_pk_f16(dv.x, dv.y);
             }
           }
@@ -465,9 +470,9 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 // build_variant library): 1 = no DMA after the prologue, 2 = no wait for the previous
 // K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue at all, 5 = epilogue
 // arithmetic without its stores
-template <int EPI, bool NT, int PROBE, bool BIAS = false>
+template <int EPI, bool NT, int PROBE, bool BIAS = false, bool H = false>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
-  __shared__ __attribute__((aligned(16))) char smem[Q_SMEM + (EPI == Q_EPI_GELU ? Q_GTAB_BYTES : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[Q_SMEM + (EPI == Q_EPI_GELU && !H ? Q_GTAB_BYTES : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -483,7 +488,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + v / 8;
   }
   if (v >= g.tiles) return;
-  if constexpr (EPI == Q_EPI_GELU) {  // the GELU table into LDS (before any operand DMA is in flight)
+  if constexpr (EPI == Q_EPI_GELU && !H) {  // the GELU table into LDS (before any operand DMA is in flight)
     const uint4* src = reinterpret_cast<const uint4*>(g.U);
     uint4* dst = reinterpret_cast<uint4*>(smem + Q_SMEM);
     for (int k = threadIdx.x; k < Q_GTAB_BYTES / 16; k += Q_THR) dst[k] = src[k];
@@ -590,10 +595,10 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       constexpr int n = decltype(I)::value;
       constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
       if constexpr (kk == 0) {
-        if constexpr (FIRST) q_mfma0(acc[i][j], a0[i], b0[j]);
-        else q_mfma(acc[i][j], a0[i], b0[j]);
+        if constexpr (FIRST) q_mfma0<H>(acc[i][j], a0[i], b0[j]);
+        else q_mfma<H>(acc[i][j], a0[i], b0[j]);
       } else {
-        q_mfma(acc[i][j], a1[i], b1[j]);
+        q_mfma<H>(acc[i][j], a1[i], b1[j]);
       }
       // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
       // K-tile t+2 spread one per DS MFMAs, then K-tile t+1's k-step-0 fragments
@@ -633,7 +638,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT, BIAS, PROBE == 5>(g, acc, seq, wm, wn, lane, smem + Q_SMEM);
+      q_epilogue<EPI, NT, BIAS, PROBE == 5, H>(g, acc, seq, wm, wn, lane, smem + Q_SMEM);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -676,22 +681,22 @@ void nt4_geometry(Nt4Args& a, int gmsel) {
   a.gm = gmsel ? gmsel : (a.tiles_n <= 4 ? 4 : a.tiles_n <= 16 ? 1 : 8);
 }
 
-template <int E, bool B>
+template <int E, bool B, bool H = false>
 void nt4_launch(const Nt4Args& a, dim3 gr, bool nt, int probe, hipStream_t s) {
 #ifdef NSA_PROBES
   switch (probe) {
-    case 1: gemm_nt4_kernel<E, true, 1, B><<<gr, Q_THR, 0, s>>>(a); return;
-    case 2: gemm_nt4_kernel<E, true, 2, B><<<gr, Q_THR, 0, s>>>(a); return;
-    case 3: gemm_nt4_kernel<E, true, 3, B><<<gr, Q_THR, 0, s>>>(a); return;
-    case 4: gemm_nt4_kernel<E, true, 4, B><<<gr, Q_THR, 0, s>>>(a); return;
-    case 5: gemm_nt4_kernel<E, true, 5, B><<<gr, Q_THR, 0, s>>>(a); return;
+    case 1: gemm_nt4_kernel<E, true, 1, B, H><<<gr, Q_THR, 0, s>>>(a); return;
+    case 2: gemm_nt4_kernel<E, true, 2, B, H><<<gr, Q_THR, 0, s>>>(a); return;
+    case 3: gemm_nt4_kernel<E, true, 3, B, H><<<gr, Q_THR, 0, s>>>(a); return;
+    case 4: gemm_nt4_kernel<E, true, 4, B, H><<<gr, Q_THR, 0, s>>>(a); return;
+    case 5: gemm_nt4_kernel<E, true, 5, B, H><<<gr, Q_THR, 0, s>>>(a); return;
     default: break;
   }
 #else
   (void)probe;
 #endif
-  if (nt) gemm_nt4_kernel<E, true, 0, B><<<gr, Q_THR, 0, s>>>(a);
-  else gemm_nt4_kernel<E, false, 0, B><<<gr, Q_THR, 0, s>>>(a);
+  if (nt) gemm_nt4_kernel<E, true, 0, B, H><<<gr, Q_THR, 0, s>>>(a);
+  else gemm_nt4_kernel<E, false, 0, B, H><<<gr, Q_THR, 0, s>>>(a);
 }
 
 bool nt4_store_nt(int stp, int64_t out_bytes) { return stp == 1 || (stp == 0 && out_bytes >= NSA_NT_MIN_BYTES); }
@@ -703,8 +708,10 @@ bool nt4_store_nt(int stp, int64_t out_bytes) { return stp == 1 || (stp == 0 && 
 // builds only; 1 no DMA, 4 no stores, ...); bits 12-13 store policy: 0 nontemporal above the
 // Infinity Cache, 1 always, 2 never; bits 16-23 row-blocks per tile group, 0 = automatic.
 // grid = persistent workgroups.
-NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
-                                const void* U, const void* bias, int M, int N, int K, int grid, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t gemm_nt4_entry(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                          const void* U, const void* bias, int M, int N, int K, int grid, hipStream_t s) {
   const int stp = (epi >> 12) & 0x3;
   const int probe = (epi >> 8) & 0xf;
   const int gmsel = (epi >> 16) & 0xff;
@@ -723,7 +730,7 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   a.ldb = ldb;
   a.ldc = ldc;
   if (nt4_check(a, grid) != hipSuccess) return hipErrorInvalidValue;
-  if ((epi == Q_EPI_GELU && (!C2 || !U || (uintptr_t)U % 16)) || (epi == Q_EPI_DGELU && (!U || bias)) ||
+  if ((epi == Q_EPI_GELU && (!C2 || (!U && !H) || (uintptr_t)U % 16)) || (epi == Q_EPI_DGELU && (!U || bias)) ||
       (bias && (uintptr_t)bias % 16))
     return hipErrorInvalidValue;
   nt4_geometry(a, gmsel);
@@ -731,17 +738,29 @@ NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, 
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
   switch (epi) {
     case Q_EPI_BF16:
-      if (bias) nt4_launch<Q_EPI_BF16, true>(a, gr, nt, probe, s);
-      else nt4_launch<Q_EPI_BF16, false>(a, gr, nt, probe, s);
+      if (bias) nt4_launch<Q_EPI_BF16, true, H>(a, gr, nt, probe, s);
+      else nt4_launch<Q_EPI_BF16, false, H>(a, gr, nt, probe, s);
       break;
     case Q_EPI_GELU:
-      if (bias) nt4_launch<Q_EPI_GELU, true>(a, gr, nt, probe, s);
-      else nt4_launch<Q_EPI_GELU, false>(a, gr, nt, probe, s);
+      if (bias) nt4_launch<Q_EPI_GELU, true, H>(a, gr, nt, probe, s);
+      else nt4_launch<Q_EPI_GELU, false, H>(a, gr, nt, probe, s);
       break;
-    case Q_EPI_DGELU: nt4_launch<Q_EPI_DGELU, false>(a, gr, nt, probe, s); break;
+    case Q_EPI_DGELU: nt4_launch<Q_EPI_DGELU, false, H>(a, gr, nt, probe, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+}  // namespace
+
+NSA_API hipError_t nsa_gemm_nt4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                                const void* U, const void* bias, int M, int N, int K, int grid, hipStream_t s) {
+  return gemm_nt4_entry<false>(epi, A, lda, B, ldb, C, ldc, C2, U, bias, M, N, K, grid, s);
+}
+// fp16 operands and outputs (gelu'(u) stays fp16; the GELU epilogue computes instead of
+// looking up, U may be null there)
+NSA_API hipError_t nsa_gemm_nt4_h(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                                  const void* U, const void* bias, int M, int N, int K, int grid, hipStream_t s) {
+  return gemm_nt4_entry<true>(epi, A, lda, B, ldb, C, ldc, C2, U, bias, M, N, K, grid, s);
 }
 
 // Fused cross-entropy, forward: E = exp(A · B^T - c[row]) (bf16, [M, N] at ldc; columns >=

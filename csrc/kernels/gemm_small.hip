@@ -19,7 +19,7 @@ constexpr int S_LD = S_BK + 8;  // LDS row pitch in bf16 (80 B: the 16-B fragmen
 
 enum { S_EPI_BF16 = 0, S_EPI_GELU = 1, S_EPI_DGELU = 2 };
 
-template <int EPI, bool BIAS>
+template <int EPI, bool BIAS, bool H = false>
 __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restrict__ A, int lda,
                                                          const bf16_t* __restrict__ B, int ldb, bf16_t* __restrict__ C,
                                                          bf16_t* __restrict__ C2, int ldc,
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restric
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16e<H>(fa[i], fb[j], acc[i][j]);
   }
   // C/D layout: lane l holds rows 4 (l >> 4) + e, column l & 15 of each 16 x 16 block
 #pragma unroll
@@ -68,19 +68,19 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restric
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn * 32 + j * 16 + (lane & 15);
       if (col >= N) continue;
-      const float bcol = BIAS ? bf2f(bias[col]) : 0.0f;
+      const float bcol = BIAS ? e2f<H>(bias[col]) : 0.0f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + e;
         if (row >= M) continue;
         const int64_t o = (int64_t)row * ldc + col;
         float v = acc[i][j][e] + bcol;
-        if constexpr (EPI == S_EPI_DGELU) v = bf2f(f2bf(v)) * nsa_h2f(U[o]);  // U = gelu'(u), fp16
-        const bf16_t vb = f2bf(v);
+        if constexpr (EPI == S_EPI_DGELU) v = e2f<H>(f2e<H>(v)) * nsa_h2f(U[o]);  // U = gelu'(u), fp16
+        const bf16_t vb = f2e<H>(v);
         if constexpr (EPI == S_EPI_GELU) {  // C <- gelu'(u) (fp16), C2 <- gelu(u)
-          const float uf = bf2f(vb);
+          const float uf = e2f<H>(vb);
           C[o] = nsa_f2h(nsa_gelu_grad(uf));
-          C2[o] = f2bf(nsa_gelu(uf));
+          C2[o] = f2e<H>(nsa_gelu(uf));
         } else {
           C[o] = vb;
         }
@@ -94,8 +94,10 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const bf16_t* __restric
 // Same contract as nsa_gemm_nt4 (epi 0 bf16, 1 gelu'(u) (fp16) / gelu(u) into C / C2, 2 acc * U with
 // U = gelu'(u) in fp16;
 // optional bias[N]) for any M, N >= 1 and K % 8 == 0 (lda, ldb % 8 == 0, 16-B aligned rows).
-NSA_API hipError_t nsa_gemm_small(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
-                                  const void* U, const void* bias, int M, int N, int K, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t gemm_small_entry(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                            const void* U, const void* bias, int M, int N, int K, hipStream_t s) {
   if (M < 1 || N < 1 || K < 1 || K % 8 || lda % 8 || ldb % 8 || lda < K || ldb < K || ldc < N ||
       (uintptr_t)A % 16 || (uintptr_t)B % 16)
     return hipErrorInvalidValue;
@@ -103,7 +105,7 @@ NSA_API hipError_t nsa_gemm_small(int epi, const void* A, int lda, const void* B
   const dim3 grid((N + S_BN - 1) / S_BN, (M + S_BM - 1) / S_BM);
   const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B, *u = (const bf16_t*)U, *bi = (const bf16_t*)bias;
   bf16_t *c = (bf16_t*)C, *c2 = (bf16_t*)C2;
-#define SMALL(E, BI) gemm_small_kernel<E, BI><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, c2, ldc, u, bi, M, N, K)
+#define SMALL(E, BI) gemm_small_kernel<E, BI, H><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, c2, ldc, u, bi, M, N, K)
   switch (epi) {
     case S_EPI_BF16:
       if (bias) SMALL(S_EPI_BF16, true);
@@ -118,4 +120,15 @@ NSA_API hipError_t nsa_gemm_small(int epi, const void* A, int lda, const void* B
   }
 #undef SMALL
   return hipGetLastError();
+}
+}  // namespace
+
+NSA_API hipError_t nsa_gemm_small(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* C2,
+                                  const void* U, const void* bias, int M, int N, int K, hipStream_t s) {
+  return gemm_small_entry<false>(epi, A, lda, B, ldb, C, ldc, C2, U, bias, M, N, K, s);
+}
+// fp16 operands / outputs
+NSA_API hipError_t nsa_gemm_small_h(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                    void* C2, const void* U, const void* bias, int M, int N, int K, hipStream_t s) {
+  return gemm_small_entry<true>(epi, A, lda, B, ldb, C, ldc, C2, U, bias, M, N, K, s);
 }

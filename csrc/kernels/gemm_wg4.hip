@@ -61,11 +61,15 @@ __device__ __forceinline__ void w_for(F&& f) {
   w_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+template <bool H>
 __device__ __forceinline__ void w_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+  if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
+template <bool H>
 __device__ __forceinline__ void w_mfma0(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+  if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
 }
 __device__ __forceinline__ void w_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -129,12 +133,22 @@ __device__ __forceinline__ int w_g(int r) { return (r & 3) | (((r >> 3) & 1) << 
 }  // namespace
 
 // sum of a fragment's 8 bf16 values into an f32 (v_dot2c_f32_bf16 against a literal 1.0 pair)
+// (fp16: v_dot2_f32_f16 against 1.0 pairs)
+template <bool H>
 __device__ __forceinline__ float w_sum8(const bf16x8& a, float acc) {
-  typedef __bf16 w_bf16x2 __attribute__((ext_vector_type(2)));
-  const w_bf16x2 one = __builtin_bit_cast(w_bf16x2, 0x3F803F80u);
+  if constexpr (H) {
+    typedef _Float16 w_f16x2 __attribute__((ext_vector_type(2)));
+    const f16x8 h = __builtin_bit_cast(f16x8, a);
+    const w_f16x2 one = __builtin_bit_cast(w_f16x2, 0x3C003C00u);
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
-    acc = __builtin_amdgcn_fdot2_f32_bf16(w_bf16x2{a[2 * e], a[2 * e + 1]}, one, acc, false);
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_fdot2(w_f16x2{h[2 * e], h[2 * e + 1]}, one, acc, false);
+  } else {
+    typedef __bf16 w_bf16x2 __attribute__((ext_vector_type(2)));
+    const w_bf16x2 one = __builtin_bit_cast(w_bf16x2, 0x3F803F80u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      acc = __builtin_amdgcn_fdot2_f32_bf16(w_bf16x2{a[2 * e], a[2 * e + 1]}, one, acc, false);
+  }
   return acc;
 }
 
@@ -146,7 +160,7 @@ __device__ __forceinline__ float w_sum8(const bf16x8& a, float acc) {
 // fragments i with i % 2 == wn (4 v_dot2c per fragment, in MFMA gaps).  Each wave ends
 // with one atomic add per column it summed.  (All sums in the first column block's wn = 0
 // waves measured +16-18 % on that kernel: the slowest workgroup sets a one-round grid.)
-template <int EPI, bool BG = false>
+template <int EPI, bool BG = false, bool H = false>
 __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
   __shared__ __attribute__((aligned(16))) char smem[W_SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -282,13 +296,13 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
       constexpr int n = decltype(I)::value;
       constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
       if constexpr (kk == 0) {
-        if constexpr (FIRST) w_mfma0(acc[i][j], b0[j], a0[i]);
-        else w_mfma(acc[i][j], b0[j], a0[i]);
+        if constexpr (FIRST) w_mfma0<H>(acc[i][j], b0[j], a0[i]);
+        else w_mfma<H>(acc[i][j], b0[j], a0[i]);
       } else {
-        w_mfma(acc[i][j], b1[j], a1[i]);
+        w_mfma<H>(acc[i][j], b1[j], a1[i]);
       }
       if constexpr (BG && j == 1) {  // the fragment the previous slot's MFMA read
-        if (do_bg && (i & 1) == wn) bsum[i] = w_sum8(kk == 0 ? a0[i] : a1[i], bsum[i]);
+        if (do_bg && (i & 1) == wn) bsum[i] = w_sum8<H>(kk == 0 ? a0[i] : a1[i], bsum[i]);
       }
       // k-step 1 fragments of this buffer, one transposed read per MFMA
       if constexpr (n < 32) {
@@ -396,14 +410,11 @@ __global__ __launch_bounds__(W_THR, 1) void wgrad4_kernel(Wg4Args g) {
 // epi: 1 = fp32 atomic add into C, 4 = split z stores its partial into C + z*M*ldc.
 // M, N >= 256, M % 8 == N % 8 == 0, K % 64 == 0, splits <= K / 64.
 // gb (optional, epi 1 only): the bias gradient gb[m] += sum_k A[k][m], fused (see BG).
-NSA_API hipError_t nsa_gemm_wgrad4b(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* gb,
-                                    int M, int N, int K, int splits, hipStream_t s);
-NSA_API hipError_t nsa_gemm_wgrad4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M,
-                                   int N, int K, int splits, hipStream_t s) {
-  return nsa_gemm_wgrad4b(epi, A, lda, B, ldb, C, ldc, nullptr, M, N, K, splits, s);
-}
-NSA_API hipError_t nsa_gemm_wgrad4b(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* gb,
-                                    int M, int N, int K, int splits, hipStream_t s) {
+// (the _h entry points take fp16 A / B)
+namespace {
+template <bool H>
+hipError_t wgrad4_entry(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* gb, int M,
+                        int N, int K, int splits, hipStream_t s) {
   if (gb && epi != W_EPI_ATOMIC) return hipErrorInvalidValue;
   if ((epi != W_EPI_ATOMIC && epi != W_EPI_STORE) || M < W_BM || N < W_BN || M % 8 || N % 8 || K % W_BK ||
       splits < 1 || splits > K / W_BK || lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N)
@@ -425,8 +436,26 @@ NSA_API hipError_t nsa_gemm_wgrad4b(int epi, const void* A, int lda, const void*
   a.splits = splits;
   const dim3 grid(a.tiles_m * a.tiles_n * splits);
   a.gb = (float*)gb;
-  if (gb) wgrad4_kernel<W_EPI_ATOMIC, true><<<grid, W_THR, 0, s>>>(a);
-  else if (epi == W_EPI_ATOMIC) wgrad4_kernel<W_EPI_ATOMIC><<<grid, W_THR, 0, s>>>(a);
-  else wgrad4_kernel<W_EPI_STORE><<<grid, W_THR, 0, s>>>(a);
+  if (gb) wgrad4_kernel<W_EPI_ATOMIC, true, H><<<grid, W_THR, 0, s>>>(a);
+  else if (epi == W_EPI_ATOMIC) wgrad4_kernel<W_EPI_ATOMIC, false, H><<<grid, W_THR, 0, s>>>(a);
+  else wgrad4_kernel<W_EPI_STORE, false, H><<<grid, W_THR, 0, s>>>(a);
   return hipGetLastError();
+}
+}  // namespace
+
+NSA_API hipError_t nsa_gemm_wgrad4b(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, void* gb,
+                                    int M, int N, int K, int splits, hipStream_t s) {
+  return wgrad4_entry<false>(epi, A, lda, B, ldb, C, ldc, gb, M, N, K, splits, s);
+}
+NSA_API hipError_t nsa_gemm_wgrad4(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M,
+                                   int N, int K, int splits, hipStream_t s) {
+  return wgrad4_entry<false>(epi, A, lda, B, ldb, C, ldc, nullptr, M, N, K, splits, s);
+}
+NSA_API hipError_t nsa_gemm_wgrad4b_h(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                      void* gb, int M, int N, int K, int splits, hipStream_t s) {
+  return wgrad4_entry<true>(epi, A, lda, B, ldb, C, ldc, gb, M, N, K, splits, s);
+}
+NSA_API hipError_t nsa_gemm_wgrad4_h(int epi, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M,
+                                     int N, int K, int splits, hipStream_t s) {
+  return wgrad4_entry<true>(epi, A, lda, B, ldb, C, ldc, nullptr, M, N, K, splits, s);
 }

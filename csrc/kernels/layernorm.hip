@@ -92,8 +92,8 @@ __device__ __forceinline__ Raw8<T> ld_raw_n(const T* p) {
   for (int i = 0; i < Raw8<T>::W; ++i) r.u[i] = ld16n<NT>(reinterpret_cast<const uint4*>(p) + i);
   return r;
 }
-template <bool NT>
-__device__ __forceinline__ void load8n(const bf16_t* p, float (&f)[8]) { unpack8(ld16n<NT>(p), f); }
+template <bool NT, bool H = false>
+__device__ __forceinline__ void load8n(const bf16_t* p, float (&f)[8]) { unpack8e<H>(ld16n<NT>(p), f); }
 template <bool NT>
 __device__ __forceinline__ void load8xn(const bf16_t* p, float (&f)[8]) { load8n<NT>(p, f); }
 template <bool NT>
@@ -113,7 +113,8 @@ __device__ __forceinline__ void store8xn(float* p, const float (&f)[8]) {
 __device__ __forceinline__ float as_stream(float v, bf16_t*) { return bf2f(f2bf(v)); }
 __device__ __forceinline__ float as_stream(float v, float*) { return v; }
 
-template <int NK, typename XT, bool NT = false>
+// H: the 16-bit tensors (branch, weights, output) are fp16 (dtype float16; fp32 stream only)
+template <int NK, typename XT, bool NT = false, bool H = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, const bf16_t* __restrict__ res,
                                                     XT* __restrict__ sum_out, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
       load8xn<NT>(xr + c, v[k]);
       if (res) {  // fused residual add: s = x + res, written out (XT) and normalised
         float rv[8];
-        load8n<NT>(res + (int64_t)row * C + c, rv);
+        load8n<NT, H>(res + (int64_t)row * C + c, rv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = as_stream(v[k][j] + rv[j], (XT*)nullptr);
         store8xn<NT>(sum_out + (int64_t)row * C + c, v[k]);
@@ -163,16 +164,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
     const int c = (k * 64 + lane) * 8;
     if (c < C) {
       float wf[8], bfv[8], o[8];
-      load8(w + c, wf);
+      load8e<H>(w + c, wf);
       if (b) {
-        load8(b + c, bfv);
+        load8e<H>(b + c, bfv);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bfv[j] = 0.0f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * wf[j] + bfv[j];
-      store8(y + (int64_t)row * C + c, o);
+      store8e<H>(y + (int64_t)row * C + c, o);
     }
   }
   if (lane == 0) {
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
 // per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
 // xhat and dy*w are recomputed from the raw words in the second pass rather than
 // kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
-template <int NK, bool PIPE, typename XT, bool NT = false>
+template <int NK, bool PIPE, typename XT, bool NT = false, bool H = false>
 __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const XT* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
                                                     const float* __restrict__ rstd_in, const XT* __restrict__ dres,
@@ -248,8 +249,8 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
       if (c < C) {
         float xv[8], dv[8], wf[8], aw[8], ab[8];
         unpack_raw(cx[k], xv);
-        unpack8(cd[k], dv);
-        unpack8(wraw[k], wf);
+        unpack8e<H>(cd[k], dv);
+        unpack8e<H>(wraw[k], wf);
         float4* pw = reinterpret_cast<float4*>(accw + c);
         float4* pb = reinterpret_cast<float4*>(accb + c);
         *reinterpret_cast<float4*>(aw) = pw[0];
@@ -279,8 +280,8 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
       if (c < C) {
         float xv[8], dv[8], wf[8], o[8];
         unpack_raw(cx[k], xv);
-        unpack8(cd[k], dv);
-        unpack8(wraw[k], wf);
+        unpack8e<H>(cd[k], dv);
+        unpack8e<H>(wraw[k], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[j] * wf[j] - m1 - (xv[j] - mean) * rstd * m2);
         if (dres) {  // gradient arriving through the residual path of the fused add
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
         store8xn<NT>(dx + (int64_t)row * C + c, o);
-        if (dx_branch) store8(dx_branch + (int64_t)row * C + c, o);  // bf16 copy for the branch GEMMs
+        if (dx_branch) store8e<H>(dx_branch + (int64_t)row * C + c, o);  // 16-bit copy for the branch GEMMs
       }
     }
   }
@@ -317,21 +318,21 @@ int& ln_nt_flag() {  // resolved once from NSA_LN_NT (0 = plain); nsa_ln_set_nt 
 }
 bool ln_nt() { return ln_nt_flag() != 0; }
 
-template <int NK, typename XT>
+template <int NK, typename XT, bool H = false>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
                       void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
   if (ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
-    ln_fwd_kernel<NK, XT, true><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
+    ln_fwd_kernel<NK, XT, true, H><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
                                                             (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
                                                             (float*)mean, (float*)rstd, N, C, eps);
   else
-    ln_fwd_kernel<NK, XT, false><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
+    ln_fwd_kernel<NK, XT, false, H><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
                                                              (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
                                                              (float*)mean, (float*)rstd, N, C, eps);
   return hipGetLastError();
 }
 
-template <int NK, typename XT>
+template <int NK, typename XT, bool H = false>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd,
                       const void* dres, void* dx, void* dx_branch, void* dw_part, void* db_part, int N, int C,
                       int nblk, hipStream_t s) {
@@ -339,15 +340,15 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* 
   const bool pipe = !(nblk & (1 << 30));
   nblk &= ~(1 << 30);
   if (pipe && ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
-    ln_bwd_kernel<NK, true, XT, true><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+    ln_bwd_kernel<NK, true, XT, true, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
         (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
         (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
   else if (pipe)
-    ln_bwd_kernel<NK, true, XT><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+    ln_bwd_kernel<NK, true, XT, false, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
         (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
         (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
   else
-    ln_bwd_kernel<NK, false, XT><<<nblk, 256, 8 * C * sizeof(float), s>>>(
+    ln_bwd_kernel<NK, false, XT, false, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
         (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
         (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
   return hipGetLastError();
@@ -400,6 +401,21 @@ NSA_API hipError_t nsa_layernorm_bwd_x32(const void* dy, const void* x, const vo
   if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
   NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
                                                         N, C, nblk, s)));
+}
+
+// fp16 branch / weights / output with the fp32 stream (dtype float16)
+NSA_API hipError_t nsa_layernorm_fwd_x32_h(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                                           void* y, void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512,
+                (launch_fwd<K_, float, true>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s)));
+}
+NSA_API hipError_t nsa_layernorm_bwd_x32_h(const void* dy, const void* x, const void* w, const void* mean,
+                                           const void* rstd, const void* dres, void* dx, void* dx_branch,
+                                           void* dw_part, void* db_part, int N, int C, int nblk, hipStream_t s) {
+  if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float, true>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
+                                                              db_part, N, C, nblk, s)));
 }
 
 // set the streaming-store policy of the LayerNorm kernels (on < 0: keep); returns the old one

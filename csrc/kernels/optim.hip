@@ -30,6 +30,7 @@ constexpr int kBlock = 256;
 // dynamic loss-scale state slots (float32), mirrored in optim/loss_scale.py
 enum { LS_SCALE = 0, LS_TRACKER = 1, LS_FOUND = 2, LS_SKIPPED = 3, LS_STEP = 4 };
 
+template <bool H = false>  // H: the compute shadow is fp16 (dtype float16)
 __global__ __launch_bounds__(kBlock) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       bf16_t* __restrict__ pb, const uint8_t* __restrict__ wd_mask,
@@ -68,8 +69,8 @@ __global__ __launch_bounds__(kBlock) void adamw_kernel(float* __restrict__ p, co
     reinterpret_cast<float4*>(v)[i] = vv;
     if (pb) {
       uint2 o;
-      o.x = pack2(pp.x, pp.y);
-      o.y = pack2(pp.z, pp.w);
+      o.x = pk2<H>(pp.x, pp.y);
+      o.y = pk2<H>(pp.z, pp.w);
       reinterpret_cast<uint2*>(pb)[i] = o;
     }
   }
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict_
 // Bias gradient, first stage: partial[b][c] = sum over row slice b of dy[r][c] (bf16 in, fp32
 // sums).  Block = 4 row lanes x 64 column chunks of 8 (16-byte loads); the 4 row lanes fold
 // in LDS.  The second stage is colsum_kernel (nsa_colsum_accum[_ordered]) into the gradient.
+template <bool H = false>  // H: dy is fp16
 __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(const bf16_t* __restrict__ dy, int ld, int rows, int C,
                                                             int rows_per_block, float* __restrict__ partial) {
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(const bf16_t* __res
   if (c < C) {
     for (int r = r0 + ry; r < r1; r += 4) {
       float f[8];
-      load8(dy + (int64_t)r * ld + c, f);
+      load8e<H>(dy + (int64_t)r * ld + c, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += f[j];
     }
@@ -223,22 +225,42 @@ NSA_API hipError_t nsa_colsum_bf16_partial(const void* dy, int ld, int rows, int
                                            hipStream_t s) {
   if (C % 8 || ld % 8 || nblk < 1) return hipErrorInvalidValue;
   dim3 grid((C / 8 + 63) / 64, nblk);
-  colsum_bf16_kernel<<<grid, kBlock, 0, s>>>((const bf16_t*)dy, ld, rows, C, (rows + nblk - 1) / nblk,
-                                             (float*)partial);
+  colsum_bf16_kernel<false><<<grid, kBlock, 0, s>>>((const bf16_t*)dy, ld, rows, C, (rows + nblk - 1) / nblk,
+                                                    (float*)partial);
+  NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_colsum_bf16_partial_h(const void* dy, int ld, int rows, int C, void* partial, int nblk,
+                                             hipStream_t s) {
+  if (C % 8 || ld % 8 || nblk < 1) return hipErrorInvalidValue;
+  dim3 grid((C / 8 + 63) / 64, nblk);
+  colsum_bf16_kernel<true><<<grid, kBlock, 0, s>>>((const bf16_t*)dy, ld, rows, C, (rows + nblk - 1) / nblk,
+                                                   (float*)partial);
   NSA_LAUNCH_CHECK();
 }
 
-NSA_API hipError_t nsa_adamw_step(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask,
-                                  int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,
-                                  float bc2_sqrt, const void* coef, const void* ls, hipStream_t s) {
+template <bool H>
+static hipError_t adamw_entry(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask, int64_t n,
+                              float lr, float beta1, float beta2, float eps, float wd, float bc1, float bc2_sqrt,
+                              const void* coef, const void* ls, hipStream_t s) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   int64_t grid = (n4 + kBlock - 1) / kBlock;
   if (grid > 4096) grid = 4096;
-  adamw_kernel<<<(int)grid, kBlock, 0, s>>>((float*)p, (const float*)g, (float*)m, (float*)v, (bf16_t*)p_bf16,
+  adamw_kernel<H><<<(int)grid, kBlock, 0, s>>>((float*)p, (const float*)g, (float*)m, (float*)v, (bf16_t*)p_bf16,
                                             (const uint8_t*)wd_mask, n4, lr, beta1, beta2, eps, wd, lr / bc1,
                                             1.0f / bc2_sqrt, (const float*)coef, (const float*)ls);
   NSA_LAUNCH_CHECK();
+}
+NSA_API hipError_t nsa_adamw_step(void* p, const void* g, void* m, void* v, void* p_bf16, const void* wd_mask,
+                                  int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,
+                                  float bc2_sqrt, const void* coef, const void* ls, hipStream_t s) {
+  return adamw_entry<false>(p, g, m, v, p_bf16, wd_mask, n, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, coef, ls, s);
+}
+// the same with an fp16 compute shadow
+NSA_API hipError_t nsa_adamw_step_h(void* p, const void* g, void* m, void* v, void* p_f16, const void* wd_mask,
+                                    int64_t n, float lr, float beta1, float beta2, float eps, float wd, float bc1,
+                                    float bc2_sqrt, const void* coef, const void* ls, hipStream_t s) {
+  return adamw_entry<true>(p, g, m, v, p_f16, wd_mask, n, lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, coef, ls, s);
 }
 
 // partial holds nblocks floats, 2 * nblocks with a loss scale (ls != null)

@@ -32,7 +32,7 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
   }
 }
 
-template <bool VEC>
+template <bool VEC, bool H = false>
 __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                      float* __restrict__ row_loss, int V, int ld, int write_grad) {
   const int row = blockIdx.x;
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
     const int nv = ld / 8;
     for (int i = threadIdx.x; i < nv; i += kBlock) {
       float f[8];
-      load8(lr + i * 8, f);
+      load8e<H>(lr + i * 8, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = i * 8 + j < V ? f[j] : -INFINITY;
       float bm = f[0];
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
       online_merge(m, s, bm, bs);
     }
   } else {
-    for (int i = threadIdx.x; i < V; i += kBlock) online_merge(m, s, bf2f(lr[i]), 1.0f);
+    for (int i = threadIdx.x; i < V; i += kBlock) online_merge(m, s, e2f<H>(lr[i]), 1.0f);
   }
   // wave reduce of (m, s)
 #pragma unroll
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
     sm[threadIdx.x >> 6] = m;
     ss[threadIdx.x >> 6] = s;
   }
-  if (threadIdx.x == 0) tgt_logit = (tgt >= 0 && tgt < V) ? bf2f(lr[tgt]) : 0.0f;
+  if (threadIdx.x == 0) tgt_logit = (tgt >= 0 && tgt < V) ? e2f<H>(lr[tgt]) : 0.0f;
   __syncthreads();
   float M = sm[0], S = ss[0];
 #pragma unroll
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
     const int nv = ld / 8;
     for (int i = threadIdx.x; i < nv; i += kBlock) {
       float f[8];
-      load8(lr + i * 8, f);
+      load8e<H>(lr + i * 8, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = i * 8 + j;
@@ -93,13 +93,13 @@ __global__ __launch_bounds__(kBlock) void xent_kernel(bf16_t* __restrict__ logit
         if (valid && col == tgt) p -= 1.0f;
         f[j] = p;
       }
-      store8(lr + i * 8, f);
+      store8e<H>(lr + i * 8, f);
     }
   } else {
     for (int i = threadIdx.x; i < V; i += kBlock) {
-      float p = valid ? __expf(bf2f(lr[i]) - M) * invS : 0.0f;
+      float p = valid ? __expf(e2f<H>(lr[i]) - M) * invS : 0.0f;
       if (valid && i == tgt) p -= 1.0f;
-      lr[i] = f2bf(p);
+      lr[i] = f2e<H>(p);
     }
   }
 }
@@ -140,7 +140,7 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // NT bit 0: nontemporal logit loads, bit 1: nontemporal gradient stores + packed
 // v_cvt_pk_bf16_f32 conversion (the logits are streamed exactly once each way)
-template <int RB, int RC, int NT = 0>
+template <int RB, int RC, int NT = 0, bool H = false>
 __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logits,
                                                      const int64_t* __restrict__ targets,
                                                      float* __restrict__ row_loss, int V, int ld,
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
       r[c] = *reinterpret_cast<const uint4*>(lr + (int64_t)i * 8);
     }
   }
-  const float tgt_logit = valid ? bf2f(lr[tgt]) : 0.0f;
+  const float tgt_logit = valid ? e2f<H>(lr[tgt]) : 0.0f;
   float m = -INFINITY;
 #pragma unroll
   for (int c = 0; c < kRegChunks; ++c) {
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
       const int col = ((int)threadIdx.x + c * kBlock) * 8;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float lo = !pad || col + 2 * q < V ? __uint_as_float(w4[q] << 16) : -INFINITY;
-        const float hi = !pad || col + 2 * q + 1 < V ? __uint_as_float(w4[q] & 0xffff0000u) : -INFINITY;
+        const float lo = !pad || col + 2 * q < V ? lo2f<H>(w4[q]) : -INFINITY;
+        const float hi = !pad || col + 2 * q + 1 < V ? hi2f<H>(w4[q]) : -INFINITY;
         m = fmaxf(m, fmaxf(lo, hi));
       }
     }
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
       const int col = ((int)threadIdx.x + c * kBlock) * 8;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float e0 = __expf(__uint_as_float(w4[q] << 16) - M), e1 = __expf(__uint_as_float(w4[q] & 0xffff0000u) - M);
+        const float e0 = __expf(lo2f<H>(w4[q]) - M), e1 = __expf(hi2f<H>(w4[q]) - M);
         s += (!pad || col + 2 * q < V ? e0 : 0.0f) + (!pad || col + 2 * q + 1 < V ? e1 : 0.0f);
       }
     }
@@ -207,20 +207,19 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
       float f[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        f[2 * q] = valid && (!pad || i * 8 + 2 * q < V) ? __expf(__uint_as_float(w4[q] << 16) - M) * invS : 0.0f;
-        f[2 * q + 1] =
-            valid && (!pad || i * 8 + 2 * q + 1 < V) ? __expf(__uint_as_float(w4[q] & 0xffff0000u) - M) * invS : 0.0f;
+        f[2 * q] = valid && (!pad || i * 8 + 2 * q < V) ? __expf(lo2f<H>(w4[q]) - M) * invS : 0.0f;
+        f[2 * q + 1] = valid && (!pad || i * 8 + 2 * q + 1 < V) ? __expf(hi2f<H>(w4[q]) - M) * invS : 0.0f;
       }
       if (valid && (tgt >> 3) == i) f[tgt & 7] -= 1.0f;
       if constexpr (NT & 2) {
         u32x4_t v;
-        v.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[0], f[1]}, bf16x2_t));
-        v.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[2], f[3]}, bf16x2_t));
-        v.z = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[4], f[5]}, bf16x2_t));
-        v.w = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){f[6], f[7]}, bf16x2_t));
+        v.x = pk2<H>(f[0], f[1]);
+        v.y = pk2<H>(f[2], f[3]);
+        v.z = pk2<H>(f[4], f[5]);
+        v.w = pk2<H>(f[6], f[7]);
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(lr + (int64_t)i * 8));
       } else {
-        store8(lr + (int64_t)i * 8, f);
+        store8e<H>(lr + (int64_t)i * 8, f);
       }
     }
   }
@@ -237,8 +236,10 @@ __global__ __launch_bounds__(RB) void xent_reg_kernel(bf16_t* __restrict__ logit
 // Rows are `ld` apart; columns >= V (vocabulary padding, ld > V) are excluded and get a
 // zero gradient.  Since round 4 this separate pass serves deterministic mode and the shapes
 // the fused path (xent_fused.hip) does not take.
-NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int ld,
-                                int write_grad, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t xent_entry(void* logits, const void* targets, void* row_loss, int N, int V, int ld, int write_grad,
+                      hipStream_t s) {
   const int variant = (write_grad >> 8) & 0xff;
   write_grad &= 0xff;
   if (ld < V) return hipErrorInvalidValue;
@@ -248,20 +249,31 @@ NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_los
   const bool vec = ld % 8 == 0;
   if (vec && variant >= 3 && variant <= 5 && ld <= 1024 * 8 * 7) {
     // 3: nontemporal loads + stores, 4: nontemporal stores, 5: nontemporal loads
-    if (variant == 3) xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
-    else if (variant == 4) xent_reg_kernel<1024, 7, 2><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
-    else xent_reg_kernel<1024, 7, 1><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    if (variant == 3) xent_reg_kernel<1024, 7, 3, H><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    else if (variant == 4) xent_reg_kernel<1024, 7, 2, H><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    else xent_reg_kernel<1024, 7, 1, H><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   } else if (vec && variant == 1 && ld <= 256 * 8 * 25)
-    xent_reg_kernel<256, 25><<<N, 256, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_reg_kernel<256, 25, 0, H><<<N, 256, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else if (vec && variant == 2 && ld <= 512 * 8 * 13)
-    xent_reg_kernel<512, 13><<<N, 512, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_reg_kernel<512, 13, 0, H><<<N, 512, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else if (vec && (variant == 6 || (int64_t)N * ld * 2 < NSA_NT_MIN_BYTES) && ld <= 1024 * 8 * 7)
-    xent_reg_kernel<1024, 7, 0><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_reg_kernel<1024, 7, 0, H><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else if (vec && ld <= 1024 * 8 * 7)  // default: nontemporal loads + stores
-    xent_reg_kernel<1024, 7, 3><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_reg_kernel<1024, 7, 3, H><<<N, 1024, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else if (vec)
-    xent_kernel<true><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_kernel<true, H><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   else
-    xent_kernel<false><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
+    xent_kernel<false, H><<<N, kBlock, 0, s>>>(lg, tg, rl, V, ld, write_grad);
   return hipGetLastError();
+}
+}  // namespace
+
+NSA_API hipError_t nsa_xent_fwd(void* logits, const void* targets, void* row_loss, int N, int V, int ld,
+                                int write_grad, hipStream_t s) {
+  return xent_entry<false>(logits, targets, row_loss, N, V, ld, write_grad, s);
+}
+// fp16 logits (dtype float16: autocast's fp16 logits, the softmax and loss in fp32)
+NSA_API hipError_t nsa_xent_fwd_h(void* logits, const void* targets, void* row_loss, int N, int V, int ld,
+                                  int write_grad, hipStream_t s) {
+  return xent_entry<true>(logits, targets, row_loss, N, V, ld, write_grad, s);
 }

@@ -65,9 +65,18 @@ def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
              "-munsafe-fp-atomics", "-I", os.path.join(CSRC, "kernels"), *[f"-D{d}" for d in defines]]
 
+    def deps(src):
+        # sources a kernel file #includes from this directory (flash_attn_f16.hip is
+        # flash_attn.hip compiled again for fp16)
+        out = []
+        for line in open(src):
+            if line.startswith('#include "') and line.rstrip().endswith('.hip"'):
+                out.append(os.path.join(os.path.dirname(src), line.split('"')[1]))
+        return out
+
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-        if force or _newer(obj, [src] + headers):
+        if force or _newer(obj, [src] + headers + deps(src)):
             _run([hipcc, *flags, "-c", src, "-o", obj])
             if verbose:
                 print(f"  [hipcc {ARCH}] {os.path.relpath(src, ROOT)}")

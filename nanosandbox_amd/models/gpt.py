@@ -181,8 +181,9 @@ class GPT(nn.Module):
         fp32 + bf16 residual add promotes to fp32.  bf16 halves the residual bytes
         (opt-in, ``fp32_residual=False``)."""
         self.compute_dtype = dtype
-        # bf16 compute runs our kernels; fp16 (GradScaler) and fp32 compute take the torch
-        # reference path of every op (train.py --dtype), with an fp32 residual stream
+        # bf16 and fp16 (with the dynamic loss scale) compute run our kernels; fp32 compute takes
+        # the torch reference path of every op (train.py --dtype); fp16 / fp32 keep an fp32
+        # residual stream
         self.residual_dtype = residual_dtype if dtype == torch.bfloat16 else torch.float32
         for m in self.modules():
             if isinstance(m, LayerNorm):

@@ -133,11 +133,13 @@ def lib():
                 "`python -m nanosandbox_amd.build` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name, argtypes in _SIGNATURES.items():
-            fn = getattr(L, name, None)
-            if fn is None:
-                continue  # optional entry points (checked at call time)
-            fn.argtypes = argtypes
-            fn.restype = c_int
+            # NAME_h: the fp16 instantiation of an entry point, same C signature
+            for sym in (name, name + "_h"):
+                fn = getattr(L, sym, None)
+                if fn is None:
+                    continue  # optional entry points (checked at call time)
+                fn.argtypes = argtypes
+                fn.restype = c_int
         _lib = L
         return _lib
 

@@ -44,7 +44,14 @@ from . import gemm as _gemm
 from . import gemm_dispatch as _gd
 
 BF16 = torch.bfloat16
+F16 = torch.float16
 F32 = torch.float32
+KDT = (BF16, F16)  # the compute dtypes our kernels take (fp16: nanoGPT dtype='float16')
+
+
+def _sym(name, dtype):
+    """NAME for bf16, NAME_h for the fp16 instantiation of the same kernel."""
+    return name + "_h" if dtype == F16 else name
 
 
 # ----------------------------------------------------------------------------
@@ -83,7 +90,7 @@ def weight_grad(p: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
     fp32 partial tiles straight into the flat gradient (no bf16 dW, no separate
     accumulate pass)."""
     mg = getattr(p, "main_grad", None)
-    if dy2.is_cuda and dy2.dtype == BF16:
+    if dy2.is_cuda and dy2.dtype in KDT:
         dy2 = dy2.contiguous()
         x2 = x2.contiguous()
         if mg is not None:
@@ -104,7 +111,7 @@ def weight_bias_grad(w: torch.Tensor, b, dy2: torch.Tensor, x2: torch.Tensor):
     if b is None:
         return weight_grad(w, dy2, x2), None
     mw, mb = getattr(w, "main_grad", None), getattr(b, "main_grad", None)
-    if dy2.is_cuda and dy2.dtype == BF16 and mw is not None and mb is not None:
+    if dy2.is_cuda and dy2.dtype in KDT and mw is not None and mb is not None:
         _gd.wgrad_acc(dy2.contiguous(), x2.contiguous(), mw, gb32=mb)
         notify_grad_ready(w)
         notify_grad_ready(b)
@@ -118,7 +125,7 @@ def bias_grad(p, dy2: torch.Tensor):
     if p is None:
         return None
     mg = getattr(p, "main_grad", None)
-    if dy2.is_cuda and dy2.dtype == BF16:
+    if dy2.is_cuda and dy2.dtype in KDT:
         dy2 = dy2.contiguous()
         if mg is not None:
             _gd.bias_grad_acc(dy2, mg)
@@ -174,10 +181,11 @@ def _cpu_keep_mask(shape, p, seed, device=None):
 
 
 def _kern(t) -> bool:
-    """Whether an activation runs on our kernels: bf16 on the GPU.  fp32 / fp16 compute on
-    the GPU (``--dtype=float32`` / ``float16``) takes the plain torch reference path of each
-    op (the numerics contract, not the performance path)."""
-    return t.is_cuda and t.dtype == BF16
+    """Whether an activation runs on our kernels: bf16 or fp16 on the GPU (the fp16 kernels
+    are the same sources instantiated with fp16 conversions and v_mfma_*_f16).  fp32 compute
+    on the GPU (``--dtype=float32``) takes the plain torch reference path of each op (the
+    numerics contract, not the performance path)."""
+    return t.is_cuda and t.dtype in KDT
 
 
 class DropoutFn(torch.autograd.Function):
@@ -188,7 +196,7 @@ class DropoutFn(torch.autograd.Function):
         if _kern(x):
             y = torch.empty_like(x)
             xc = x.contiguous()
-            _lib.call("nsa_dropout", _lib.ptr(xc), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
+            _lib.call(_sym("nsa_dropout", x.dtype), _lib.ptr(xc), _lib.ptr(y), x.numel(), p, seed, _lib.stream())
             return y
         mask = _cpu_keep_mask(x.shape, p, seed, x.device)
         return x * mask / (1.0 - p)
@@ -198,7 +206,7 @@ class DropoutFn(torch.autograd.Function):
         if _kern(dy):
             dx = torch.empty_like(dy)
             dyc = dy.contiguous()
-            _lib.call("nsa_dropout", _lib.ptr(dyc), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
+            _lib.call(_sym("nsa_dropout", dy.dtype), _lib.ptr(dyc), _lib.ptr(dx), dy.numel(), ctx.p, ctx.seed,
                       _lib.stream())
             return dx, None
         mask = _cpu_keep_mask(dy.shape, ctx.p, ctx.seed, dy.device)
@@ -222,7 +230,7 @@ class EmbeddingFn(torch.autograd.Function):
         V, C = wte.shape
         seed = new_seed() if p > 0 else 0
         ctx.p, ctx.seed, ctx.shape = p, seed, (B, T, V, C)
-        ctx.kern = idx.is_cuda and cdtype == BF16
+        ctx.kern = idx.is_cuda and cdtype in KDT
         # the kernels index idx as a dense [B*T] array in both passes: save the
         # contiguous copy (a sliced batch such as d[:, :-1] has row stride T+1)
         idx = idx.contiguous()
@@ -231,13 +239,14 @@ class EmbeddingFn(torch.autograd.Function):
             # bf16 weight shadows; the sum (the residual stream) is written in ``dtype``:
             # fp32 (nanoGPT autocast contract) or bf16
             assert C % 8 == 0, "embedding kernel needs n_embd % 8 == 0"
-            assert dtype in (F32, BF16)
+            assert dtype in (F32, BF16) and (cdtype == BF16 or dtype == F32), "fp16 weights take an fp32 stream"
             out = torch.empty(B, T, C, device=idx.device, dtype=dtype)
-            # keep the bf16 weight copies referenced until the launch: without an optimizer's
+            # keep the 16-bit weight copies referenced until the launch: without an optimizer's
             # persistent shadow they are temporaries, and the caching allocator would hand
             # the first one's block to the second before the kernel is enqueued
-            wte_c, wpe_c = compute_weight(wte, BF16), compute_weight(wpe, BF16)
-            _lib.call("nsa_embedding_fwd_x32" if dtype == F32 else "nsa_embedding_fwd", _lib.ptr(idx),
+            wte_c, wpe_c = compute_weight(wte, cdtype), compute_weight(wpe, cdtype)
+            name = _sym("nsa_embedding_fwd_x32", cdtype) if dtype == F32 else "nsa_embedding_fwd"
+            _lib.call(name, _lib.ptr(idx),
                       _lib.ptr(wte_c), _lib.ptr(wpe_c), _lib.ptr(out), B * T, T, C, p, seed, _lib.stream())
             return out
         # fp32 master weights, as nanoGPT's autocast leaves nn.Embedding in fp32
@@ -303,6 +312,8 @@ def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32, cdtype=None):
     takes the fp32 torch path)."""
     if cdtype is None:
         cdtype = BF16 if idx.is_cuda else F32
+    if cdtype not in KDT:
+        cdtype = F32  # fp32 compute: the torch path
     return EmbeddingFn.apply(idx, wte, wpe, p if training else 0.0, dtype, cdtype)
 
 
@@ -344,22 +355,24 @@ class LayerNormFn(torch.autograd.Function):
         ctx.passthrough = passthrough and y is None
         out_dtype = out_dtype or (y.dtype if y is not None else x.dtype)
         ctx.y_dtype = y.dtype if y is not None else None
-        ctx.kern = x.is_cuda and out_dtype == BF16
+        ctx.kern = x.is_cuda and out_dtype in KDT
         if ctx.kern:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
             x32 = x.dtype == F32
-            assert x.dtype in (F32, BF16) and out_dtype == BF16, "layernorm kernel: bf16/fp32 stream, bf16 out"
+            assert x.dtype in (F32, BF16) and (x32 or out_dtype == BF16), \
+                "layernorm kernel: bf16 stream with bf16 out, or fp32 stream with bf16 / fp16 out"
             x2 = x2.contiguous()
             y2 = y.reshape(-1, C).contiguous() if y is not None else None
             if y2 is not None:
-                assert y2.dtype == BF16
+                assert y2.dtype == out_dtype
             s2 = torch.empty_like(x2) if y is not None else None
             h = torch.empty(N, C, device=x.device, dtype=out_dtype)
             mean = torch.empty(N, device=x.device, dtype=F32)
             rstd = torch.empty(N, device=x.device, dtype=F32)
             wc = compute_weight(w, out_dtype)
             bc = compute_weight(b, out_dtype) if b is not None else None
-            _lib.call("nsa_layernorm_fwd_x32" if x32 else "nsa_layernorm_fwd", _lib.ptr(x2), _lib.ptr(y2),
+            _lib.call(_sym("nsa_layernorm_fwd_x32", out_dtype) if x32 else "nsa_layernorm_fwd", _lib.ptr(x2),
+                      _lib.ptr(y2),
                       _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C,
                       LN_EPS, _lib.stream())
             inp = s2 if y is not None else x2
@@ -415,7 +428,7 @@ class LayerNormFn(torch.autograd.Function):
             db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
             wc = compute_weight(w, dy2.dtype)
             if x32:
-                _lib.call("nsa_layernorm_bwd_x32", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
+                _lib.call(_sym("nsa_layernorm_bwd_x32", dy2.dtype), _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
                           _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dyb), _lib.ptr(dw_part),
                           _lib.ptr(db_part), N, C, nblk, _lib.stream())
             else:
@@ -491,7 +504,7 @@ class LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         wc = compute_weight(w, x.dtype)
         bc = compute_weight(b, x.dtype) if b is not None else None
-        if x2.is_cuda and x2.dtype == BF16:
+        if x2.is_cuda and x2.dtype in KDT:
             out = _gd.fwd(x2.contiguous(), wc, bc)
         else:
             out = x2 @ wc.t()
@@ -511,7 +524,7 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             wc = compute_weight(w, d2.dtype)
-            dx = _gd.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype == BF16 else d2 @ wc
+            dx = _gd.dgrad(d2.contiguous(), wc) if d2.is_cuda and d2.dtype in KDT else d2 @ wc
             dx = dx.view(*dout.shape[:-1], x2.shape[-1])
         gw, gb = weight_bias_grad(w, b, d2, x2)
         dres = dout if ctx.has_residual else None
@@ -560,8 +573,8 @@ class MLPFn(torch.autograd.Function):
 
 
 def mlp(x, w_fc, b_fc, w_proj, b_proj):
-    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X (bf16)."""
-    if x.is_cuda and x.dtype == BF16:
+    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X (bf16 / fp16)."""
+    if x.is_cuda and x.dtype in KDT:
         return MLPFn.apply(x, w_fc, b_fc, w_proj, b_proj)
     return linear(gelu(linear(x, w_fc, b_fc)), w_proj, b_proj)
 
@@ -581,7 +594,7 @@ class GeluFn(torch.autograd.Function):
         if _kern(x):
             x = x.contiguous()
             y = torch.empty_like(x)
-            _lib.call("nsa_gelu_fwd", _lib.ptr(x), _lib.ptr(y), x.numel(), _lib.stream())
+            _lib.call(_sym("nsa_gelu_fwd", x.dtype), _lib.ptr(x), _lib.ptr(y), x.numel(), _lib.stream())
             return y
         return F.gelu(x.float()).to(x.dtype)
 
@@ -591,7 +604,7 @@ class GeluFn(torch.autograd.Function):
         if _kern(dy):
             dy = dy.contiguous()
             dx = torch.empty_like(x)
-            _lib.call("nsa_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dx), x.numel(), _lib.stream())
+            _lib.call(_sym("nsa_gelu_bwd", dy.dtype), _lib.ptr(dy), _lib.ptr(x), _lib.ptr(dx), x.numel(), _lib.stream())
             return dx
         xf = x.float()
         cdf = 0.5 * (1.0 + torch.erf(xf * _INV_SQRT2))
@@ -654,8 +667,8 @@ class AttentionFn(torch.autograd.Function):
             qkv = qkv.contiguous()
             y = torch.empty(B, T, C, device=qkv.device, dtype=qkv.dtype)
             lse = torch.empty(B, H, T, device=qkv.device, dtype=F32)
-            _lib.call("nsa_flash_fwd", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, D, scale, p, seed,
-                      _lib.stream())
+            _lib.call(_sym("nsa_flash_fwd", qkv.dtype), _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(lse), B, T, H, D,
+                      scale, p, seed, _lib.stream())
             ctx.save_for_backward(qkv, y, lse)
             return y
         q, k, v = qkv.float().view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
@@ -674,8 +687,9 @@ class AttentionFn(torch.autograd.Function):
             # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
             # dQ is written once, in bf16, by its own kernel (no atomics)
             ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
-            _lib.call("nsa_flash_bwd2", _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse), _lib.ptr(ws),
-                      _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
+            dy = dy.to(qkv.dtype)
+            _lib.call(_sym("nsa_flash_bwd2", qkv.dtype), _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse),
+                      _lib.ptr(ws), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
             return dqkv, None, None
         (qkv,) = ctx.saved_tensors
         with torch.enable_grad():
@@ -921,28 +935,30 @@ def lm_head_rows(V: int) -> int:
     return V if (V % 64 == 0 and V >= 256) else max(256, -(-V // 64) * 64)
 
 
-def _lm_weight(w):
-    """(bf16 [Vpad, C] operand, fp32 [Vpad, C] gradient view or None).  A FlatParamStore keeps
-    padded views of the tied weight (``compute_padded`` / ``main_grad_padded``); otherwise
-    the padded operand is a per-call copy and the gradient is returned to autograd."""
+def _lm_weight(w, dtype=BF16):
+    """(16-bit [Vpad, C] operand in ``dtype``, fp32 [Vpad, C] gradient view or None).  A
+    FlatParamStore keeps padded views of the tied weight (``compute_padded`` /
+    ``main_grad_padded``); otherwise the padded operand is a per-call copy and the gradient is
+    returned to autograd."""
     V, C = w.shape
     Vp = lm_head_rows(V)
     cp = getattr(w, "compute_padded", None)
-    if cp is not None and cp.dtype == BF16:
+    if cp is not None and cp.dtype == dtype:
         return cp, getattr(w, "main_grad_padded", None)
     if Vp == V:
-        return compute_weight(w, BF16), getattr(w, "main_grad", None)
+        return compute_weight(w, dtype), getattr(w, "main_grad", None)
     # no flat store (sample / eval scripts): the padded operand is cached on the weight for
     # its current contents (generation, version, storage), so a token-by-token generate()
     # does not allocate and copy the whole [Vpad, C] table per token; never cached while a
     # HIP graph is being captured (the copy is then part of the graph)
     capturing = w.is_cuda and torch.cuda.is_current_stream_capturing()
-    key = (_gd._weight_gen, w._version, w.data_ptr())
+    key = (_gd._weight_gen, w._version, w.data_ptr(), dtype)
     hit = getattr(w, "_nsa_lm_pad", None)
     if not capturing and hit is not None and hit[0] == key:
         return hit[1], None
-    wp = hit[1] if (hit is not None and not capturing) else torch.zeros(Vp, C, device=w.device, dtype=BF16)
-    wp[:V] = compute_weight(w, BF16)
+    reuse = hit is not None and not capturing and hit[1].dtype == dtype
+    wp = hit[1] if reuse else torch.zeros(Vp, C, device=w.device, dtype=dtype)
+    wp[:V] = compute_weight(w, dtype)
     if not capturing:
         try:
             w._nsa_lm_pad = (key, wp)
@@ -990,13 +1006,15 @@ class LMHeadLossFn(torch.autograd.Function):
         V = w.shape[0]
         ctx.xshape = x.shape
         ctx.V = V
-        if x.is_cuda and x.dtype == BF16:
+        if x.is_cuda and x.dtype in KDT:
             x2 = x2.contiguous()
             t = t.contiguous()
-            wp, _ = _lm_weight(w)
+            wp, _ = _lm_weight(w, x.dtype)
             Vp = wp.shape[0]
             row_loss = torch.empty(N, device=x.device, dtype=F32)
-            ctx.fused = _fused_xent_ok(N, C, Vp)
+            # the fused form keeps E = exp(logit - target logit) in bf16 (fp16's range would
+            # overflow it): fp16 runs autocast's form, fp16 logits + an fp32 softmax pass
+            ctx.fused = x.dtype == BF16 and _fused_xent_ok(N, C, Vp)
             if ctx.fused:
                 crow = torch.empty(N, device=x.device, dtype=F32)
                 t32 = torch.empty(N, device=x.device, dtype=torch.int32)
@@ -1018,7 +1036,7 @@ class LMHeadLossFn(torch.autograd.Function):
                 ctx.save_for_backward(x2, w, e, t32, inv_s, n_valid)
             else:
                 logits = _gd.fwd(x2, wp)
-                _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(t), _lib.ptr(row_loss), N, V, Vp,
+                _lib.call(_sym("nsa_xent_fwd", x.dtype), _lib.ptr(logits), _lib.ptr(t), _lib.ptr(row_loss), N, V, Vp,
                           1 if need_grad else 0, _lib.stream())
                 n_valid = ((t >= 0) & (t < V)).sum().to(F32)
                 ctx.save_for_backward(x2, w, logits, n_valid)
@@ -1062,16 +1080,17 @@ class LMHeadLossFn(torch.autograd.Function):
             return dx.view(ctx.xshape), _lm_grad_out(w, gw, ret), None, None
         x2, w, dlogits, n_valid = ctx.saved_tensors
         g = (gl.float() / n_valid)
-        if x2.is_cuda and x2.dtype == BF16:
+        if x2.is_cuda and x2.dtype in KDT:
             # the loss scale g = grad / n_valid stays fp32 (a device scalar read by the
-            # kernel): only the scaled products are rounded to bf16, not g itself
-            wp, gwp = _lm_weight(w)
+            # kernel): only the scaled products are rounded to bf16 / fp16, not g itself
+            wp, gwp = _lm_weight(w, x2.dtype)
             Vp = wp.shape[0]
             g = g.reshape(1).contiguous()
             xs = torch.empty_like(x2)
-            _lib.call("nsa_scale_rows_bf16", _lib.ptr(x2), _lib.ptr(xs), _lib.ptr(g), xs.numel(), _lib.stream())
+            scale_rows = _sym("nsa_scale_rows_bf16", x2.dtype)
+            _lib.call(scale_rows, _lib.ptr(x2), _lib.ptr(xs), _lib.ptr(g), xs.numel(), _lib.stream())
             dx = _gd.dgrad(dlogits, wp)
-            _lib.call("nsa_scale_rows_bf16", _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())
+            _lib.call(scale_rows, _lib.ptr(dx), _lib.ptr(dx), _lib.ptr(g), dx.numel(), _lib.stream())
             ret = gwp is None
             gw = torch.zeros(Vp, x2.shape[1], device=x2.device, dtype=F32) if ret else gwp
             _gd.wgrad_acc(dlogits, xs, gw)

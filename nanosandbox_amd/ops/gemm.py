@@ -27,7 +27,18 @@ import torch
 from . import _lib
 
 BF16 = torch.bfloat16
+F16 = torch.float16
 LAYOUT_TN = 2
+
+
+def _sym(name, t):
+    """Entry point for the operand dtype: NAME (bf16) or NAME_h (fp16, nanoGPT dtype='float16';
+    the same kernels with v_mfma_*_f16 and fp16 conversions)."""
+    if t.dtype == F16:
+        return name + "_h"
+    if t.dtype != BF16:
+        raise ValueError(f"GEMM kernels take bf16 or fp16 operands, got {t.dtype}")
+    return name
 EPI_ATOMIC, EPI_STORE_F32 = 1, 4
 BK = 64
 TILE = 256
@@ -72,7 +83,7 @@ def wgrad_supported(n_out, n_in, tokens) -> bool:
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
 
 
-def _out(M, N, device, out, dtype=BF16):
+def _out(M, N, device, out, dtype=BF16):  # noqa: D401
     if out is None:
         return torch.empty(M, N, device=device, dtype=dtype)
     _check(out, "out")
@@ -125,14 +136,17 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, g
     _check(b, "b")
     if bias is not None:
         _check(bias, "bias")
-    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else BF16)
+    if b.dtype != a.dtype:
+        raise ValueError("a and b must have the same dtype")
+    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else a.dtype)
     var = NT_VAR if var is None else var
-    c2 = (_out(M, N, a.device, out2)) if epi == NT_EPI_GELU else None
+    c2 = (_out(M, N, a.device, out2, a.dtype)) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
         _check_gp(u)
     if epi == NT_EPI_GELU:
-        u = gelu_table(a.device)  # rides in the U slot
-    _lib.call("nsa_gemm_nt4", epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
+        # rides in the U slot; the table is indexed by bf16 bits (fp16 computes the GELU)
+        u = gelu_table(a.device) if a.dtype == BF16 else None
+    _lib.call(_sym("nsa_gemm_nt4", a), epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
               b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
               grid or num_cus(a.device), _lib.stream())
     return (c, c2) if epi == NT_EPI_GELU else c
@@ -144,11 +158,13 @@ def small(a, b, epi=NT_EPI_BF16, u=None, bias=None, out=None, out2=None):
     N = b.shape[0]
     _check(a, "a")
     _check(b, "b")
-    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else BF16)
-    c2 = _out(M, N, a.device, out2) if epi == NT_EPI_GELU else None
+    if b.dtype != a.dtype:
+        raise ValueError("a and b must have the same dtype")
+    c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else a.dtype)
+    c2 = _out(M, N, a.device, out2, a.dtype) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
         _check_gp(u)
-    _lib.call("nsa_gemm_small", epi, _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), _lib.ptr(c), c.stride(0),
+    _lib.call(_sym("nsa_gemm_small", a), epi, _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), _lib.ptr(c), c.stride(0),
               _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K, _lib.stream())
     return (c, c2) if epi == NT_EPI_GELU else c
 
@@ -238,7 +254,7 @@ def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False, gb32=None):
         # not in deterministic mode at any split count: the fused kernel spreads each bias
         # column's token sum over the column blocks, each adding its own fp32 atomic
         if four and not deterministic:
-            _lib.call("nsa_gemm_wgrad4b", EPI_ATOMIC, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
+            _lib.call(_sym("nsa_gemm_wgrad4b", dy2), EPI_ATOMIC, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
                       _lib.ptr(g32), K_in, _lib.ptr(gb32), N_out, K_in, T, splits, _lib.stream())
             return g32
         wgrad_acc(dy2, x2, g32, splits, deterministic)
@@ -247,10 +263,10 @@ def wgrad_acc(dy2, x2, g32, splits=None, deterministic=False, gb32=None):
 
     def launch(epi, C):
         if four:
-            _lib.call("nsa_gemm_wgrad4", epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(C),
+            _lib.call(_sym("nsa_gemm_wgrad4", dy2), epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(C),
                       K_in, N_out, K_in, T, splits, _lib.stream())
         else:
-            _lib.call("nsa_gemm", LAYOUT_TN, epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
+            _lib.call(_sym("nsa_gemm", dy2), LAYOUT_TN, epi, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0),
                       _lib.ptr(C), K_in, None, None, N_out, K_in, T, splits, _lib.stream())
 
     if deterministic and splits > 1:
@@ -269,7 +285,7 @@ def bias_grad_acc(dy2, gb32, deterministic=False):
     _check(dy2, "dy")
     nblk = max(1, min(256, T // 64))
     part = torch.empty(nblk, N, device=dy2.device, dtype=torch.float32)
-    _lib.call("nsa_colsum_bf16_partial", _lib.ptr(dy2), dy2.stride(0), T, N, _lib.ptr(part), nblk, _lib.stream())
+    _lib.call(_sym("nsa_colsum_bf16_partial", dy2), _lib.ptr(dy2), dy2.stride(0), T, N, _lib.ptr(part), nblk, _lib.stream())
     _lib.call("nsa_colsum_accum_ordered" if deterministic else "nsa_colsum_accum", _lib.ptr(part), _lib.ptr(gb32),
               nblk, N, _lib.stream())
     return gb32

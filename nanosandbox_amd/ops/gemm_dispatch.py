@@ -42,8 +42,14 @@ BF16 = torch.bfloat16
 DETERMINISTIC = False
 
 
+F16 = torch.float16
+
+
 def _ok(*ts):
-    return all(t.is_cuda and t.dtype == BF16 and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
+    """Operands our kernels take: CUDA, contiguous, 16-byte aligned, all bf16 or all fp16."""
+    return (ts[0].dtype in (BF16, F16)
+            and all(t.is_cuda and t.dtype == ts[0].dtype and t.is_contiguous() and t.data_ptr() % 16 == 0
+                    for t in ts))
 
 
 def kernel_for(op: str, M: int, N: int, K: int) -> str:
@@ -77,7 +83,7 @@ def record(op: str, M: int, N: int, K: int, kernel: str) -> None:
 def _nt(a, b, epi=_gemm.NT_EPI_BF16, u=None, bias=None, op="fwd"):
     M, K = a.shape
     N = b.shape[0]
-    k = kernel_for("fwd", M, N, K) if _ok(a, b) and (bias is None or _ok(bias)) else "torch"
+    k = kernel_for("fwd", M, N, K) if _ok(a, b, *([] if bias is None else [bias])) else "torch"
     _used.setdefault((op, M, N, K), k)
     if k == "nt4":
         return _gemm.nt(a, b, epi=epi, u=u, bias=bias)
@@ -187,7 +193,8 @@ def _transpose(w, out=None):
     """w^T, contiguous: our bf16 transpose kernel (LDS-free 8x8 register blocks) when the
     shape allows, else torch's copy."""
     R, C = w.shape
-    if w.is_cuda and w.dtype == BF16 and R % 64 == 0 and C % 64 == 0 and w.is_contiguous():
+    # a 16-bit transpose: the same bit moves for bf16 and fp16
+    if w.is_cuda and w.dtype in (BF16, F16) and R % 64 == 0 and C % 64 == 0 and w.is_contiguous():
         if out is None or out.shape != (C, R) or out.dtype != w.dtype or out.device != w.device:
             out = torch.empty(C, R, device=w.device, dtype=w.dtype)
         _lib.call("nsa_transpose_bf16", _lib.ptr(w), _lib.ptr(out), R, C, _lib.stream())

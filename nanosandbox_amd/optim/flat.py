@@ -9,7 +9,7 @@ win is in the number and size of passes):
   view.  Linear/LayerNorm/Embedding backward kernels accumulate into it
   directly, and the DDP reducer all-reduces contiguous slices of it (buckets)
   with zero copies.
-* ``compute`` — one contiguous bf16 buffer, the forward/backward weights
+* ``compute`` — one contiguous bf16 (or fp16, dtype='float16') buffer, the forward/backward weights
   (``param.compute``), rewritten by the fused AdamW kernel in the same pass
   that updates ``master`` — so no per-micro-step autocast weight casts.
 * ``wd_mask`` — one byte per 64-element chunk: 1 where weight decay applies
@@ -118,8 +118,8 @@ class FlatParamStore:
             return
         if self.device.type == "cuda":
             from ..ops import _lib
-            _lib.call("nsa_cast_f32_bf16", _lib.ptr(self.master), _lib.ptr(self.compute), self.numel,
-                      _lib.stream())
+            name = "nsa_cast_f32_bf16_h" if self.compute.dtype == torch.float16 else "nsa_cast_f32_bf16"
+            _lib.call(name, _lib.ptr(self.master), _lib.ptr(self.compute), self.numel, _lib.stream())
         else:
             self.compute.copy_(self.master)
 
@@ -135,10 +135,10 @@ class FlatParamStore:
     def buckets(self, cap_bytes: int):
         """Contiguous [start, end) element ranges of ``grad``, cut at parameter boundaries
         so that no bucket exceeds ``cap_bytes`` (fp32) unless it holds a single parameter
-        larger than the cap, or is the late tail below.  A bucket is
-        closed *before* the parameter that would push it past the cap, so with the 64 MiB
-        default the transformer blocks of GPT-2 124M go two per bucket (54 MiB) instead of
-        three (81 MiB, the round-4 rule that closed a bucket only after it passed the cap).
+        larger than the cap, or is the late tail below.  A bucket is closed *before* the
+        parameter that would push it past the cap: with the 64 MiB default GPT-2 124M gets five
+        63 MiB buckets and a 9 MiB one (the round-4 rule closed a bucket only after it passed
+        the cap: about 85 MiB each).
         Parameters tagged ``_nsa_late_grad`` (wte, wpe: complete only after the embedding
         backward, the last kernel of the step) never share a bucket with earlier ones; they
         form one tail bucket (GPT-2 124M: 150 MiB, the one all-reduce that cannot overlap

@@ -138,7 +138,9 @@ class FusedAdamW:
         if self._is_gpu:
             from ..ops import _lib, gemm_dispatch
             gemm_dispatch.weights_changed()  # the kernel rewrites the bf16 compute weights
-            _lib.call("nsa_adamw_step", _lib.ptr(st.master), _lib.ptr(st.grad), _lib.ptr(self.exp_avg),
+            # the fp16 instantiation writes an fp16 compute shadow (dtype float16)
+            name = "nsa_adamw_step_h" if st.compute is not None and st.compute.dtype == torch.float16 else "nsa_adamw_step"
+            _lib.call(name, _lib.ptr(st.master), _lib.ptr(st.grad), _lib.ptr(self.exp_avg),
                       _lib.ptr(self.exp_avg_sq), _lib.ptr(st.compute), _lib.ptr(st.wd_mask), st.numel,
                       float(lr), float(beta1), float(beta2), float(eps), float(wd), float(bc1), float(bc2_sqrt),
                       _lib.ptr(self._coef), _lib.ptr(ls.state) if ls is not None else None, _lib.stream())

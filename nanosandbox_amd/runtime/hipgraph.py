@@ -54,7 +54,10 @@ class MicroStepGraph:
     """Captured ``loss = model(X, Y)[1] / gas; loss.backward()``, replayed per micro-step."""
 
     def __init__(self, model, X: torch.Tensor, Y: torch.Tensor, gas: int, warmup: int = 2, zero_grad=None,
-                 dropout: bool = False):
+                 dropout: bool = False, loss_scale: torch.Tensor | None = None):
+        """``loss_scale``: the fp16 dynamic loss scale as a 1-element device tensor; the
+        backward is taken of loss * scale, with the scale read at replay time (it changes
+        between steps on the device)."""
         from ..ops import rng_advance
 
         self.model = model
@@ -68,7 +71,7 @@ class MicroStepGraph:
                 if dropout:
                     rng_advance(self.X.device)
                 _, loss = model(self.X, self.Y)
-                (loss / gas).backward()
+                ((loss / gas) * loss_scale if loss_scale is not None else loss / gas).backward()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if zero_grad is not None:
@@ -79,7 +82,7 @@ class MicroStepGraph:
                 rng_advance(self.X.device)  # replayed: fresh dropout masks per micro-step
             _, loss = model(self.X, self.Y)
             self.loss = loss / gas
-            self.loss.backward()
+            (self.loss * loss_scale if loss_scale is not None else self.loss).backward()
         self.replays = 0
 
     def run(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:

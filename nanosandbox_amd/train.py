@@ -42,10 +42,11 @@ _DTYPES = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torc
 
 def _compute_dtype(device_type: str, dtype: str) -> torch.dtype:
     """nanoGPT's ``dtype`` key: 'bfloat16' (default on MI355X), 'float16' (with a dynamic loss
-    scale) or 'float32'.  On the GPU bf16 runs our HIP kernels; fp16 and fp32
-    run every op's torch reference implementation (the numerics contract, at library speed:
-    gfx950's fp16 MFMA rate equals bf16's, so fp16 buys nothing but the scaler here).  The
-    CPU always computes in fp32 (nanoGPT: nullcontext on CPU)."""
+    scale) or 'float32'.  On the GPU bf16 and fp16 run our HIP kernels (the
+    fp16 ones are the same sources with v_mfma_*_f16 and fp16 conversions; gfx950's fp16 MFMA
+    rate equals bf16's); fp32 runs every op's torch reference implementation (the numerics
+    contract, at library speed).  The CPU always computes in fp32 (nanoGPT: nullcontext on
+    CPU)."""
     if dtype not in _DTYPES:
         raise ValueError(f"dtype must be one of {sorted(_DTYPES)}, got {dtype!r}")
     if device_type != "cuda":
@@ -79,8 +80,8 @@ class Trainer:
             from .optim.loss_scale import DynamicLossScale
             self.scaler = DynamicLossScale(device=self.device)
         if self.device_type == "cuda" and self.compute_dtype != torch.bfloat16 and self.master:
-            print(f"dtype={c['dtype']}: torch reference ops (HIP kernels run bf16 only)"
-                  + (", dynamic loss scale" if self.scaler else ""))
+            print(f"dtype={c['dtype']}: " + ("fp16 HIP kernels, dynamic loss scale on the device" if self.scaler
+                                            else "torch reference ops (the HIP kernels run bf16 / fp16)"))
 
         # ---------------------------------------------------------------- data
         self.data_dir = resolve_data_dir(c["dataset"], c["data_dir"])
@@ -141,8 +142,9 @@ class Trainer:
         # ------------------------------------------- flat store + fused AdamW
         self.ddp_impl = c["ddp_impl"] if info.ddp else "none"
         fused_grad = self.ddp_impl != "torch"
-        self.store = FlatParamStore(model, self.device,
-                                    compute_dtype=torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None,
+        # the 16-bit compute shadow the fused AdamW kernel rewrites each step (bf16 or fp16)
+        shadow = self.compute_dtype if self.compute_dtype in (torch.bfloat16, torch.float16) else None
+        self.store = FlatParamStore(model, self.device, compute_dtype=shadow if self.device_type == "cuda" else None,
                                     fused_grad=fused_grad)
         self.optimizer = model.configure_optimizers(c["weight_decay"], c["learning_rate"], (c["beta1"], c["beta2"]),
                                                     self.device_type, store=self.store)
@@ -169,7 +171,7 @@ class Trainer:
         self.use_graph = False
         if c["compile"]:
             ok, why = graph_capture_supported(self.device, c["dropout"], info.world_size, self.ddp_impl, self.gas)
-            if ok and self.compute_dtype != torch.bfloat16:
+            if ok and self.compute_dtype not in (torch.bfloat16, torch.float16):
                 ok, why = False, f"dtype={c['dtype']} runs the torch reference ops"
             self.use_graph = ok
             if self.master:
@@ -249,7 +251,8 @@ class Trainer:
                     self.reducer.prepare(False)  # capture with the bucket hooks disarmed
                 self.graph = MicroStepGraph(self.model, X, Y, self.gas,
                                             zero_grad=lambda: self.optimizer.zero_grad(set_to_none=True),
-                                            dropout=c["dropout"] > 0.0)
+                                            dropout=c["dropout"] > 0.0,
+                                            loss_scale=self.scaler.scale_t if self.scaler is not None else None)
             for _ in range(n_graph):
                 loss = self.graph.run(X, Y)
                 X, Y = self.batches.get_batch("train")
