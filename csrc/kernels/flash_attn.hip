@@ -140,7 +140,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
 //         kernel taking two query slices per barrier; v1 = the generic kernels
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6 };
 enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -156,7 +156,7 @@ FlashConfig& flash_config() {
   static FlashConfig c = [] {
     FlashConfig d{FWD_AUTO, BWD_V3, ATTN_ORDER_DEFAULT};
     if (const char* e = getenv("NSA_FLASH_FWD"))
-      d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '3' || e[1] == '4' || e[1] == '5')) ? e[1] - '0' : FWD_AUTO;
+      d.fwd = (e[0] == 'v' && (e[1] == '1' || (e[1] >= '3' && e[1] <= '6'))) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
       d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
@@ -330,6 +330,60 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
   }
 }
 
+// The v5 fast tile (scores without the row max while they stay in range, see
+// fwd_tile5 below) for ONE 32-query block per wave: the v1 kernel's geometry (4 waves per
+// SIMD), "v6".  Returns false (nothing accumulated) when the tile leaves range.
+template <bool MASK>
+__device__ __forceinline__ bool fwd_tile_fast(const char* kt, const char* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2],
+                                              float& l_i, int kv0, int qpos, int h, int r, int lane,
+                                              float scale_log2) {
+  constexpr int D = 64;
+  f32x16 st[2];
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    st[sb] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
+  }
+  bf16x8 pf[2][2];
+  float acc[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {  // one v_pk_mul_f32 per score pair
+      nsa_f32x2 v2 = nsa_f32x2{st[sb][i], st[sb][i + 1]} * scale_log2;
+      st[sb][i] = v2.x;
+      st[sb][i + 1] = v2.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float sv = st[sb][i];
+      if constexpr (MASK) {
+        if (kv0 + 32 * sb + acc_row(i, h) > qpos) sv = -INFINITY;
+      }
+      const float p = fast_exp2(sv);
+      acc[sb] += p;
+      pf[sb][i >> 3][i & 7] = fa_elt(p);
+    }
+  }
+  const float rs = half_swap_sum(acc[0] + acc[1]);
+  const float ln = l_i + rs;
+  // bf16 P holds any fp32 value; fp16 P only up to 65504 (the fp16 build's bound)
+  const float hi = kFaH ? 0x1p15f : 0x1p64f, lo = kFaH ? 0x1p-8f : 0x1p-60f;
+  if (__builtin_amdgcn_ballot_w64(!(rs <= hi && ln >= lo))) return false;
+  l_i = ln;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r0 = 32 * sb + 16 * s + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
+    }
+  }
+  return true;
+}
+
 // K/V tile staging through registers (T14 split: issue before compute, write after)
 #define NSA_FWD_STAGE_LOAD(J)                                                                   \
   _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
@@ -355,8 +409,10 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
 // T14 split intends, but hipcc sinks the staging loads out of the loop head into the
 // latch, right before their LDS writes (the tile compute sits in branches), so every
 // tile waited out a full global-memory round trip.
-template <int D, bool DROP, bool DMA = false>
-__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void flash_fwd_kernel(
+// FAST (D = 64 with DMA, no dropout): fast tiles (fwd_tile_fast) until a tile leaves range,
+// exact tiles from then on ("v6")
+template <int D, bool DROP, bool DMA = false, bool FAST = false>
+__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA && !FAST ? 4 : 3) : 2) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, float* __restrict__ lse_out, int B, int T, int H,
     float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
   constexpr int BN = 64;
@@ -398,7 +454,8 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
   f32x16 o[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
-  float m_i = -1e30f, l_i = 0.0f;
+  float m_i = FAST ? 0.0f : -1e30f, l_i = 0.0f;
+  bool fast = FAST;  // wave-uniform
 
   const int kv_end = min(T, q0 + 128);
   const int n_tiles = (kv_end + BN - 1) / BN;
@@ -444,10 +501,34 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void f
       issue(min(j + 1, n_tiles - 1), cur ^ 1);
       const char* kt = smem + cur * TILE_BYTES;
       const char* vt = smem + (2 + cur) * TILE_BYTES;
-      if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
-        fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-      else if (kv0 <= q0w + 31)  // the wave's diagonal tile
-        fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      if constexpr (FAST && D == 64 && !DROP) {
+        const bool full = kv0 + BN - 1 <= q0w, diag = !full && kv0 <= q0w + 31;
+        if (full || diag) {
+          const bool ok = fast && (full ? fwd_tile_fast<false>(kt, vt, qf, o, l_i, kv0, qpos, h, r, lane, scale_log2)
+                                        : fwd_tile_fast<true>(kt, vt, qf, o, l_i, kv0, qpos, h, r, lane, scale_log2));
+          if (!ok) {
+            if (fast) {  // hand-over to exact tiles: m' = log2(l) (see fwd5_to_exact)
+              if (l_i > 0.0f) {
+                const float mp = __log2f(l_i), f = fast_exp2(-mp);
+                l_i *= f;
+                o[0] *= f;
+                o[1] *= f;
+                m_i = mp / scale_log2;
+              } else {
+                m_i = -1e30f;
+              }
+              fast = false;
+            }
+            if (full) fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+            else fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+          }
+        }
+      } else {
+        if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+          fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+        else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+          fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -886,6 +967,11 @@ __device__ unsigned long long g_fwd3_stamps[16384 * 4 * 6];
 // NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
 // end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
 // not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
+// Probe build only (-DNSA_PROBE_SKIP_TILE=1, build_variant): the v4 forward skips key tile
+// 1 of every workgroup -- wrong output, used to show the test suite catches a dropped tile.
+#ifndef NSA_PROBE_SKIP_TILE
+#define NSA_PROBE_SKIP_TILE 0
+#endif
 template <bool DROP, int NS, bool PAIR = false>
 __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse_out, int B, int T, int H,
@@ -981,6 +1067,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __rest
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int jj = j + u;
+        if (NSA_PROBE_SKIP_TILE && jj == 1) continue;  // test-suite probe: one causal tile dropped
         if (jj < n_tiles) {
           const int kv0 = jj * BN;
           const char* kt = smem + (jj % 4) * TILE_BYTES;
@@ -2075,6 +2162,11 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
                                                                   T, H, scale * kLog2e, th, dscale, seed);
       return hipGetLastError();
     }
+    if (sel == FWD_V6 && !th) {  // v1 geometry with the fast tiles
+      flash_fwd_kernel<D, false, true, true><<<n_qt * B * H, 256, 0, s>>>(
+          (const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H, scale * kLog2e, th, dscale, seed, order);
+      return hipGetLastError();
+    }
     // v1 with LDS-DMA K/V staging
     if (th)
       flash_fwd_kernel<D, true, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B,
@@ -2217,7 +2309,7 @@ NSA_API void* nsa_flash_config_ptr() { return &flash_config(); }
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V3 || fwd == FWD_V4 || fwd == FWD_V5) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || (fwd >= FWD_V3 && fwd <= FWD_V6)) c.fwd = fwd;
   if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order >= 0 && order <= 2) c.order = order;
   return prev;

@@ -270,6 +270,125 @@ def test_lm_head_loss_fixup_rows(kernels):
     assert rel_err(w.main_grad, wr.grad) < 2e-2
 
 
+def _lm_loss_and_grads(x0, w0, t):
+    from nanosandbox_amd import ops
+    x = x0.clone().requires_grad_(True)
+    w = param(w0, fused=True)
+    loss = ops.lm_head_loss(x, w, t)
+    loss.backward()
+    return loss.detach(), x.grad, w.main_grad
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_lm_head_loss_fixup_many_rows(kernels, graph):
+    """more flagged rows (100) than the fix-up grid (64 workgroups, so
+    workgroups take several rows), some with the last real vocabulary id as target (the
+    tile beside the 50257 -> 50304 padding), under HIP-graph capture and replay too.  Loss
+    and every gradient element against fp32, bounds scaled by the terms that form them."""
+    torch.manual_seed(5)
+    N, V, C = 1024, 50257, 256
+    x0 = torch.randn(N, C, device=DEV)
+    flagged = torch.arange(0, 1000, 10, device=DEV)  # 100 rows
+    x0[flagged] *= 400.0  # logits ~ +-1300: S = sum exp(l - l_t) overflows fp32
+    x0 = x0.to(BF)
+    w0 = torch.randn(V, C, device=DEV) * 0.05
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[flagged[::20]] = V - 1
+    t[3::97] = -1
+    if graph:
+        from nanosandbox_amd import ops
+        xs = x0.clone().requires_grad_(True)
+        w = param(w0, fused=True)
+        ops.lm_head_loss(xs, w, t).backward()  # warm-up (allocator, caches) outside the graph
+        torch.cuda.synchronize()
+        xs.grad = None
+        w.main_grad.zero_()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            loss_s = ops.lm_head_loss(xs, w, t)
+            loss_s.backward()
+        w.main_grad.zero_()
+        gr.replay()
+        torch.cuda.synchronize()
+        loss, gx, gw = loss_s.detach().clone(), xs.grad.clone(), w.main_grad.clone()
+    else:
+        loss, gx, gw = _lm_loss_and_grads(x0, w0, t)
+    xr = x0.float().requires_grad_(True)
+    wr = w0.to(BF).float().requires_grad_(True)
+    lr = F.cross_entropy(xr @ wr.t(), t, ignore_index=-1)
+    lr.backward()
+    assert math.isfinite(loss.item()) and abs(loss.item() - lr.item()) < 2e-3 * abs(lr.item())
+    n_valid = (t >= 0).sum().float()
+    p = torch.softmax(xr.detach() @ wr.detach().t(), -1)
+    valid = (t >= 0).float()[:, None]
+    magx = (p @ wr.detach().abs() + wr.detach().abs()[t.clamp(min=0)]) * valid / n_valid
+    assert torch.isfinite(gx.float()).all()
+    assert ((gx.float() - xr.grad).abs() <= 2 ** -7 * magx + 1e-7).all()
+    magw = ((p * valid).t() @ xr.detach().abs()) / n_valid
+    magw.index_add_(0, t.clamp(min=0), xr.detach().abs() * valid / n_valid)
+    assert ((gw - wr.grad).abs() <= 2 ** -7 * magw + 1e-7).all()
+
+
+def test_layernorm_raw_nan_prefilled(kernels):
+    """nsa_layernorm_fwd_x32 / bwd_x32 into NaN-prefilled outputs, every element checked:
+    s = x + y exactly, h within one bf16 rounding of fp32 LN, mean / rstd per row, dx and
+    its bf16 branch copy against fp32 autograd, the dw partial rows summed."""
+    from nanosandbox_amd.ops import _lib
+    torch.manual_seed(4)
+    N, C = 300, 768
+    x = torch.randn(N, C, device=DEV) * 2 + 0.5
+    y = torch.randn(N, C, device=DEV).to(BF)
+    w = (torch.randn(C, device=DEV) * 0.5 + 1).to(BF)
+    b = (torch.randn(C, device=DEV) * 0.1).to(BF)
+    nan = lambda *sh, dt=torch.float32: torch.full(sh, float("nan"), device=DEV, dtype=dt)  # noqa: E731
+    s_out, h, mean, rstd = nan(N, C), nan(N, C, dt=BF), nan(N), nan(N)
+    _lib.call("nsa_layernorm_fwd_x32", _lib.ptr(x), _lib.ptr(y), _lib.ptr(s_out), _lib.ptr(w), _lib.ptr(b),
+              _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C, 1e-5, _lib.stream())
+    torch.cuda.synchronize()
+    sr = x + y.float()
+    assert torch.equal(s_out, sr)
+    hr = F.layer_norm(sr, (C,), w.float(), b.float(), 1e-5)
+    assert ((h.float() - hr).abs() <= 2 ** -8 * hr.abs() + 2 ** -12).all()
+    assert torch.allclose(mean, sr.mean(-1), atol=1e-5)
+    assert torch.allclose(rstd, torch.rsqrt(sr.var(-1, unbiased=False) + 1e-5), rtol=1e-5)
+    dh = torch.randn(N, C, device=DEV).to(BF)
+    dres = torch.randn(N, C, device=DEV) * 0.1
+    nblk = 16
+    dx, dxb, dwp, dbp = nan(N, C), nan(N, C, dt=BF), nan(nblk, C), nan(nblk, C)
+    _lib.call("nsa_layernorm_bwd_x32", _lib.ptr(dh), _lib.ptr(s_out), _lib.ptr(w), _lib.ptr(mean), _lib.ptr(rstd),
+              _lib.ptr(dres), _lib.ptr(dx), _lib.ptr(dxb), _lib.ptr(dwp), _lib.ptr(dbp), N, C, nblk, _lib.stream())
+    torch.cuda.synchronize()
+    srq = sr.clone().requires_grad_(True)
+    wq = w.float().requires_grad_(True)
+    bq = b.float().requires_grad_(True)
+    F.layer_norm(srq, (C,), wq, bq, 1e-5).backward(dh.float())
+    ref = srq.grad + dres
+    xhat_mag = (rstd[:, None] * (dh.float() * w.float()).abs()).sum(-1, keepdim=True) / C * 4 + dres.abs()
+    assert ((dx - ref).abs() <= 1e-5 * xhat_mag + 1e-5 * ref.abs() + 1e-6).all()
+    assert torch.equal(dxb, dx.to(BF))
+    assert torch.allclose(dwp.sum(0), wq.grad, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(dbp.sum(0), bq.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_embedding_raw_nan_prefilled(kernels):
+    """nsa_embedding_fwd_x32 into a NaN-prefilled fp32 stream: wte[idx] + wpe[t], bit-exact
+    (a sum of two bf16 values is exact in fp32) for every element, repeated and last-id
+    tokens included."""
+    from nanosandbox_amd.ops import _lib
+    torch.manual_seed(6)
+    B, T, V, C = 3, 200, 50304, 768
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    idx[0, :7] = V - 1
+    idx[1, 10:20] = 5
+    wte = (torch.randn(V, C, device=DEV) * 0.02).to(BF)
+    wpe = (torch.randn(T, C, device=DEV) * 0.02).to(BF)
+    out = torch.full((B, T, C), float("nan"), device=DEV)
+    _lib.call("nsa_embedding_fwd_x32", _lib.ptr(idx), _lib.ptr(wte), _lib.ptr(wpe), _lib.ptr(out), B * T, T, C, 0.0,
+              0, _lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, wte.float()[idx] + wpe.float()[None])
+
+
 # ----------------------------------------------------------------- dropout
 def test_dropout_mask_consistency(kernels):
     from nanosandbox_amd import ops
@@ -338,7 +457,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
@@ -386,7 +505,7 @@ def _flash_fwd_raw(qkv, H, out_nan=True):
     return y, lse
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6"])
 @pytest.mark.parametrize("T,D", [(1024, 64), (320, 64), (200, 64), (64, 64), (77, 32), (192, 128), (1024, 32)])
 @pytest.mark.parametrize("layout", ["tile", "row"])
 def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
@@ -462,7 +581,7 @@ def test_flash_bwd_exact_structure(kernels, flash_variant, T):
         assert (err <= 2 ** -6 * m + 1e-5).all(), (name, err.max().item())
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative", "overflow", "underflow"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -568,12 +687,13 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
 
 
-def test_flash_fwd_v5_fallback_mid_sequence(kernels, flash_variant):
-    """v5 switches a wave from fast (m = 0) to exact tiles when a later tile overflows: the
-    first tiles ran with m = 0 and are then rescaled by the exact path's max."""
+@pytest.mark.parametrize("fwd", ["v5", "v6"])
+def test_flash_fwd_v5_fallback_mid_sequence(kernels, flash_variant, fwd):
+    """v5 / v6 switch a wave from fast (m = 0) to exact tiles when a later tile overflows:
+    the first tiles ran with m = 0 and are then rescaled by the exact path's max."""
     from nanosandbox_amd.ops import functional as fn
 
-    flash_variant(fwd="v5")
+    flash_variant(fwd=fwd)
     torch.manual_seed(3)
     B, T, H, D = 1, 1024, 2, 64
     C = H * D
