@@ -21,6 +21,8 @@
 // reduces the partial rows (split over row ranges, fp32 atomics) into the flat
 // gradient buffer.  Backward rows are software-pipelined (next row's loads in
 // flight while the current row is reduced).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -109,6 +111,35 @@ __device__ __forceinline__ void store8xn(float* p, const float (&f)[8]) {
             make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7])));
 }
 
+// Split-plane fp32 residual gradient (bf16 compute, fp32 stream).  An [N, C] fp32 gradient
+// is stored as two 16-bit planes in the same 4·N·C bytes: hi = bf16(g) (the branch GEMMs'
+// operand, read in place), then lo = bits(g) − (hi << 16) as int16, so hi, lo give g back bit
+// for bit.  hi rounds to nearest with ties away from zero ((bits + 0x8000) >> 16): then lo
+// spans exactly [−0x8000, 0x7fff] — round-to-nearest-even would need the 65537th value
+// +0x8000 at a tie rounded down.  It differs from torch's bf16 cast only at exact ties (low 16
+// bits 0x8000); infinities round-trip, a NaN keeps a quiet-NaN hi and decodes to a NaN.  The
+// backward thereby writes 4 bytes per element where fp32 + a bf16 copy wrote 6.
+__device__ __forceinline__ void split8(const float (&f)[8], uint4& hi, uint4& lo) {
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t u = __float_as_uint(f[j]);
+    h[j] = (u & 0x7fffffffu) > 0x7f800000u ? ((u >> 16) | 0x40u) : ((u + 0x8000u) >> 16);
+    l[j] = (u - (h[j] << 16)) & 0xffffu;
+  }
+  hi = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+  lo = make_uint4(l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16));
+}
+__device__ __forceinline__ void unsplit8(uint4 hi, uint4 lo, float (&f)[8]) {
+  const uint32_t hw[4] = {hi.x, hi.y, hi.z, hi.w}, lw[4] = {lo.x, lo.y, lo.z, lo.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int32_t l0 = (int32_t)(int16_t)(lw[i] & 0xffffu), l1 = (int32_t)(int16_t)(lw[i] >> 16);
+    f[2 * i] = __uint_as_float((hw[i] << 16) + (uint32_t)l0);
+    f[2 * i + 1] = __uint_as_float((hw[i] & 0xffff0000u) + (uint32_t)l1);
+  }
+}
+
 // value as stored in the residual stream (bf16 rounding for a bf16 stream)
 __device__ __forceinline__ float as_stream(float v, bf16_t*) { return bf2f(f2bf(v)); }
 __device__ __forceinline__ float as_stream(float v, float*) { return v; }
@@ -190,7 +221,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
 // per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
 // xhat and dy*w are recomputed from the raw words in the second pass rather than
 // kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
-template <int NK, bool PIPE, typename XT, bool NT = false, bool H = false>
+// SPLIT (fp32 stream, bf16 compute): bit 0 — dres is a split-plane gradient (split8);
+// bit 1 — dx is written split (its hi plane is the branch copy, dx_branch unused)
+template <int NK, bool PIPE, typename XT, bool NT = false, bool H = false, int SPLIT = 0>
 __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const XT* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
                                                     const float* __restrict__ rstd_in, const XT* __restrict__ dres,
@@ -226,7 +259,13 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
     const int64_t off = (int64_t)min((R), N - 1) * C + c;                                \
     nx[k] = ld_raw_n<NT>(x + off);                                                       \
     nd[k] = ld16n<NT>(dy + off);                                                         \
-    if (dres) nr[k] = ld_raw_n<NT>(dres + off);                                          \
+    if constexpr (SPLIT & 1) {                                                           \
+      const uint16_t* hp = reinterpret_cast<const uint16_t*>(dres);                      \
+      nr[k].u[0] = ld16n<NT>(hp + off);                                                  \
+      nr[k].u[Raw8<XT>::W - 1] = ld16n<NT>(hp + (int64_t)N * C + off);                    \
+    } else if (dres) {                                                                   \
+      nr[k] = ld_raw_n<NT>(dres + off);                                                  \
+    }                                                                                    \
   }
   if (PIPE) NSA_LNB_LOAD(row)
   for (; row < N; row += row_step) {
@@ -286,12 +325,21 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
         for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[j] * wf[j] - m1 - (xv[j] - mean) * rstd * m2);
         if (dres) {  // gradient arriving through the residual path of the fused add
           float rv[8];
-          unpack_raw(cr[k], rv);
+          if constexpr (SPLIT & 1) unsplit8(cr[k].u[0], cr[k].u[Raw8<XT>::W - 1], rv);
+          else unpack_raw(cr[k], rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
-        store8xn<NT>(dx + (int64_t)row * C + c, o);
-        if (dx_branch) store8e<H>(dx_branch + (int64_t)row * C + c, o);  // 16-bit copy for the branch GEMMs
+        if constexpr (SPLIT & 2) {  // hi plane: plain store (the branch GEMMs read it next)
+          uint4 hi, lo;
+          split8(o, hi, lo);
+          uint16_t* hp = reinterpret_cast<uint16_t*>(dx);
+          *reinterpret_cast<uint4*>(hp + (int64_t)row * C + c) = hi;
+          st16n<NT>(hp + (int64_t)N * C + (int64_t)row * C + c, lo);
+        } else {
+          store8xn<NT>(dx + (int64_t)row * C + c, o);
+          if (dx_branch) store8e<H>(dx_branch + (int64_t)row * C + c, o);  // 16-bit copy for the branch GEMMs
+        }
       }
     }
   }
@@ -332,26 +380,45 @@ hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void*
   return hipGetLastError();
 }
 
+template <int NK, bool PIPE, typename XT, bool NT, bool H>
+hipError_t launch_bwd_split(int split, const void* dy, const void* x, const void* w, const void* mean,
+                            const void* rstd, const void* dres, void* dx, void* dx_branch, void* dw_part,
+                            void* db_part, int N, int C, int nblk, hipStream_t s) {
+#define NSA_LNB_GO(SP)                                                                                  \
+  ln_bwd_kernel<NK, PIPE, XT, NT, H, SP><<<nblk, 256, 8 * C * sizeof(float), s>>>(                      \
+      (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,         \
+      (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C)
+  if constexpr (std::is_same<XT, float>::value && !H) {
+    switch (split) {
+      case 1: NSA_LNB_GO(1); return hipGetLastError();
+      case 2: NSA_LNB_GO(2); return hipGetLastError();
+      case 3: NSA_LNB_GO(3); return hipGetLastError();
+      default: break;
+    }
+  }
+  NSA_LNB_GO(0);
+#undef NSA_LNB_GO
+  return hipGetLastError();
+}
+
 template <int NK, typename XT, bool H = false>
 hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* mean, const void* rstd,
                       const void* dres, void* dx, void* dx_branch, void* dw_part, void* db_part, int N, int C,
                       int nblk, hipStream_t s) {
-  // bit 30 of nblk selects the non-pipelined body (A/B timing)
+  // bit 30 of nblk selects the non-pipelined body (A/B timing); bits 28-29 the split planes
   const bool pipe = !(nblk & (1 << 30));
-  nblk &= ~(1 << 30);
+  const int split = (nblk >> 28) & 3;
+  nblk &= (1 << 28) - 1;
+  if (split && (!std::is_same<XT, float>::value || H)) return hipErrorInvalidValue;
+  if ((split & 1) && dres == nullptr) return hipErrorInvalidValue;
   if (pipe && ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
-    ln_bwd_kernel<NK, true, XT, true, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
-        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
-  else if (pipe)
-    ln_bwd_kernel<NK, true, XT, false, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
-        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
-  else
-    ln_bwd_kernel<NK, false, XT, false, H><<<nblk, 256, 8 * C * sizeof(float), s>>>(
-        (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,
-        (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C);
-  return hipGetLastError();
+    return launch_bwd_split<NK, true, XT, true, H>(split, dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
+                                                   db_part, N, C, nblk, s);
+  if (pipe)
+    return launch_bwd_split<NK, true, XT, false, H>(split, dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
+                                                    db_part, N, C, nblk, s);
+  return launch_bwd_split<NK, false, XT, false, H>(split, dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
+                                                   db_part, N, C, nblk, s);
 }
 
 }  // namespace
@@ -399,6 +466,20 @@ NSA_API hipError_t nsa_layernorm_bwd_x32(const void* dy, const void* x, const vo
                                          const void* rstd, const void* dres, void* dx, void* dx_branch,
                                          void* dw_part, void* db_part, int N, int C, int nblk, hipStream_t s) {
   if (C % 8 != 0 || C > 8192) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
+                                                        N, C, nblk, s)));
+}
+
+// nsa_layernorm_bwd_x32 with split-plane residual gradients (bf16 compute): split bit 0 —
+// dres is split (split8: hi plane then lo plane in its 4·N·C bytes), bit 1 — dx is written
+// split, its hi plane being the bf16 branch gradient (dx_branch unused)
+NSA_API hipError_t nsa_layernorm_bwd_x32s(const void* dy, const void* x, const void* w, const void* mean,
+                                          const void* rstd, const void* dres, void* dx, void* dx_branch,
+                                          void* dw_part, void* db_part, int N, int C, int nblk, int split,
+                                          hipStream_t s) {
+  if (C % 8 != 0 || C > 8192 || split < 0 || split > 3 || (nblk & ~(1 << 30)) >= (1 << 28))
+    return hipErrorInvalidValue;
+  nblk |= split << 28;
   NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
                                                         N, C, nblk, s)));
 }

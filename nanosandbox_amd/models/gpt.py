@@ -103,8 +103,8 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(config.n_embd, bias=config.bias)
         self.mlp = MLP(config)
 
-    def fused_forward(self, x, h):
-        x, h2 = ops.add_layer_norm(x, self.attn(h), self.ln_2.weight, self.ln_2.bias)
+    def fused_forward(self, x, h, split_grad=False):
+        x, h2 = ops.add_layer_norm(x, self.attn(h), self.ln_2.weight, self.ln_2.bias, split_grad=split_grad)
         return x, self.mlp(h2)
 
     def forward(self, x):
@@ -113,8 +113,10 @@ class Block(nn.Module):
 
 
 def _block_step(block, next_ln, x, h):
-    x, y = block.fused_forward(x, h)
-    return ops.add_layer_norm(x, y, next_ln.weight, next_ln.bias)
+    # the trunk's residual stream runs from one fused LayerNorm to the next with no other
+    # reader, so its gradient may travel split (ops.add_layer_norm split_grad)
+    x, y = block.fused_forward(x, h, split_grad=True)
+    return ops.add_layer_norm(x, y, next_ln.weight, next_ln.bias, split_grad=True)
 
 
 class GPT(nn.Module):

@@ -175,6 +175,15 @@ def rng_advance(device) -> None:
 # ----------------------------------------------------------------------------
 
 def _cpu_keep_mask(shape, p, seed, device=None):
+    """Keep-mask of the torch reference path, a pure function of ``seed``: the forward
+    and the backward redraw it rather than store it.  A GPU tensor (fp32 compute on the
+    GPU) draws it with a device generator seeded the same way, so the mask never crosses
+    the host link (a full [B, H, T, T] attention mask per layer would otherwise be drawn
+    on the CPU and copied, twice per step)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        g = torch.Generator(device=dev).manual_seed(seed)
+        return torch.rand(shape, generator=g, device=dev) >= p
     g = torch.Generator().manual_seed(seed)
     m = torch.rand(shape, generator=g) >= p
     return m if device is None else m.to(device)
@@ -329,6 +338,39 @@ LN_EPS = 1e-5
 _LN_BWD_BLOCKS = 768
 # fp32 residual stream: ~174 VGPRs -> 2 resident 256-thread blocks per CU
 _LN_BWD_BLOCKS_X32 = int(os.environ.get("NSA_LN_BWD_BLOCKS", "512"))
+# split-plane residual gradients between our LayerNorm backward passes (NSA_LN_SPLIT=0: plain
+# fp32 + a bf16 copy, for A/B); see LayerNormFn and csrc/kernels/layernorm.hip split8
+LN_SPLIT = os.environ.get("NSA_LN_SPLIT", "1") != "0"
+
+
+def split_planes(g: torch.Tensor) -> torch.Tensor:
+    """fp32 [.., C] -> the split-plane encoding of csrc/kernels/layernorm.hip (split8), as an
+    fp32 tensor of the same shape: hi = bf16(g) rounded to nearest, ties away from zero, in the
+    first half of its bytes, the int16 correction bits(g) - (hi << 16) in the second."""
+    n = g.numel()
+    bits = g.detach().contiguous().view(torch.int32).reshape(-1).to(torch.int64) & 0xFFFFFFFF
+    hi = ((bits + 0x8000) >> 16) & 0xFFFF
+    hi = torch.where(torch.isnan(g.detach().reshape(-1)), ((bits >> 16) | 0x40) & 0xFFFF, hi)
+    lo = (bits - (hi << 16)) & 0xFFFF
+    out = torch.empty(2 * n, dtype=torch.int16, device=g.device)
+    out[:n] = torch.where(hi >= 0x8000, hi - 0x10000, hi).to(torch.int16)
+    out[n:] = torch.where(lo >= 0x8000, lo - 0x10000, lo).to(torch.int16)
+    return out.view(torch.float32).view(g.shape)
+
+
+def unsplit_planes(t: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``split_planes``: the fp32 values, bit for bit."""
+    n = t.numel()
+    raw = t.detach().contiguous().reshape(-1).view(torch.int16)
+    hi = raw[:n].to(torch.int64) & 0xFFFF
+    lo = raw[n:].to(torch.int64)  # sign-extended correction
+    bits = ((hi << 16) + lo) & 0xFFFFFFFF
+    bits = torch.where(bits >= 0x80000000, bits - 0x100000000, bits).to(torch.int32)
+    return bits.view(torch.float32).view(t.shape)
+
+
+def _is_split(g) -> bool:
+    return g is not None and getattr(g, "_nsa_split", False)
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -342,10 +384,18 @@ class LayerNormFn(torch.autograd.Function):
 
     Backward of the fused form: ds_total = LN'(dh) + ds (gradient that reached s
     through the residual stream), computed in one kernel pass, and returned as
-    the gradient of both x and y — no separate autograd add kernel."""
+    the gradient of both x and y — no separate autograd add kernel.
+
+    ``split_grad`` (the GPT trunk, where x comes from another of these nodes and has no other
+    consumer): with the fp32 stream and bf16 compute the backward returns x's gradient in the
+    split-plane encoding (``split_planes``; the tensor carries ``_nsa_split``), whose first
+    half IS the bf16 gradient handed to y — 4 bytes written per element instead of fp32 + a
+    bf16 copy (6).  The producing LayerNorm's kernel reads it back exactly; any other
+    receiver decodes it with ``unsplit_planes``.  The bf16 half rounds ties away from zero
+    (torch's cast: to even), the one difference, at elements whose low 16 bits are 0x8000."""
 
     @staticmethod
-    def forward(ctx, x, y, w, b, out_dtype, passthrough=False):
+    def forward(ctx, x, y, w, b, out_dtype, passthrough=False, split_grad=False):
         ctx.set_materialize_grads(False)
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
@@ -356,6 +406,8 @@ class LayerNormFn(torch.autograd.Function):
         out_dtype = out_dtype or (y.dtype if y is not None else x.dtype)
         ctx.y_dtype = y.dtype if y is not None else None
         ctx.kern = x.is_cuda and out_dtype in KDT
+        ctx.split_out = bool(split_grad and LN_SPLIT and ctx.kern and y is not None and x.dtype == F32
+                             and out_dtype == BF16)
         if ctx.kern:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
             x32 = x.dtype == F32
@@ -403,15 +455,18 @@ class LayerNormFn(torch.autograd.Function):
         else:
             ds, dh = None, grads[0]
         if dh is None and ds is None:  # no output reached the loss (grads are not materialised)
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
+        ds_split = _is_split(ds)
+        if ds_split and (dh is None or not ctx.kern or x2.dtype != F32 or dh.dtype != BF16):
+            ds, ds_split = unsplit_planes(ds), False  # a receiver the split kernel does not cover
         b = b_or_mean if ctx.has_bias else None
         C = x2.shape[-1]
         N = x2.shape[0]
         shape = (*(dh if dh is not None else ds).shape[:-1], C)
         if dh is None:  # only the residual output was used
             dyb = ds.to(ctx.y_dtype) if (ctx.fused and not ctx.passthrough) else None
-            return ds, dyb, None, None, None, None
+            return ds, dyb, None, None, None, None, None
         dy2 = dh.reshape(-1, C)
         if ctx.kern:
             x32 = x2.dtype == F32
@@ -420,14 +475,24 @@ class LayerNormFn(torch.autograd.Function):
             if ds2 is not None and ds2.dtype != x2.dtype:
                 ds2 = ds2.to(x2.dtype)
             dx = torch.empty_like(x2)
-            # the fused form also hands the branch (y) its gradient in y's dtype
-            dyb = (torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype)
-                   if (ctx.fused and x32 and not ctx.passthrough) else None)
+            split_out = ctx.split_out and x32 and dy2.dtype == BF16
+            # the fused form also hands the branch (y) its gradient in y's dtype (split: the
+            # hi plane of dx itself)
+            if split_out:
+                dyb = dx.view(BF16).view(-1)[:N * C].view(N, C)
+            else:
+                dyb = (torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype)
+                       if (ctx.fused and x32 and not ctx.passthrough) else None)
             nblk = min(_LN_BWD_BLOCKS_X32 if x32 else _LN_BWD_BLOCKS, max(1, (N + 7) // 8))
             dw_part = torch.empty(nblk, C, device=dh.device, dtype=F32)
             db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
             wc = compute_weight(w, dy2.dtype)
-            if x32:
+            if x32 and (ds_split or split_out):
+                _lib.call("nsa_layernorm_bwd_x32s", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
+                          _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), None, _lib.ptr(dw_part),
+                          _lib.ptr(db_part), N, C, nblk, (1 if ds_split else 0) | (2 if split_out else 0),
+                          _lib.stream())
+            elif x32:
                 _lib.call(_sym("nsa_layernorm_bwd_x32", dy2.dtype), _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
                           _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), _lib.ptr(dyb), _lib.ptr(dw_part),
                           _lib.ptr(db_part), N, C, nblk, _lib.stream())
@@ -438,9 +503,11 @@ class LayerNormFn(torch.autograd.Function):
             gw = _colsum_into(w, dw_part)
             gb = _colsum_into(b, db_part) if b is not None else None
             dx = dx.view(shape)
+            if split_out:
+                dx._nsa_split = True
             if not ctx.fused or ctx.passthrough:
-                return dx, None, gw, gb, None, None
-            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None, None
+                return dx, None, gw, gb, None, None, None
+            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None, None, None
         xf = x2.float()
         d = dy2.float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
@@ -453,8 +520,8 @@ class LayerNormFn(torch.autograd.Function):
         gb = _accumulate(b, d.sum(0)) if b is not None else None
         dxs = dx.to(x2.dtype).view(shape)
         if not ctx.fused or ctx.passthrough:
-            return dxs, None, gw, gb, None, None
-        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None, None
+            return dxs, None, gw, gb, None, None, None
+        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None, None, None
 
 
 def _colsum_into(p, partial):
@@ -484,12 +551,14 @@ def layer_norm_pass(x, w, b, out_dtype=None):
     return LayerNormFn.apply(x, None, w, b, out_dtype, True)
 
 
-def add_layer_norm(x, y, w, b, out_dtype=None):
+def add_layer_norm(x, y, w, b, out_dtype=None, split_grad=False):
     """Fused residual add + LayerNorm: returns (x + y, LN(x + y)).
 
     x + y keeps x's (residual-stream) dtype; LN(x + y) is in ``out_dtype``
-    (default y's dtype, the compute dtype)."""
-    return LayerNormFn.apply(x, y, w, b, out_dtype)
+    (default y's dtype, the compute dtype).  ``split_grad``: x is the residual output of
+    another ``add_layer_norm`` / ``layer_norm_pass`` and nothing else reads it, so x's
+    gradient may travel in the split-plane encoding (see LayerNormFn)."""
+    return LayerNormFn.apply(x, y, w, b, out_dtype, False, split_grad)
 
 
 # ----------------------------------------------------------------------------
@@ -628,12 +697,12 @@ def _attn_reference(q, k, v, p, seed):
     att = att.masked_fill(~mask, float("-inf"))
     att = torch.softmax(att, dim=-1)
     if p > 0:
-        att = att * _cpu_keep_mask(att.shape, p, seed).to(att.device) / (1.0 - p)
+        att = att * _cpu_keep_mask(att.shape, p, seed, att.device) / (1.0 - p)
     return att @ v
 
 
 _FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6}
-_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3}
+_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3, "v4": 4}
 
 
 @contextlib.contextmanager

@@ -370,6 +370,76 @@ def test_layernorm_raw_nan_prefilled(kernels):
     assert torch.allclose(dbp.sum(0), bq.grad, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("split", [1, 2, 3])
+def test_layernorm_bwd_split_planes(kernels, split):
+    """nsa_layernorm_bwd_x32s against nsa_layernorm_bwd_x32 on the same inputs, NaN-prefilled
+    outputs: a split-plane dres (bit 0) is read back exactly and a split dx (bit 1) decodes to
+    the plain kernel's fp32 dx bit for bit, its hi plane equal to the host encoding and to the
+    plain bf16 branch copy away from exact rounding ties."""
+    from nanosandbox_amd.ops import _lib
+    from nanosandbox_amd.ops.functional import split_planes, unsplit_planes
+    torch.manual_seed(11)
+    N, C = 1100, 768
+    s = torch.randn(N, C, device=DEV) * 2 + 0.5
+    w = (torch.randn(C, device=DEV) * 0.5 + 1).to(BF)
+    mean = s.mean(-1)
+    rstd = torch.rsqrt(s.var(-1, unbiased=False) + 1e-5)
+    dh = torch.randn(N, C, device=DEV).to(BF)
+    dres = torch.randn(N, C, device=DEV) * 0.1
+    dres[0, :4] = torch.tensor([1e30, -3e-39, 0.0, -0.0])  # large, denormal, signed zeros
+    nblk = 16
+    nan = lambda *sh, dt=torch.float32: torch.full(sh, float("nan"), device=DEV, dtype=dt)  # noqa: E731
+    dx0, dxb0, dwp0 = nan(N, C), nan(N, C, dt=BF), nan(nblk, C)
+    _lib.call("nsa_layernorm_bwd_x32", _lib.ptr(dh), _lib.ptr(s), _lib.ptr(w), _lib.ptr(mean), _lib.ptr(rstd),
+              _lib.ptr(dres), _lib.ptr(dx0), _lib.ptr(dxb0), _lib.ptr(dwp0), None, N, C, nblk, _lib.stream())
+    din = split_planes(dres) if split & 1 else dres
+    dx1, dwp1 = nan(N, C), nan(nblk, C)
+    _lib.call("nsa_layernorm_bwd_x32s", _lib.ptr(dh), _lib.ptr(s), _lib.ptr(w), _lib.ptr(mean), _lib.ptr(rstd),
+              _lib.ptr(din), _lib.ptr(dx1), None, _lib.ptr(dwp1), None, N, C, nblk, split, _lib.stream())
+    torch.cuda.synchronize()
+    assert not torch.isnan(dx0).any()
+    if split & 2:
+        assert torch.equal(unsplit_planes(dx1), dx0)
+        hi = dx1.view(BF).reshape(-1)[:N * C].view(N, C)
+        tie = (dx0.view(torch.int32) & 0xFFFF) == 0x8000  # the one place ties-away and RNE differ
+        assert torch.equal(hi[~tie], dxb0[~tie])
+        assert torch.equal(hi, split_planes(dx0).view(BF).reshape(-1)[:N * C].view(N, C))
+    else:
+        assert torch.equal(dx1, dx0)
+    assert torch.equal(dwp1, dwp0)
+
+
+def test_gpt_split_residual_grad_matches_plain(kernels):
+    """The GPT trunk with split-plane residual gradients (default) against plain fp32 + bf16-copy
+    gradients, deterministic mode: the residual path is exact, so the parameter gradients
+    differ only through branch-gradient elements at exact rounding ties (ties away from zero
+    vs to even: one bf16 ulp at about 2^-16 of the elements)."""
+    from nanosandbox_amd.models.gpt import GPT, GPTConfig
+    from nanosandbox_amd.ops import functional as Fn
+    torch.manual_seed(2)
+    cfg = GPTConfig(block_size=256, vocab_size=512, n_layer=3, n_head=4, n_embd=256, dropout=0.0, bias=True)
+    model = GPT(cfg).to(DEV).set_compute_dtype(BF)
+    idx = torch.randint(0, 512, (4, 256), device=DEV)
+    tgt = torch.randint(0, 512, (4, 256), device=DEV)
+    prev = (Fn.LN_SPLIT, Fn._gd.DETERMINISTIC)
+    grads = []
+    try:
+        Fn.set_deterministic(True)
+        for flag in (True, False, True):
+            Fn.LN_SPLIT = flag
+            model.zero_grad(set_to_none=True)
+            _, loss = model(idx, tgt)
+            loss.backward()
+            grads.append({n: p.grad.clone() for n, p in model.named_parameters()})
+    finally:
+        Fn.LN_SPLIT, Fn._gd.DETERMINISTIC = prev
+    for n in grads[0]:
+        assert torch.isfinite(grads[0][n]).all(), n
+        assert torch.equal(grads[0][n], grads[2][n]), n  # the split run itself is reproducible
+        ref = grads[1][n]
+        assert ((grads[0][n] - ref).abs() <= 2 ** -10 * ref.abs().max() + 1e-9).all(), n
+
+
 def test_embedding_raw_nan_prefilled(kernels):
     """nsa_embedding_fwd_x32 into a NaN-prefilled fp32 stream: wte[idx] + wpe[t], bit-exact
     (a sum of two bf16 values is exact in fp32) for every element, repeated and last-id
@@ -538,14 +608,16 @@ def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
     assert ((lse - lref[None, None]).abs() <= 1e-5 * lref[None, None] + 1e-6).all()
 
 
+@pytest.mark.parametrize("bwd", ["v3", "v4"])
 @pytest.mark.parametrize("T", [1024, 320, 96])
-def test_flash_bwd_exact_structure(kernels, flash_variant, T):
+def test_flash_bwd_exact_structure(kernels, flash_variant, T, bwd):
     """Backward counterpart: Q = 0 (uniform P = 1/(q+1)), K one-hot by key tile, dO one-hot
     by query slice, V random.  Every gradient element is compared with the fp32 reference
     against a bound scaled by the absolute terms that form it, so a skipped query slice
     (dK / dV) or key tile (dQ) is a whole column far outside its bound."""
     from nanosandbox_amd.ops import functional as fn
 
+    flash_variant(bwd=bwd)
     B, H, D = 1, 2, 64
     C = H * D
     k_idx = torch.arange(T, device=DEV)
@@ -640,10 +712,11 @@ def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
 
 
 @pytest.mark.parametrize("T", [320, 1024, 96, 64])
-@pytest.mark.parametrize("ver", ["v3"])
+@pytest.mark.parametrize("ver", ["v3", "v4"])
 def test_flash_bwd_pair_matches_v2(kernels, flash_variant, T, ver):
-    """Backward v3 (the default: the v2 dK/dV kernel with two query slices per barrier)
-    against v2 (one slice per barrier), bitwise (same per-slice arithmetic)."""
+    """Backward v3 (the default: the v2 dK/dV kernel with two query slices per barrier) and
+    v4 (v3 with the dQ tile's key halves software-pipelined) against v2 (one slice per
+    barrier), bitwise (same per-slice arithmetic, same accumulation order)."""
     from nanosandbox_amd.ops import functional as fn
 
     torch.manual_seed(0)

@@ -243,3 +243,34 @@ def test_from_pretrained_matches_hf_gpt2_forward(tmp_path, monkeypatch):
     rel = ((last[:, -1].float() - ref[:, -1]).norm() / ref[:, -1].norm()).item()
     assert rel < 1e-4, rel
     assert abs(loss.item() - out.loss.item()) < 1e-4 * abs(out.loss.item()), (loss.item(), out.loss.item())
+
+
+def test_split_planes_roundtrip_bitwise():
+    """The split-plane residual-gradient encoding (LayerNorm backward, csrc/kernels/layernorm.hip
+    split8): hi + lo give g back bit for bit at binade edges, denormals, signed zeros,
+    infinities and arbitrary bit patterns (a NaN stays a NaN); the hi plane is bf16(g) rounded
+    to nearest, equal to torch's cast except at exact ties, which round away from zero."""
+    from nanosandbox_amd.ops.functional import split_planes, unsplit_planes
+    torch.manual_seed(0)
+    g = torch.randn(64, 48) * torch.logspace(-40, 38, 48)[None]
+    special = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), 1e-45, -1e-45, 3.4e38, -3.4e38,
+                            1.00390625, -1.00390625, 1.01171875, 1.0 + 2 ** -8 + 2 ** -20, 255.99998])
+    g[0, :special.numel()] = special
+    bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (16, 48), dtype=torch.int64).to(torch.int32)
+    g[-16:] = bits.view(torch.float32)  # arbitrary bit patterns, NaNs included
+    enc = split_planes(g)
+    assert enc.dtype == torch.float32 and enc.shape == g.shape
+    n = g.numel()
+    fin = ~torch.isnan(g)
+    tie = (g.view(torch.int32) & 0xFFFF) == 0x8000
+    hi = enc.reshape(-1).view(torch.bfloat16)[:n].view(g.shape)
+    rne = g.to(torch.bfloat16)
+    sel = fin & ~tie
+    assert torch.equal(hi.view(torch.int16)[sel], rne.view(torch.int16)[sel])
+    assert tie[0, 8] and tie[0, 9] and tie[0, 10]
+    assert hi[0, 8].item() == 1.0078125 and hi[0, 9].item() == -1.0078125  # away from zero
+    assert hi[0, 10].item() == 1.015625  # (1.01171875 is a tie between 1.0078125 and 1.015625)
+    assert torch.isnan(hi[~fin]).all()
+    back = unsplit_planes(enc)
+    assert torch.equal(back.view(torch.int32)[fin], g.view(torch.int32)[fin])
+    assert torch.isnan(back[~fin]).all()
