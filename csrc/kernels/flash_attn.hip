@@ -137,12 +137,14 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4: D = 64 forward kernel; auto = v4
 //         (v3 with two K/V tiles per barrier) without dropout once the grid has >= 4096
 //         v3 workgroups, else v1 (fwd_launch); v3 = one tile per barrier
-//   bwd   NSA_FLASH_BWD = v3 (default) | v4 | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
-//         kernel taking two query slices per barrier; v4 = v3 with the dQ tile's two key
-//         halves software-pipelined; v1 = the generic kernels
+//   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
+//         kernel taking two query slices per barrier; v1 = the generic kernels
+//         (software-pipelining the dQ tile's / the dK/dV slice pair's MFMAs under each
+//         other's VALU with sched_group_barrier measured no gain / a spilling kernel:
+//         docs/performance.md, round 5)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
 enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6 };
-enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3, BWD_V4 = 4 };
+enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
@@ -159,7 +161,7 @@ FlashConfig& flash_config() {
     if (const char* e = getenv("NSA_FLASH_FWD"))
       d.fwd = (e[0] == 'v' && (e[1] == '1' || (e[1] >= '3' && e[1] <= '6'))) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
-      d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '4') ? e[1] - '0' : BWD_V3;
+      d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
     return d;
   }();
@@ -1937,84 +1939,12 @@ constexpr int DQ2_T = 64 * 64 * 2;  // one [64][64] bf16 tile
 #define NSA_DQ2_OCC 2  // waves per SIMD the v2 dQ kernel is compiled for
 #endif
 
-// PIPE (backward v4): the tile's two 32-key halves software-pipelined (see below)
-template <bool MASK, bool DROP, bool PIPE = false>
+template <bool MASK, bool DROP>
 __device__ __forceinline__ void dq2_tile(const char* kt, const char* vt, const bf16x8 (&qf)[4],
                                          const bf16x8 (&gf)[4], const f32x16& ndt, f32x16 (&dq)[2], float lse2,
                                          int kv0, int qpos, int h, int r, int lane, float scale_log2,
                                          const DropArgs& dr) {
   constexpr int D = 64;
-  if constexpr (PIPE && !DROP) {
-    // software pipeline over the tile's two 32-key halves, fixed by sched_group_barrier:
-    // every K / V fragment read first; half 1's S / dP MFMAs under half 0's softmax-gradient
-    // VALU; half 0's dQ MFMAs under half 1's VALU (no LDS read -> wait -> MFMA chains)
-    bf16x8 kf[2][4], vf[2][4];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        kf[sb][ks] = as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h)));
-        vf[sb][ks] = as_frag(lds_b128(vt, swz<D>(32 * sb + r, 2 * ks + h)));
-      }
-    f32x16 st[2], pt[2];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      st[sb] = f32x16{};
-      pt[sb] = ndt;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(kf[sb][ks], qf[ks], st[sb]);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) pt[sb] = mfma(vf[sb][ks], gf[ks], pt[sb]);
-    }
-    bf16x8 dsf[2][2], tf[2][2][2];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      float dsv[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kpos = kv0 + 32 * sb + acc_row(i, h);
-        float p = fast_exp2(st[sb][i] * scale_log2 - lse2);
-        if constexpr (MASK) p = kpos > qpos ? 0.0f : p;
-        dsv[i] = p * pt[sb][i];
-      }
-      pack16(dsv, dsf[sb]);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) tf[sb][s][dt] = tr_frag<D>(kt, r0, r0 + 8, 32 * dt, lane);
-      }
-    }
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma(tf[sb][s][dt], dsf[sb][s], dq[dt]);
-    // schedule: 8 reads (half 0) | 8 x (MFMA, read of half 1) | 8 x (MFMA, 6 VALU of half 0,
-    // a transposed read of half 0) | 4 x (MFMA, 12 VALU of half 1, 2 transposed reads) | 4 MFMA
-    constexpr int kDSR = 0x100, kMFMA = 0x8, kVALU = 0x2;
-    __builtin_amdgcn_sched_group_barrier(kDSR, 8, 0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(kDSR, 1, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(kVALU, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(kDSR, 1, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(kVALU, 12, 0);
-      __builtin_amdgcn_sched_group_barrier(kDSR, 2, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(kMFMA, 4, 0);
-    return;
-  }
   f32x16 st[2], pt[2];
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
@@ -2055,7 +1985,7 @@ __device__ __forceinline__ void dq2_tile(const char* kt, const char* vt, const b
 }
 
 
-template <bool DROP, bool PIPE = false>
+template <bool DROP>
 __global__ __launch_bounds__(256, NSA_DQ2_OCC) void flash_bwd_dq2_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
     const float* __restrict__ lse, float* __restrict__ nls, float* __restrict__ nd, bf16_t* __restrict__ dqkv, int B,
@@ -2155,14 +2085,14 @@ __global__ __launch_bounds__(256, NSA_DQ2_OCC) void flash_bwd_dq2_kernel(
   auto tile_full = [&](int j) {
     auto f = [&](auto slot) {
       const char* kt = smem + decltype(slot)::value * SLOT;
-      dq2_tile<false, DROP, PIPE>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
+      dq2_tile<false, DROP>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
     };
     slot_dispatch<0, NS>(j % NS, f);
   };
   auto tile_diag = [&](int j) {
     auto f = [&](auto slot) {
       const char* kt = smem + decltype(slot)::value * SLOT;
-      dq2_tile<true, DROP, PIPE>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
+      dq2_tile<true, DROP>(kt, kt + DQ2_T, qf, gf, ndt, dq, lse2, 64 * j, qpos, h, r, lane, scale_log2, dr);
     };
     slot_dispatch<0, NS>(j % NS, f);
   };
@@ -2309,11 +2239,6 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
     flash_bwd_dq2_kernel<true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                             (const bf16_t*)o, (const float*)lse, nls, nd, (bf16_t*)dqkv,
                                                             B, T, H, scale, scale * kLog2e, th, dscale, seed, order);
-  else if (flash_config().bwd == BWD_V4)
-    flash_bwd_dq2_kernel<false, true><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
-                                                                   (const bf16_t*)o, (const float*)lse, nls, nd,
-                                                                   (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e, th,
-                                                                   dscale, seed, order);
   else
     flash_bwd_dq2_kernel<false><<<n_qt * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                              (const bf16_t*)o, (const float*)lse, nls, nd,
@@ -2325,7 +2250,7 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   // two query slices per barrier (v3, default): B120 T1024 H12 whole backward 1151 vs 1181 us
   // (profiles/r4_attn_ab_pair.log; the same change in the dQ kernel measured 1152)
   // (three slices per barrier in a 6-slot ring measured 1171 vs 1141 us: profiles/r4_attn_ab_dkdv_g3.log)
-  if (flash_config().bwd >= BWD_V3 && !th)
+  if (flash_config().bwd == BWD_V3 && !th)
     flash_bwd_dkdv2_kernel<1, 4, false, 2><<<n_kb * B * H, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout,
                                                                           nls, nd, (bf16_t*)dqkv, B, T, H, scale,
                                                                           scale * kLog2e, th, dscale, seed, order);
@@ -2381,14 +2306,13 @@ NSA_API hipError_t NSA_FA_SYM(nsa_flash_fwd)(const void* qkv, void* out, void* l
 #if !NSA_FA_F16
 NSA_API void* nsa_flash_config_ptr() { return &flash_config(); }
 
-// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5 / 6 v6, bwd 1 v1 / 2 v2 / 3 v3 /
-// 4 v4, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5 / 6 v6, bwd 1 v1 / 2 v2 / 3 v3, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
 // fwd | bwd << 4 | order << 8.
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || (fwd >= FWD_V3 && fwd <= FWD_V6)) c.fwd = fwd;
-  if (bwd >= BWD_V1 && bwd <= BWD_V4) c.bwd = bwd;
+  if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order >= 0 && order <= 2) c.order = order;
   return prev;
 }

@@ -321,14 +321,21 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
         unpack_raw(cx[k], xv);
         unpack8e<H>(cd[k], dv);
         unpack8e<H>(wraw[k], wf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[j] * wf[j] - m1 - (xv[j] - mean) * rstd * m2);
-        if (dres) {  // gradient arriving through the residual path of the fused add
-          float rv[8];
+        float rv[8];  // gradient arriving through the residual path of the fused add
+        if (dres) {
           if constexpr (SPLIT & 1) unsplit8(cr[k].u[0], cr[k].u[Raw8<XT>::W - 1], rv);
           else unpack_raw(cr[k], rv);
+        } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += rv[j];
+          for (int j = 0; j < 8; ++j) rv[j] = 0.0f;
+        }
+        // explicit fused multiply-adds: the same roundings in every instantiation (the
+        // split-plane and plain forms agree bit for bit, whatever the compiler contracts)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mean) * rstd;
+          const float t = __builtin_fmaf(-xh, m2, __builtin_fmaf(dv[j], wf[j], -m1));
+          o[j] = __builtin_fmaf(rstd, t, rv[j]);
         }
         if constexpr (SPLIT & 2) {  // hi plane: plain store (the branch GEMMs read it next)
           uint4 hi, lo;

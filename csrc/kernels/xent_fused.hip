@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void xent_tlogit_kernel(const bf16_t* __restri
 }
 
 // S_r = sum of the GEMM epilogue's partials; loss_r = log S_r, invS_r = 1 / S_r (0 and 0 for
-// an ignored row); rows outside [0.5, 1e30] go on the fix-up list
+// an ignored row); rows outside [0.5, 1e30] go on the fix-up list (ignored rows above 1e30 too)
 __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restrict__ part, int slots,
                                                            const int* __restrict__ t32, float* __restrict__ loss,
                                                            float* __restrict__ invS, int* __restrict__ nfix,
@@ -58,6 +58,9 @@ __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restri
   if (t32[row] < 0) {
     loss[row] = 0.0f;
     invS[row] = 0.0f;
+    // an ignored row is scaled by 0 in both backward GEMMs, which an overflowed E (inf, with
+    // the shift c = 0: any logit above ~88) would turn into NaN: the fix-up zeroes its E row
+    if (!(S <= 1e30f)) fixlist[atomicAdd(nfix, 1)] = row;
     return;
   }
   if (!(S >= 0.5f && S <= 1e30f)) {  // also catches NaN / inf
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restri
 }
 
 // Exact recompute of a flagged row: logits l_v = x_r · W_v (fp32), m = max, E = exp(l - m),
-// S = sum E, loss = m + log S - l_t.  One workgroup per listed row (grid-stride over the
+// S = sum E, loss = m + log S - l_t (a flagged ignored row: E = 0).  One workgroup per listed row (grid-stride over the
 // device-side count: with no flagged row every workgroup exits at once).
 __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restrict__ x, int ldx,
                                                          const bf16_t* __restrict__ W, int ldw, bf16_t* __restrict__ E,
@@ -85,6 +88,11 @@ __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restric
   for (int f = blockIdx.x; f < n; f += gridDim.x) {
     const int row = fixlist[f];
     __syncthreads();
+    if (t32[row] < 0) {  // ignored row (workgroup-uniform): E = 0, loss and 1/S stay 0
+      for (int v = threadIdx.x * 8; v < Vpad; v += 256 * 8)
+        *reinterpret_cast<uint4*>(E + (int64_t)row * lde + v) = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
     for (int c = threadIdx.x; c < C; c += 256) xs[c] = bf2f(x[(int64_t)row * ldx + c]);
     __syncthreads();
     auto logit = [&](int v) {

@@ -702,7 +702,7 @@ def _attn_reference(q, k, v, p, seed):
 
 
 _FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6}
-_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3, "v4": 4}
+_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3}
 
 
 @contextlib.contextmanager

@@ -608,7 +608,7 @@ def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
     assert ((lse - lref[None, None]).abs() <= 1e-5 * lref[None, None] + 1e-6).all()
 
 
-@pytest.mark.parametrize("bwd", ["v3", "v4"])
+@pytest.mark.parametrize("bwd", ["v2", "v3"])
 @pytest.mark.parametrize("T", [1024, 320, 96])
 def test_flash_bwd_exact_structure(kernels, flash_variant, T, bwd):
     """Backward counterpart: Q = 0 (uniform P = 1/(q+1)), K one-hot by key tile, dO one-hot
@@ -712,11 +712,10 @@ def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
 
 
 @pytest.mark.parametrize("T", [320, 1024, 96, 64])
-@pytest.mark.parametrize("ver", ["v3", "v4"])
+@pytest.mark.parametrize("ver", ["v3"])
 def test_flash_bwd_pair_matches_v2(kernels, flash_variant, T, ver):
-    """Backward v3 (the default: the v2 dK/dV kernel with two query slices per barrier) and
-    v4 (v3 with the dQ tile's key halves software-pipelined) against v2 (one slice per
-    barrier), bitwise (same per-slice arithmetic, same accumulation order)."""
+    """Backward v3 (the default: the v2 dK/dV kernel with two query slices per barrier)
+    against v2 (one slice per barrier), bitwise (same per-slice arithmetic)."""
     from nanosandbox_amd.ops import functional as fn
 
     torch.manual_seed(0)
