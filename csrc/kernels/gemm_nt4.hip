@@ -357,7 +357,7 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           // no early exit here: every lane takes part in the row reduction
           const float c = crow[i][e];
           uint32_t w[4];
-          float s = 0.0f;
+          float s = 0.0f, mx = 0.0f;
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][2 * h][e], kLog2e, -c));
@@ -366,9 +366,13 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
               e0 = col + 2 * h < g.nvalid ? e0 : 0.0f;
               e1 = col + 2 * h + 1 < g.nvalid ? e1 : 0.0f;
             }
-            w[h] = q_pk(e0, e1);
+            w[h] = H ? pk2<true>(e0, e1) : q_pk(e0, e1);
             s += e0 + e1;
+            if constexpr (H) mx = __builtin_fmaxf(mx, __builtin_fmaxf(e0, e1));
           }
+          // fp16 E saturates at 65504 (a logit ~11 nats above the row's target): such a row's
+          // sum is made inf, so nsa_xent_combine sends it to the exact fix-up
+          if constexpr (H) s = mx > 65504.0f ? __builtin_inff() : s;
           rs[e] = q_rowsum16(col < nlo ? 0.0f : s);
           if (!skip) {
             if constexpr (NOSTORE) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
@@ -384,8 +388,9 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             const uint32_t wr = uv[i & 1][e][h];
-            w[h] = q_pk(__builtin_fmaf(sc, acc[i][2 * h][e], -gw * __uint_as_float(wr << 16)),
-                        __builtin_fmaf(sc, acc[i][2 * h + 1][e], -gw * __uint_as_float(wr & 0xffff0000u)));
+            const float v0 = __builtin_fmaf(sc, acc[i][2 * h][e], -gw * lo2f<H>(wr));
+            const float v1 = __builtin_fmaf(sc, acc[i][2 * h + 1][e], -gw * hi2f<H>(wr));
+            w[h] = H ? pk2<true>(v0, v1) : q_pk(v0, v1);
           }
         } else if constexpr (BIAS) {
 #pragma unroll
@@ -768,9 +773,10 @@ NSA_API hipError_t nsa_gemm_nt4_h(int epi, const void* A, int lda, const void* B
 // that half tile (2 * ceil(N / 256) slots of M floats).  c = the target logit of the row
 // (computed before this GEMM), so sum_j E = exp(loss_row) >= ~1: no overflow short of a
 // per-token loss of ~80 nats (nsa_xent_combine flags such rows for an exact recompute).
-NSA_API hipError_t nsa_gemm_nt4_xent(const void* A, int lda, const void* B, int ldb, void* E, int ldc,
-                                     const void* crow, void* part, int M, int N, int nvalid, int K, int grid,
-                                     hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t nt4_xent_entry(const void* A, int lda, const void* B, int ldb, void* E, int ldc, const void* crow,
+                          void* part, int M, int N, int nvalid, int K, int grid, hipStream_t s) {
   Nt4Args a{};
   a.A = (const bf16_t*)A;
   a.B = (const bf16_t*)B;
@@ -788,16 +794,33 @@ NSA_API hipError_t nsa_gemm_nt4_xent(const void* A, int lda, const void* B, int 
     return hipErrorInvalidValue;
   nt4_geometry(a, 0);
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
-  nt4_launch<Q_EPI_XENT, false>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
+  nt4_launch<Q_EPI_XENT, false, H>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
   return hipGetLastError();
+}
+}  // namespace
+NSA_API hipError_t nsa_gemm_nt4_xent(const void* A, int lda, const void* B, int ldb, void* E, int ldc,
+                                     const void* crow, void* part, int M, int N, int nvalid, int K, int grid,
+                                     hipStream_t s) {
+  return nt4_xent_entry<false>(A, lda, B, ldb, E, ldc, crow, part, M, N, nvalid, K, grid, s);
+}
+// fp16 operands and E = exp(logit - target logit) in fp16: entries far below the target sit in
+// fp16's subnormal range (absolute precision 2^-24, as autocast's fp16 dlogits), and a row
+// whose largest logit passes its target's by more than ~11 nats (an E entry above 65504)
+// returns an inf row sum, which nsa_xent_combine sends to the exact fix-up.
+NSA_API hipError_t nsa_gemm_nt4_xent_h(const void* A, int lda, const void* B, int ldb, void* E, int ldc,
+                                       const void* crow, void* part, int M, int N, int nvalid, int K, int grid,
+                                       hipStream_t s) {
+  return nt4_xent_entry<true>(A, lda, B, ldb, E, ldc, crow, part, M, N, nvalid, K, grid, s);
 }
 
 // Fused cross-entropy, input gradient: C = cs[row] * (A · B^T) - cw[row] * U with A = E [M, K]
 // (the forward's exp), B = W^T [N, K] (K = the padded vocabulary), U [M, N] (ld ldc) = the
 // rows W[target] gathered by nsa_xent_bwd_prep, and rowc [M][2] = {cs, cw} = {g / S, g} (0, 0
 // for an ignored row): g (softmax - onehot) · W with the subtraction in fp32.
-NSA_API hipError_t nsa_gemm_nt4_xdx(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
-                                    const void* U, const void* rowc, int M, int N, int K, int grid, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t nt4_xdx_entry(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* U,
+                         const void* rowc, int M, int N, int K, int grid, hipStream_t s) {
   Nt4Args a{};
   a.A = (const bf16_t*)A;
   a.B = (const bf16_t*)B;
@@ -813,6 +836,15 @@ NSA_API hipError_t nsa_gemm_nt4_xdx(const void* A, int lda, const void* B, int l
   if (nt4_check(a, grid) != hipSuccess || M % 4 || !U || !rowc) return hipErrorInvalidValue;
   nt4_geometry(a, 0);
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
-  nt4_launch<Q_EPI_XDX, false>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
+  nt4_launch<Q_EPI_XDX, false, H>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
   return hipGetLastError();
+}
+}  // namespace
+NSA_API hipError_t nsa_gemm_nt4_xdx(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                    const void* U, const void* rowc, int M, int N, int K, int grid, hipStream_t s) {
+  return nt4_xdx_entry<false>(A, lda, B, ldb, C, ldc, U, rowc, M, N, K, grid, s);
+}
+NSA_API hipError_t nsa_gemm_nt4_xdx_h(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                      const void* U, const void* rowc, int M, int N, int K, int grid, hipStream_t s) {
+  return nt4_xdx_entry<true>(A, lda, B, ldb, C, ldc, U, rowc, M, N, K, grid, s);
 }

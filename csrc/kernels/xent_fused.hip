@@ -18,10 +18,12 @@ namespace {
 
 // c_r = x_r · W[t_r] (fp32 from bf16), t32_r = t_r (or -1 when ignored / out of range): one
 // wave per row, 16-byte loads
+// H: fp16 x / W / E (dtype float16); shift: added to c (fp16 E range, see nsa_gemm_nt4_xent_h)
+template <bool H>
 __global__ __launch_bounds__(256) void xent_tlogit_kernel(const bf16_t* __restrict__ x, int ldx,
                                                           const bf16_t* __restrict__ W, int ldw,
                                                           const int64_t* __restrict__ tgt, float* __restrict__ crow,
-                                                          int* __restrict__ t32, int M, int C, int V) {
+                                                          int* __restrict__ t32, int M, int C, int V, float shift) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const int64_t t = tgt[row];
@@ -32,25 +34,28 @@ __global__ __launch_bounds__(256) void xent_tlogit_kernel(const bf16_t* __restri
     const bf16_t* wr = W + t * ldw;
     for (int c = lane * 8; c < C; c += 512) {
       float a[8], b[8];
-      load8(xr + c, a);
-      load8(wr + c, b);
+      load8e<H>(xr + c, a);
+      load8e<H>(wr + c, b);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s = __builtin_fmaf(a[j], b[j], s);
     }
     s = wave_sum(s);
   }
   if (lane == 0) {
-    crow[row] = s;
+    crow[row] = s + shift;
     t32[row] = valid ? (int)t : -1;
   }
 }
 
 // S_r = sum of the GEMM epilogue's partials; loss_r = log S_r, invS_r = 1 / S_r (0 and 0 for
 // an ignored row); rows outside [0.5, 1e30] go on the fix-up list (ignored rows above 1e30 too)
+// [lo, hi]: the range of S kept (bf16 E: [0.5, 1e30]; fp16 E, shifted: [0.5 e^-shift, 6e4]);
+// loss = log S + shift
 __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restrict__ part, int slots,
                                                            const int* __restrict__ t32, float* __restrict__ loss,
                                                            float* __restrict__ invS, int* __restrict__ nfix,
-                                                           int* __restrict__ fixlist, int M) {
+                                                           int* __restrict__ fixlist, int M, float lo, float hi,
+                                                           float shift) {
   const int row = blockIdx.x * 256 + threadIdx.x;
   if (row >= M) return;
   float S = 0.0f;
@@ -60,22 +65,23 @@ __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restri
     invS[row] = 0.0f;
     // an ignored row is scaled by 0 in both backward GEMMs, which an overflowed E (inf, with
     // the shift c = 0: any logit above ~88) would turn into NaN: the fix-up zeroes its E row
-    if (!(S <= 1e30f)) fixlist[atomicAdd(nfix, 1)] = row;
+    if (!(S <= hi)) fixlist[atomicAdd(nfix, 1)] = row;
     return;
   }
-  if (!(S >= 0.5f && S <= 1e30f)) {  // also catches NaN / inf
+  if (!(S >= lo && S <= hi)) {  // also catches NaN / inf
     fixlist[atomicAdd(nfix, 1)] = row;
     loss[row] = 0.0f;
     invS[row] = 0.0f;
     return;
   }
-  loss[row] = __logf(S);
+  loss[row] = __logf(S) + shift;
   invS[row] = 1.0f / S;
 }
 
 // Exact recompute of a flagged row: logits l_v = x_r · W_v (fp32), m = max, E = exp(l - m),
 // S = sum E, loss = m + log S - l_t (a flagged ignored row: E = 0).  One workgroup per listed row (grid-stride over the
 // device-side count: with no flagged row every workgroup exits at once).
+template <bool H>
 __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restrict__ x, int ldx,
                                                          const bf16_t* __restrict__ W, int ldw, bf16_t* __restrict__ E,
                                                          int lde, const int* __restrict__ t32,
@@ -93,14 +99,14 @@ __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restric
         *reinterpret_cast<uint4*>(E + (int64_t)row * lde + v) = make_uint4(0u, 0u, 0u, 0u);
       continue;
     }
-    for (int c = threadIdx.x; c < C; c += 256) xs[c] = bf2f(x[(int64_t)row * ldx + c]);
+    for (int c = threadIdx.x; c < C; c += 256) xs[c] = e2f<H>(x[(int64_t)row * ldx + c]);
     __syncthreads();
     auto logit = [&](int v) {
       const bf16_t* wr = W + (int64_t)v * ldw;
       float s = 0.0f;
       for (int c = 0; c < C; c += 8) {
         float b[8];
-        load8(wr + c, b);
+        load8e<H>(wr + c, b);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = __builtin_fmaf(xs[c + j], b[j], s);
       }
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restric
     float s = 0.0f;
     for (int v = threadIdx.x; v < Vpad; v += 256) {
       const float e = v < V ? __expf(logit(v) - m) : 0.0f;
-      E[(int64_t)row * lde + v] = f2bf(e);
+      E[(int64_t)row * lde + v] = f2e<H>(e);
       s += e;
     }
     s = wave_sum(s);
@@ -131,6 +137,7 @@ __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restric
 
 // Backward prologue, per row: coefficient pair {g / S, g} (0, 0 ignored), the row W[t] gathered
 // for the dX epilogue, and xs = bf16(x g / S) for the weight-gradient GEMM
+template <bool H>
 __global__ __launch_bounds__(256) void xent_bwd_prep_kernel(const bf16_t* __restrict__ x, int ldx,
                                                             const bf16_t* __restrict__ W, int ldw,
                                                             const int* __restrict__ t32, const float* __restrict__ invS,
@@ -151,16 +158,17 @@ __global__ __launch_bounds__(256) void xent_bwd_prep_kernel(const bf16_t* __rest
   for (int c = lane * 8; c < C; c += 512) {
     *reinterpret_cast<uint4*>(wrows + (int64_t)row * C + c) = *reinterpret_cast<const uint4*>(wr + c);
     float a[8];
-    load8(xr + c, a);
+    load8e<H>(xr + c, a);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] *= sc;
-    store8(xs + (int64_t)row * C + c, a);
+    store8e<H>(xs + (int64_t)row * C + c, a);
   }
 }
 
 // The onehot part of dW, per valid row r with target t:  gW[t] += E[r,t] (s x_r - bf16(s x_r))
 // - g x_r  (s = g / S): subtracts g x_r and takes back the rounding the GEMM's bf16 operand
 // put on the target entry's product.  fp32 atomics, one wave per row.
+template <bool H>
 __global__ __launch_bounds__(256) void xent_dw_fix_kernel(const bf16_t* __restrict__ x, int ldx,
                                                           const bf16_t* __restrict__ E, int lde,
                                                           const int* __restrict__ t32, const float* __restrict__ invS,
@@ -172,62 +180,108 @@ __global__ __launch_bounds__(256) void xent_dw_fix_kernel(const bf16_t* __restri
   if (t < 0) return;
   const float g = *gsc;
   const float s = g * invS[row];
-  const float et = bf2f(E[(int64_t)row * lde + t]);
+  const float et = e2f<H>(E[(int64_t)row * lde + t]);
   const bf16_t* xr = x + (int64_t)row * ldx;
   float* gr = gW + (int64_t)t * ldg;
   // one column per lane per step: every atomic wave-instruction covers 256 contiguous
   // bytes of the target row (the full atomic rate; 8 columns per lane spread one
   // instruction over 2 KB and ran ~9x slower: 2.56 ms per micro-step at 122880 rows)
   for (int c = lane; c < C; c += 64) {
-    const float a = bf2f(xr[c]);
+    const float a = e2f<H>(xr[c]);
     const float p = s * a;
-    const float pr = bf2f(f2bf(p));
+    const float pr = e2f<H>(f2e<H>(p));
     atomicAdd(gr + c, et * (p - pr) - g * a);
   }
 }
 
 }  // namespace
 
-NSA_API hipError_t nsa_xent_tlogit(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow,
-                                   void* t32, int M, int C, int V, hipStream_t s) {
+namespace {
+template <bool H>
+hipError_t tlogit_entry(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow, void* t32, int M,
+                        int C, int V, float shift, hipStream_t s) {
   if (C % 8 || ldx % 8 || ldw % 8) return hipErrorInvalidValue;
-  xent_tlogit_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (const int64_t*)tgt,
-                                                 (float*)crow, (int*)t32, M, C, V);
+  xent_tlogit_kernel<H><<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw,
+                                                    (const int64_t*)tgt, (float*)crow, (int*)t32, M, C, V, shift);
   return hipGetLastError();
 }
+template <bool H>
+hipError_t fixup_entry(const void* x, int ldx, const void* W, int ldw, void* E, int lde, const void* t32,
+                       const void* nfix, const void* fixlist, void* loss, void* invS, int C, int V, int Vpad,
+                       hipStream_t s) {
+  if (C > 8192 || C % 8 || ldw % 8 || Vpad % 8 || lde % 8) return hipErrorInvalidValue;
+  xent_fixup_kernel<H><<<64, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (bf16_t*)E, lde,
+                                          (const int*)t32, (const int*)nfix, (const int*)fixlist, (float*)loss,
+                                          (float*)invS, C, V, Vpad);
+  return hipGetLastError();
+}
+template <bool H>
+hipError_t bwd_prep_entry(const void* x, int ldx, const void* W, int ldw, const void* t32, const void* invS,
+                          const void* gsc, void* coef, void* wrows, void* xs, int M, int C, hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldw % 8) return hipErrorInvalidValue;
+  xent_bwd_prep_kernel<H><<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (const int*)t32,
+                                                      (const float*)invS, (const float*)gsc, (float*)coef,
+                                                      (bf16_t*)wrows, (bf16_t*)xs, M, C);
+  return hipGetLastError();
+}
+template <bool H>
+hipError_t dw_fix_entry(const void* x, int ldx, const void* E, int lde, const void* t32, const void* invS,
+                        const void* gsc, void* gW, int ldg, int M, int C, hipStream_t s) {
+  xent_dw_fix_kernel<H><<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32,
+                                                    (const float*)invS, (const float*)gsc, (float*)gW, ldg, M, C);
+  return hipGetLastError();
+}
+}  // namespace
 
-// nfix must be zeroed by the caller before this launch (it is a stream-ordered counter)
+// c = the target logit (+ shift; 0 for bf16 E), t32 = the target or -1 (ignored / out of range)
+NSA_API hipError_t nsa_xent_tlogit(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow,
+                                   void* t32, int M, int C, int V, float shift, hipStream_t s) {
+  return tlogit_entry<false>(x, ldx, W, ldw, tgt, crow, t32, M, C, V, shift, s);
+}
+NSA_API hipError_t nsa_xent_tlogit_h(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow,
+                                     void* t32, int M, int C, int V, float shift, hipStream_t s) {
+  return tlogit_entry<true>(x, ldx, W, ldw, tgt, crow, t32, M, C, V, shift, s);
+}
+
+// nfix must be zeroed by the caller before this launch (it is a stream-ordered counter).
+// Rows with S outside [lo, hi] go on the fix-up list; loss = log S + shift.
 NSA_API hipError_t nsa_xent_combine(const void* part, int slots, const void* t32, void* loss, void* invS, void* nfix,
-                                    void* fixlist, int M, hipStream_t s) {
+                                    void* fixlist, int M, float lo, float hi, float shift, hipStream_t s) {
   xent_combine_kernel<<<(M + 255) / 256, 256, 0, s>>>((const float*)part, slots, (const int*)t32, (float*)loss,
-                                                      (float*)invS, (int*)nfix, (int*)fixlist, M);
+                                                      (float*)invS, (int*)nfix, (int*)fixlist, M, lo, hi, shift);
   return hipGetLastError();
 }
 
 NSA_API hipError_t nsa_xent_fixup(const void* x, int ldx, const void* W, int ldw, void* E, int lde, const void* t32,
                                   const void* nfix, const void* fixlist, void* loss, void* invS, int C, int V,
                                   int Vpad, hipStream_t s) {
-  if (C > 8192 || C % 8 || ldw % 8) return hipErrorInvalidValue;
-  xent_fixup_kernel<<<64, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (bf16_t*)E, lde,
-                                       (const int*)t32, (const int*)nfix, (const int*)fixlist, (float*)loss,
-                                       (float*)invS, C, V, Vpad);
-  return hipGetLastError();
+  return fixup_entry<false>(x, ldx, W, ldw, E, lde, t32, nfix, fixlist, loss, invS, C, V, Vpad, s);
+}
+NSA_API hipError_t nsa_xent_fixup_h(const void* x, int ldx, const void* W, int ldw, void* E, int lde, const void* t32,
+                                    const void* nfix, const void* fixlist, void* loss, void* invS, int C, int V,
+                                    int Vpad, hipStream_t s) {
+  return fixup_entry<true>(x, ldx, W, ldw, E, lde, t32, nfix, fixlist, loss, invS, C, V, Vpad, s);
 }
 
 NSA_API hipError_t nsa_xent_bwd_prep(const void* x, int ldx, const void* W, int ldw, const void* t32,
                                      const void* invS, const void* gsc, void* coef, void* wrows, void* xs, int M,
                                      int C, hipStream_t s) {
-  if (C % 8 || ldx % 8 || ldw % 8) return hipErrorInvalidValue;
-  xent_bwd_prep_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (const int*)t32,
-                                                   (const float*)invS, (const float*)gsc, (float*)coef,
-                                                   (bf16_t*)wrows, (bf16_t*)xs, M, C);
-  return hipGetLastError();
+  return bwd_prep_entry<false>(x, ldx, W, ldw, t32, invS, gsc, coef, wrows, xs, M, C, s);
+}
+NSA_API hipError_t nsa_xent_bwd_prep_h(const void* x, int ldx, const void* W, int ldw, const void* t32,
+                                       const void* invS, const void* gsc, void* coef, void* wrows, void* xs, int M,
+                                       int C, hipStream_t s) {
+  return bwd_prep_entry<true>(x, ldx, W, ldw, t32, invS, gsc, coef, wrows, xs, M, C, s);
 }
 
 NSA_API hipError_t nsa_xent_dw_fix(const void* x, int ldx, const void* E, int lde, const void* t32, const void* invS,
                                    const void* gsc, void* gW, int ldg, int M, int C, hipStream_t s) {
   if (C % 8 || ldx % 8) return hipErrorInvalidValue;
-  xent_dw_fix_kernel<<<(M + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32,
-                                                 (const float*)invS, (const float*)gsc, (float*)gW, ldg, M, C);
-  return hipGetLastError();
+  return dw_fix_entry<false>(x, ldx, E, lde, t32, invS, gsc, gW, ldg, M, C, s);
+}
+NSA_API hipError_t nsa_xent_dw_fix_h(const void* x, int ldx, const void* E, int lde, const void* t32,
+                                     const void* invS, const void* gsc, void* gW, int ldg, int M, int C,
+                                     hipStream_t s) {
+  if (C % 8 || ldx % 8) return hipErrorInvalidValue;
+  return dw_fix_entry<true>(x, ldx, E, lde, t32, invS, gsc, gW, ldg, M, C, s);
 }

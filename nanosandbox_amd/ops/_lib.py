@@ -105,8 +105,10 @@ _SIGNATURES = {
                           c_int, c_int, c_void_p],
     "nsa_gemm_nt4_xdx": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_void_p],
-    "nsa_xent_tlogit": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
-    "nsa_xent_combine": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "nsa_xent_tlogit": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float,
+                        c_void_p],
+    "nsa_xent_combine": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float,
+                         c_float, c_void_p],
     "nsa_xent_fixup": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p, c_int, c_int, c_int, c_void_p],
     "nsa_xent_bwd_prep": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

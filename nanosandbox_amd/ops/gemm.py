@@ -170,14 +170,15 @@ def small(a, b, epi=NT_EPI_BF16, u=None, bias=None, out=None, out2=None):
 
 
 def nt_xent(x, w, crow, part, nvalid, out=None):
-    """Fused cross-entropy forward GEMM: E = exp(x @ w^T - crow[:, None]) (bf16, columns >=
-    ``nvalid`` zero) and the per-half-tile row sums into ``part`` [2 * ceil(N / 256), M]."""
+    """Fused cross-entropy forward GEMM: E = exp(x @ w^T - crow[:, None]) (x's dtype, bf16 or
+    fp16; columns >= ``nvalid`` zero) and the per-half-tile row sums into ``part``
+    [2 * ceil(N / 256), M]."""
     M, K = x.shape
     N = w.shape[0]
     _check(x, "x")
     _check(w, "w")
-    e = _out(M, N, x.device, out)
-    _lib.call("nsa_gemm_nt4_xent", _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(e), e.stride(0),
+    e = _out(M, N, x.device, out, x.dtype)
+    _lib.call(_sym("nsa_gemm_nt4_xent", x), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(e), e.stride(0),
               _lib.ptr(crow), _lib.ptr(part), M, N, int(nvalid), K, num_cus(x.device), _lib.stream())
     return e
 
@@ -189,8 +190,8 @@ def nt_xdx(e, wt, wrows, coef, out=None):
     _check(e, "e")
     _check(wt, "wt")
     _check(wrows, "wrows")
-    c = _out(M, N, e.device, out)
-    _lib.call("nsa_gemm_nt4_xdx", _lib.ptr(e), e.stride(0), _lib.ptr(wt), wt.stride(0), _lib.ptr(c), c.stride(0),
+    c = _out(M, N, e.device, out, e.dtype)
+    _lib.call(_sym("nsa_gemm_nt4_xdx", e), _lib.ptr(e), e.stride(0), _lib.ptr(wt), wt.stride(0), _lib.ptr(c), c.stride(0),
               _lib.ptr(wrows), _lib.ptr(coef), M, N, K, num_cus(e.device), _lib.stream())
     return c
 

