@@ -134,9 +134,11 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4: D = 64 forward kernel; auto = v4
-//         (v3 with two K/V tiles per barrier) without dropout once the grid has >= 4096
-//         v3 workgroups, else v1 (fwd_launch); v3 = one tile per barrier
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4 | v5 | v6: D = 64 forward kernel;
+//         auto = v5 for bf16 / v4 for fp16 without dropout once the grid has >= 4096 v3
+//         workgroups, else v1 (fwd_launch); v3 = 64 queries per wave, one K/V tile per
+//         barrier; v4 = two tiles per barrier; v5 = v4's geometry with fast tiles (no running
+//         max while scores stay in range); v6 = v1's geometry with fast tiles
 //   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
 //         kernel taking two query slices per barrier; v1 = the generic kernels
 //         (software-pipelining the dQ tile's / the dK/dV slice pair's MFMAs under each
@@ -2146,14 +2148,17 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     const int sel = flash_config().fwd;
     const bool v3 = sel == FWD_V3 || sel == FWD_V4 || sel == FWD_V5 ||
                     (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
-    if (v3 && sel == FWD_V5 && !th && !kFaH) {  // (fp16 P cannot hold v5's m = 0 range: v4 instead)
+    // v5 (auto's pick for bf16: no running max while the scores stay in range): B120 T1024 H12
+    // 333.3 vs 338.1 us for v4, faster in 5 of 6 same-process A/Bs (profiles/r5_ab_*.log).
+    // fp16 P cannot hold v5's m = 0 range: v4 there.
+    if (v3 && (sel == FWD_V5 || sel == FWD_AUTO) && !th && !kFaH) {
       flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                       scale * kLog2e, order);
       return hipGetLastError();
     }
     if (v3) {
-      // v4 = v3 with two K/V tiles per barrier (auto's pick): B120 T1024 H12 335.5 vs
-      // 350.9 us (profiles/r4_attn_ab_pair.log)
+      // v4 = v3 with two K/V tiles per barrier (auto's pick for fp16): B120 T1024 H12 335.5
+      // vs 350.9 us (profiles/r4_attn_ab_pair.log)
       if (sel != FWD_V3 && !th)
         flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
                                                                         B, T, H, scale * kLog2e, th, dscale, seed);
