@@ -71,16 +71,24 @@ def nanogpt_lr(it, lr, warmup, decay_iters, min_lr):
 
 
 def run_parity(cfg, batches, lr=6e-4, min_lr=6e-5, warmup=10, weight_decay=0.1, betas=(0.9, 0.95), grad_clip=1.0,
-               seed=1337, device="cuda", log=None):
+               seed=1337, device="cuda", log=None, dtype=torch.bfloat16):
     """Train our model and the fp32 reference side by side; returns per-step records
-    {step, loss, loss_ref, lr}.  ``batches``: list of (X, Y) int64 CPU tensors."""
+    {step, loss, loss_ref, lr}.  ``batches``: list of (X, Y) int64 CPU tensors.  ``dtype``:
+    the compute dtype of our side (bf16, or fp16 with the dynamic loss scale as train.py
+    runs it: the loss times the device-resident scale, unscale / inf check / skip in the
+    optimizer's kernels)."""
     from ..models import GPT
     from ..optim import FlatParamStore
+    from ..optim.loss_scale import DynamicLossScale
 
     torch.manual_seed(seed)
-    model = GPT(cfg).to(device).set_compute_dtype(torch.bfloat16, residual_dtype=torch.float32)
-    store = FlatParamStore(model, device, compute_dtype=torch.bfloat16)
+    model = GPT(cfg).to(device).set_compute_dtype(dtype, residual_dtype=torch.float32)
+    store = FlatParamStore(model, device, compute_dtype=dtype)
     opt = model.configure_optimizers(weight_decay, lr, betas, "cuda", store=store)
+    scaler = None
+    if dtype == torch.float16:
+        scaler = DynamicLossScale(device=device)
+        opt.attach_loss_scale(scaler)
     ref = hf_reference(model, device)
     ropt = reference_optimizer(ref, lr, weight_decay, betas)
     steps = len(batches)
@@ -93,7 +101,7 @@ def run_parity(cfg, batches, lr=6e-4, min_lr=6e-5, warmup=10, weight_decay=0.1, 
             g["lr"] = cur
         X, Y = X.to(device), Y.to(device)
         _, loss = model(X, Y)
-        loss.backward()
+        (loss * scaler.scale_t if scaler is not None else loss).backward()
         if grad_clip:
             opt.clip_grad_norm_(grad_clip)
         opt.step()

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--block", type=int, default=1024)
     ap.add_argument("--lr", type=float, default=6e-4)
     ap.add_argument("--out", default="gpurun_out/loss_parity.jsonl")
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"])
     a = ap.parse_args()
     cfg = GPTConfig(block_size=a.block, vocab_size=50304, n_layer=a.layers, n_head=a.heads, n_embd=a.embd,
                     dropout=0.0, bias=False)
@@ -57,10 +58,11 @@ def main():
         if rec["step"] % 25 == 0:
             print(json.dumps(rec), flush=True)
 
-    recs = run_parity(cfg, batches, lr=a.lr, min_lr=a.lr / 10, warmup=max(1, a.steps // 30), log=log)
+    recs = run_parity(cfg, batches, lr=a.lr, min_lr=a.lr / 10, warmup=max(1, a.steps // 30), log=log,
+                      dtype=getattr(torch, a.dtype))
     rel = [abs(r["loss"] - r["loss_ref"]) / r["loss_ref"] for r in recs]
     tail = recs[-20:]
-    print(json.dumps({"summary": True, "steps": a.steps, "tokens_per_step": a.batch * a.block,
+    print(json.dumps({"summary": True, "dtype": a.dtype, "steps": a.steps, "tokens_per_step": a.batch * a.block,
                       "first": [round(recs[0]["loss"], 4), round(recs[0]["loss_ref"], 4)],
                       "last20_mean": [round(sum(r["loss"] for r in tail) / len(tail), 4),
                                       round(sum(r["loss_ref"] for r in tail) / len(tail), 4)],
