@@ -58,8 +58,16 @@ __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restri
                                                            float shift) {
   const int row = blockIdx.x * 256 + threadIdx.x;
   if (row >= M) return;
-  float S = 0.0f;
-  for (int k = 0; k < slots; ++k) S += part[(int64_t)k * M + row];
+  // 8 independent loads in flight per thread (the slot loop was one dependent chain of
+  // ~400 load-adds per row at GPT-2's 394 slots: 154 us for 194 MB)
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= slots; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(k + u) * M + row];
+  }
+  for (; k < slots; ++k) acc[0] += part[(int64_t)k * M + row];
+  const float S = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (t32[row] < 0) {
     loss[row] = 0.0f;
     invS[row] = 0.0f;
