@@ -139,15 +139,14 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 //         workgroups, else v1 (fwd_launch); v3 = 64 queries per wave, one K/V tile per
 //         barrier; v4 = two tiles per barrier; v5 = v4's geometry with fast tiles (no running
 //         max while scores stay in range); v6 = v1's geometry with fast tiles
-//   bwd   NSA_FLASH_BWD = v3 (default) | v4 | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
-//         kernel taking two query slices per barrier; v4 = the fused dK/dV/dQ kernel (dQ by
-//         float atomics; without dropout, else v3); v1 = the generic kernels
+//   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
+//         kernel taking two query slices per barrier; v1 = the generic kernels
 //         (software-pipelining the dQ tile's / the dK/dV slice pair's MFMAs under each
 //         other's VALU with sched_group_barrier measured no gain / a spilling kernel:
 //         docs/performance.md, round 5)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
 enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6 };
-enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3, BWD_V4 = 4 };
+enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
 };
@@ -164,7 +163,7 @@ FlashConfig& flash_config() {
     if (const char* e = getenv("NSA_FLASH_FWD"))
       d.fwd = (e[0] == 'v' && (e[1] == '1' || (e[1] >= '3' && e[1] <= '6'))) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
-      d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '4') ? e[1] - '0' : BWD_V3;
+      d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
     return d;
   }();
@@ -1678,8 +1677,7 @@ template <int NKB, bool MASK, bool DROP>
 __device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, const float* ld,
                                            const bf16x8 (&kf)[NKB][4], const bf16x8 (&vf)[NKB][4],
                                            f32x16 (&dk)[NKB][2], f32x16 (&dv)[NKB][2], int q0, int kw, int h,
-                                           int r, int lane, float scale_log2, const DropArgs& dr,
-                                           bf16x8 (*ds_out)[2] = nullptr) {
+                                           int r, int lane, float scale_log2, const DropArgs& dr) {
   constexpr int D = 64;
   bf16x8 qa[4], da[4];
 #pragma unroll
@@ -1724,10 +1722,6 @@ __device__ __forceinline__ void dkdv_slice(const char* qt, const char* dot, cons
     }
     pack16(pv, pfr[kb]);
     pack16(dsv, dsfr[kb]);
-  }
-  if (ds_out) {  // the fused backward's dQ takes dS through LDS
-    ds_out[0][0] = dsfr[0][0];
-    ds_out[0][1] = dsfr[0][1];
   }
   // dV^T += dO^T · P,  dK^T += Q^T · dS   (each transposed fragment feeds every key block)
 #pragma unroll
@@ -1921,278 +1915,6 @@ __global__ __launch_bounds__(NW * 64, NKB == 2 ? 1 : (NW == 8 ? 1 : 2)) void fla
       }
     }
   }
-}
-
-// =============================================================================
-// Fused backward (backward v4; D = 64, no dropout): one workgroup = 8 waves = 256 keys of
-// one (b, h); the dK/dV body above (key on the lane, Q / dO slices by LDS-DMA, two slices
-// per barrier) plus dQ in the same pass, so S and dP are computed once (five MFMA
-// products per tile instead of the split kernels' seven) and no second kernel re-reads
-// K / V:  each wave writes its slice's dS^T (32 keys x 32 queries, bf16, 4 ds_write_b64
-// per lane straight from the packed dK operand) into a [256 keys][32 q] LDS image; one
-// barrier later (the next slice pair's, already there) wave w computes the 16 x 16 block
-// (queries 16 (w & 1) .., d 16 (w >> 1) ..) of dQ = dS · K over the 256 keys
-// (v_mfma_f32_16x16x32_bf16, both operands by transposed reads of the dS^T image and of a
-// static [256][64] K image) and adds it to an fp32 dQ accumulator with global float
-// atomics (one workgroup per 256 keys: N / 256 adders per dQ element).  A pre-pass forms
-// the row constants and zeroes the accumulator; a post-pass scales it into dqkv (bf16).
-// (cdna_hip_programming.md Appendix B, attention backward: atomics form.)
-// =============================================================================
-constexpr int FB_NW = 8, FB_KEYS = 32 * FB_NW;
-constexpr int FB_KIMG = FB_KEYS * 64 * 2;  // [256 keys][64 d] bf16
-constexpr int FB_DSIMG = FB_KEYS * 32 * 2;  // [256 keys][32 queries] bf16, one slice
-
-// 16x16x32 operand by two transposed reads: lane (g = lane >> 4, i = lane & 15) gets column
-// col_base + i, rows r0 + 8 g .. + 7 (k = 8 g .. 8 g + 7 of a 32-deep k-step)
-template <int W>
-__device__ __forceinline__ bf16x8 tr_frag16(const char* tile, int r0, int col_base, int lane) {
-  const int g = lane >> 4, ig = lane & 15;
-  const int q = ig >> 2, p = ig & 3;
-  const int col = col_base + 4 * p;
-  const int chunk = col >> 3, half = (col >> 2) & 1;
-  const s16x4 a = lds_tr(tile, swz<W>(r0 + 8 * g + q, chunk) + half * 8);
-  const s16x4 b = lds_tr(tile, swz<W>(r0 + 8 * g + 4 + q, chunk) + half * 8);
-  return cat_tr(a, b);
-}
-
-// this lane's dS (key r, queries acc_row(i, h), packed as the dK operand) -> dS^T image
-__device__ __forceinline__ void fb_store_ds(char* img, int key, int h, const bf16x8 (&dsf)[2]) {
-#pragma unroll
-  for (int sidx = 0; sidx < 2; ++sidx) {
-    const uint4 u = __builtin_bit_cast(uint4, dsf[sidx]);
-    const int qa = 16 * sidx + 4 * h, qb = qa + 8;
-    *reinterpret_cast<uint2*>(img + swz<32>(key, qa >> 3) + ((qa >> 2) & 1) * 8) = make_uint2(u.x, u.y);
-    *reinterpret_cast<uint2*>(img + swz<32>(key, qb >> 3) + ((qb >> 2) & 1) * 8) = make_uint2(u.z, u.w);
-  }
-}
-
-__global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_fused_kernel(
-    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ nls,
-    const float* __restrict__ nd, float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B, int T, int H,
-    float scale, float scale_log2, int order) {
-  constexpr int D = 64, NW = FB_NW, G = 2, NS = 2 * G;
-  constexpr int SLOT = V2Geo<NW>::SLOT;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + FB_KIMG + 2 * G * FB_DSIMG];
-  char* const kimg = smem + NS * SLOT;
-  char* const dsimg = kimg + FB_KIMG;  // [pair parity][slice in pair] images
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  int bh, kbw;  // key blocks near 0 see the most queries: launched first
-  attn_order((T + FB_KEYS - 1) / FB_KEYS, BH, order, bh, kbw);
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, r = lane & 31;
-  const int k0 = kbw * FB_KEYS;
-  const int kw = k0 + 32 * w;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-  const bf16_t* vbase = base + 2 * C + hh * D;
-  const bf16_t* dobase = dout + (int64_t)b * T * C + hh * D;
-  const float* nls_bh = nls + (int64_t)bh * T;
-  const float* nd_bh = nd + (int64_t)bh * T;
-  const DropArgs dr{0u, 1.0f, 0ull, bh, T};
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int s_first = k0 / 32;
-  const int n_mine = T / 32 - s_first;
-
-  // slice s -> ring slot (as the dK/dV kernel with 8 waves: waves 0-3 copy Q, 4-7 dO)
-  const int piece = w & 3;
-  const int prow = 8 * piece + (lane >> 3);
-  const int pch = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const bf16_t* qsrc = qbase + (int64_t)prow * row_stride + pch * 8;
-  const bf16_t* dosrc = dobase + (int64_t)prow * C + pch * 8;
-  const float* csrc = (h == 0 ? nls_bh : nd_bh) + r;
-  auto issue = [&](int sl, int slot) {
-    const uint32_t sb = lds0 + (uint32_t)(slot * SLOT);
-    if (w < 4) glds16(qsrc + (int64_t)sl * 32 * row_stride, sb + (uint32_t)(8 * piece * 128));
-    else glds16(dosrc + (int64_t)sl * 32 * C, sb + (uint32_t)(V2_QT + 8 * piece * 128));
-    glds4(csrc + sl * 32, sb + (uint32_t)(2 * V2_QT + w * 256));
-  };
-  for (int j = 0; j < G && j < n_mine; ++j) issue(s_first + j, j);
-
-  // the workgroup's K rows [256][64] into the static image (plain loads; keys past T clamp)
-  for (int c = tid; c < FB_KEYS * 8; c += NW * 64) {
-    const int row = c >> 3, ch = c & 7;
-    const int kr = min(k0 + row, T - 1);
-    *reinterpret_cast<uint4*>(kimg + swz<D>(row, ch)) =
-        *reinterpret_cast<const uint4*>(kbase + (int64_t)kr * row_stride + 8 * ch);
-  }
-  bf16x8 kf[1][4], vf[1][4];
-  {
-    const int kc = kw + r < T ? kw + r : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[0][ks] = as_frag(*reinterpret_cast<const uint4*>(kbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
-      vf[0][ks] = as_frag(*reinterpret_cast<const uint4*>(vbase + (int64_t)kc * row_stride + 16 * ks + 8 * h));
-    }
-  }
-  asm volatile("" ::"v"(kf[0][0]), "v"(kf[0][1]), "v"(kf[0][2]), "v"(kf[0][3]), "v"(vf[0][0]), "v"(vf[0][1]),
-               "v"(vf[0][2]), "v"(vf[0][3]));
-  f32x16 dk[1][2], dv[1][2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    dk[0][dt] = f32x16{};
-    dv[0][dt] = f32x16{};
-  }
-
-  // dQ of the slice pair held in image parity `par` (its dS^T images complete: a barrier
-  // has passed since they were written): 16 x 16 block per wave, atomics into dq_acc
-  const int qb = w & 1, db = w >> 1;
-  auto dq_pair = [&](int jp, int par) {
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int jj = jp + u;
-      if (jj >= n_mine) break;
-      const char* img = dsimg + (par * G + u) * FB_DSIMG;
-      const int t_max = min(NW, jj + 1);  // key 32-blocks with any unmasked key for this slice
-      f32x4 acc = f32x4{};
-      if (t_max == NW) {  // every slice from the eighth on: four k-steps' reads in flight at a time
-#pragma unroll
-        for (int t0 = 0; t0 < NW; t0 += 4) {
-          bf16x8 fa[4], fb[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            fa[t] = tr_frag16<32>(img, 32 * (t0 + t), 16 * qb, lane);
-            fb[t] = tr_frag16<D>(kimg, 32 * (t0 + t), 16 * db, lane);
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t) acc = mfma16e<kFaH>(fa[t], fb[t], acc);
-        }
-      } else {
-        for (int t = 0; t < t_max; ++t)
-          acc = mfma16e<kFaH>(tr_frag16<32>(img, 32 * t, 16 * qb, lane), tr_frag16<D>(kimg, 32 * t, 16 * db, lane),
-                              acc);
-      }
-      const int q = (s_first + jj) * 32 + 16 * qb + 4 * (lane >> 4);
-      float* dst = dq_acc + ((int64_t)b * T + q) * C + hh * D + 16 * db + (lane & 15);
-#ifndef NSA_PROBE_FB_NOATOMIC
-#define NSA_PROBE_FB_NOATOMIC 0  // probe builds only: plain stores instead of the atomics (wrong dQ)
-#endif
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if constexpr (NSA_PROBE_FB_NOATOMIC) dst[(int64_t)e * C] = acc[e];
-        else atomicAdd(dst + (int64_t)e * C, acc[e]);
-      }
-    }
-  };
-
-  const int j_diag = min(w, n_mine);
-  const int j_full = min(w + 1, n_mine);
-  for (int j = 0; j < n_mine; j += G) {
-    // this pair's slices landed: they are older than the previous iteration's dQ atomics
-    // (8 per wave once a pair's dQ has run), which stay in flight (~3000 cycles each with
-    // every CU issuing: MI355X_MICROARCH.md 'float atomic add')
-    if (j >= 2 * G) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int u = 0; u < G; ++u)
-      if (j + G + u < n_mine) issue(s_first + j + G + u, (j + G + u) % NS);
-    if (j >= G) dq_pair(j - G, ((j - G) / G) & 1);
-    const int par = (j / G) & 1;
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int jj = j + u;
-      if (jj >= n_mine || jj < j_diag) continue;
-      bf16x8 dsf[1][2];
-      auto f = [&](auto slot) {
-        const char* qt = smem + decltype(slot)::value * SLOT;
-        const float* ld = reinterpret_cast<const float*>(qt + 2 * V2_QT) + w * 64;
-        if (jj >= j_full)
-          dkdv_slice<1, false, false>(qt, qt + V2_QT, ld, kf, vf, dk, dv, (s_first + jj) * 32, kw, h, r, lane,
-                                      scale_log2, dr, dsf);
-        else
-          dkdv_slice<1, true, false>(qt, qt + V2_QT, ld, kf, vf, dk, dv, (s_first + jj) * 32, kw, h, r, lane,
-                                     scale_log2, dr, dsf);
-      };
-      slot_dispatch<0, NS>(jj % NS, f);
-      fb_store_ds(dsimg + (par * G + u) * FB_DSIMG, 32 * w + r, h, dsf[0]);
-    }
-  }
-  // the last pair's dQ
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  {
-    const int jl = ((n_mine - 1) / G) * G;
-    dq_pair(jl, (jl / G) & 1);
-  }
-
-  // epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T
-  const int kpos = kw + r;
-  if (kpos < T) {
-    bf16_t* krow = dqkv + ((int64_t)b * T + kpos) * row_stride + C + hh * D;
-    bf16_t* vrow = krow + C;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        uint2 uk, uv;
-        uk.x = cvt2(dk[0][dt][4 * g + 0] * scale, dk[0][dt][4 * g + 1] * scale);
-        uk.y = cvt2(dk[0][dt][4 * g + 2] * scale, dk[0][dt][4 * g + 3] * scale);
-        uv.x = cvt2(dv[0][dt][4 * g + 0], dv[0][dt][4 * g + 1]);
-        uv.y = cvt2(dv[0][dt][4 * g + 2], dv[0][dt][4 * g + 3]);
-        *reinterpret_cast<uint2*>(krow + d) = uk;
-        *reinterpret_cast<uint2*>(vrow + d) = uv;
-      }
-    }
-  }
-}
-
-// fused backward pre-pass: -delta = -rowsum(dO * O) and -lse / scale per (b, h, t), and the fp32
-// dQ accumulator zeroed; one thread per 8 columns of a row (coalesced), the 8 threads of a
-// head summing by shuffles
-__global__ __launch_bounds__(256) void flash_bwd_fused_pre_kernel(const bf16_t* __restrict__ o,
-                                                                  const bf16_t* __restrict__ dout,
-                                                                  const float* __restrict__ lse,
-                                                                  float* __restrict__ nls, float* __restrict__ nd,
-                                                                  float* __restrict__ dq_acc, int B, int T, int H,
-                                                                  float scale) {
-  constexpr int D = 64;
-  const int C = H * D, cpr = C / 8;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool live = i < (int64_t)B * T * cpr;
-  const int64_t bt = live ? i / cpr : 0;
-  const int c8 = live ? (int)(i % cpr) : 0;
-  float fo[8], fg[8];
-  load8e<kFaH>(o + bt * C + 8 * c8, fo);
-  load8e<kFaH>(dout + bt * C + 8 * c8, fg);
-  float dsum = 0.0f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) dsum += fo[e] * fg[e];
-  dsum += __shfl_xor(dsum, 1, 64);
-  dsum += __shfl_xor(dsum, 2, 64);
-  dsum += __shfl_xor(dsum, 4, 64);
-  if (!live) return;
-  float4* z = reinterpret_cast<float4*>(dq_acc + bt * C + 8 * c8);
-  z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-  z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if ((c8 & 7) == 0) {
-    const int hh = c8 >> 3, t = (int)(bt % T), b = (int)(bt / T);
-    const int64_t ri = ((int64_t)b * H + hh) * T + t;
-    nd[ri] = -dsum;
-    nls[ri] = -lse[ri] / scale;
-  }
-}
-
-// fused backward post-pass: dQ = scale * acc -> dqkv[:, :, 0:C] (bf16), 8 elements per thread
-__global__ __launch_bounds__(256) void flash_bwd_fused_post_kernel(const float* __restrict__ dq_acc,
-                                                                   bf16_t* __restrict__ dqkv, int64_t rows, int C,
-                                                                   float scale) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int cpr = C / 8;
-  if (i >= rows * cpr) return;
-  const int64_t row = i / cpr;
-  const int c = (int)(i % cpr) * 8;
-  const float4* src = reinterpret_cast<const float4*>(dq_acc + row * C + c);
-  const float4 a = src[0], bb = src[1];
-  float f[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale,
-                bb.x * scale, bb.y * scale, bb.z * scale, bb.w * scale};
-  store8e<kFaH>(dqkv + row * 3 * (int64_t)C + c, f);
 }
 
 // =============================================================================
@@ -2548,35 +2270,6 @@ hipError_t bwd2_launch64(const void* qkv, const void* o, const void* dout, const
   return hipGetLastError();
 }
 
-// fused backward (v4): ws = -delta [B, H, T], -lse/scale [B, H, T], then the fp32 dQ
-// accumulator [B, T, C] (nsa_flash_bwd2_ws_floats)
-hipError_t bwd_fused_launch64(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
-                              void* dqkv, int B, int T, int H, float scale, hipStream_t s) {
-  const int64_t bht = (int64_t)B * H * T;
-  float* nd = (float*)ws;
-  float* nls = nd + bht;
-  float* acc = nls + bht;
-  const int C = H * 64;
-  flash_bwd_fused_pre_kernel<<<(unsigned)(((int64_t)B * T * (C / 8) + 255) / 256), 256, 0, s>>>(
-      (const bf16_t*)o, (const bf16_t*)dout, (const float*)lse, nls, nd, acc, B, T, H, scale);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int n_kb = (T + FB_KEYS - 1) / FB_KEYS;
-  flash_bwd_fused_kernel<<<n_kb * B * H, FB_NW * 64, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, nls, nd, acc,
-                                                              (bf16_t*)dqkv, B, T, H, scale, scale * kLog2e,
-                                                              attn_order_env());
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int64_t items = (int64_t)B * T * (C / 8);
-  flash_bwd_fused_post_kernel<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(acc, (bf16_t*)dqkv, (int64_t)B * T,
-                                                                             C, scale);
-  return hipGetLastError();
-}
-
-bool bwd_fused_applies(int T, int D, float p) {
-  return D == 64 && T % 32 == 0 && p == 0.0f && flash_config().bwd == BWD_V4;
-}
-
 }  // namespace
 
 // Backward with a 2 x [B, H, T] fp32 workspace.  D = 64 with T % 32 == 0 runs the v2
@@ -2585,7 +2278,6 @@ bool bwd_fused_applies(int T, int D, float p) {
 NSA_API hipError_t NSA_FA_SYM(nsa_flash_bwd2)(const void* qkv, const void* o, const void* dout, const void* lse, void* ws,
                                   void* dqkv, int B, int T, int H, int D, float scale, float p, uint64_t seed,
                                   hipStream_t s) {
-  if (bwd_fused_applies(T, D, p)) return bwd_fused_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, s);
   if (D == 64 && T % 32 == 0 && flash_config().bwd >= BWD_V2)
     return bwd2_launch64(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
   switch (D) {
@@ -2594,12 +2286,6 @@ NSA_API hipError_t NSA_FA_SYM(nsa_flash_bwd2)(const void* qkv, const void* o, co
     case 128: return bwd_launch<128>(qkv, o, dout, lse, ws, dqkv, B, T, H, scale, p, seed, s);
     default: return hipErrorInvalidValue;
   }
-}
-
-// fp32 workspace floats nsa_flash_bwd2 needs under the current variant selection
-NSA_API int64_t NSA_FA_SYM(nsa_flash_bwd2_ws_floats)(int B, int T, int H, int D, float p) {
-  const int64_t bht = (int64_t)B * H * T;
-  return bwd_fused_applies(T, D, p) ? 2 * bht + bht * D : 2 * bht;
 }
 
 #define NSA_FA_RNG(NAME) NSA_DEFINE_RNG_ADVANCE(NAME)
@@ -2625,13 +2311,13 @@ NSA_API hipError_t NSA_FA_SYM(nsa_flash_fwd)(const void* qkv, void* out, void* l
 #if !NSA_FA_F16
 NSA_API void* nsa_flash_config_ptr() { return &flash_config(); }
 
-// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5 / 6 v6, bwd 1 v1 / 2 v2 / 3 v3 / 4 v4, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5 / 6 v6, bwd 1 v1 / 2 v2 / 3 v3, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
 // fwd | bwd << 4 | order << 8.
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
   if (fwd == FWD_AUTO || fwd == FWD_V1 || (fwd >= FWD_V3 && fwd <= FWD_V6)) c.fwd = fwd;
-  if (bwd >= BWD_V1 && bwd <= BWD_V4) c.bwd = bwd;
+  if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order >= 0 && order <= 2) c.order = order;
   return prev;
 }

@@ -83,7 +83,6 @@ _SIGNATURES = {
     "nsa_gemv_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_gemv_ln": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                     c_float, c_int, c_int, c_void_p, c_void_p],
-    "nsa_flash_bwd2_ws_floats": [c_int, c_int, c_int, c_int, c_float],
     "nsa_flash_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_rng_advance": [c_void_p],
@@ -124,10 +123,6 @@ class KernelLibraryMissing(RuntimeError):
     pass
 
 
-# entry points whose return value is not a hipError_t / int
-_RESTYPES = {"nsa_flash_bwd2_ws_floats": c_int64}
-
-
 def lib():
     """Return the loaded kernel library (raises loudly if it was not built)."""
     global _lib
@@ -148,7 +143,7 @@ def lib():
                 if fn is None:
                     continue  # optional entry points (checked at call time)
                 fn.argtypes = argtypes
-                fn.restype = _RESTYPES.get(name, c_int)
+                fn.restype = c_int
         _lib = L
         return _lib
 

@@ -702,7 +702,7 @@ def _attn_reference(q, k, v, p, seed):
 
 
 _FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6}
-_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3, "v4": 4}
+_FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3}
 
 
 @contextlib.contextmanager
@@ -753,18 +753,13 @@ class AttentionFn(torch.autograd.Function):
             qkv, y, lse = ctx.saved_tensors
             dy = dy.contiguous()
             dqkv = torch.empty_like(qkv)
-            # fp32 workspace: the per-query row constants (delta, lse), 2 x [B, H, T], and for
-            # the fused backward (v4) its fp32 dQ accumulator [B, T, C]
+            # 2 x [B, H, T] fp32 workspace for the per-query row constants (delta, lse);
+            # dQ is written once, in bf16, by its own kernel (no atomics: a fused dK/dV/dQ
+            # kernel with dQ by float atomics measured slower, profiles/r5_attn_fused_experiment.md)
+            ws = torch.empty(2, B, H, T, device=dy.device, dtype=F32)
             dy = dy.to(qkv.dtype)
-            # deterministic mode: the fused backward's dQ float atomics are order-dependent,
-            # so a v4 selection runs v3 (split kernels, dQ written once) for this call
-            det_v4 = _gd.DETERMINISTIC and ((_lib.call_ret("nsa_flash_set_variant", -1, -1, -1) >> 4) & 0xF) == 4
-            with (flash_variant(bwd="v3") if det_v4 else contextlib.nullcontext()):
-                n_ws = _lib.call_ret(_sym("nsa_flash_bwd2_ws_floats", qkv.dtype), B, T, H, D, float(p))
-                ws = torch.empty(n_ws, device=dy.device, dtype=F32)
-                _lib.call(_sym("nsa_flash_bwd2", qkv.dtype), _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy),
-                          _lib.ptr(lse), _lib.ptr(ws), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed,
-                          _lib.stream())
+            _lib.call(_sym("nsa_flash_bwd2", qkv.dtype), _lib.ptr(qkv), _lib.ptr(y), _lib.ptr(dy), _lib.ptr(lse),
+                      _lib.ptr(ws), _lib.ptr(dqkv), B, T, H, D, 1.0 / math.sqrt(D), p, seed, _lib.stream())
             return dqkv, None, None
         (qkv,) = ctx.saved_tensors
         with torch.enable_grad():

@@ -610,7 +610,7 @@ def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
     assert ((lse - lref[None, None]).abs() <= 1e-5 * lref[None, None] + 1e-6).all()
 
 
-@pytest.mark.parametrize("bwd", ["v2", "v3", "v4"])
+@pytest.mark.parametrize("bwd", ["v2", "v3"])
 @pytest.mark.parametrize("T", [1024, 320, 96])
 def test_flash_bwd_exact_structure(kernels, flash_variant, T, bwd):
     """Backward counterpart: Q = 0 (uniform P = 1/(q+1)), K one-hot by key tile, dO one-hot
@@ -734,36 +734,6 @@ def test_flash_bwd_pair_matches_v2(kernels, flash_variant, T, ver):
     for i, name in enumerate("qkv"):
         e = rel_err(grads[ver][:, :, i], grads["v2"][:, :, i])
         assert e < 1e-6, f"d{name}: {ver} vs v2 rel err {e}"
-
-
-@pytest.mark.parametrize("T", [1024, 320, 96, 64, 2048])
-def test_flash_bwd_fused_matches_split(kernels, flash_variant, T):
-    """Backward v4 (one fused kernel: dK / dV plus dQ through an LDS dS^T image and float
-    atomics, with its pre / post passes) against v3 (split dK/dV and dQ kernels) on
-    every element: dV from identical arithmetic, dK to rounding, dQ summed in a
-    different order (fp32, 256-key blocks); T = 320 / 96 / 64 leave the last key block
-    partial, 2048 gives eight key blocks per (b, h)."""
-    from nanosandbox_amd.ops import functional as fn
-
-    torch.manual_seed(0)
-    B, H, D = 2, 3, 64
-    qkv = torch.randn(B, T, 3 * H * D, device=DEV).to(BF)
-    dy = torch.randn(B, T, H * D, device=DEV).to(BF)
-    grads = {}
-    for v in ("v3", "v4"):
-        flash_variant(bwd=v)
-        x = qkv.clone().requires_grad_(True)
-        fn.attention(x, H, 0.0, True).backward(dy)
-        torch.cuda.synchronize()
-        grads[v] = x.grad.float().view(B, T, 3, H * D)
-    g3, g4 = grads["v3"], grads["v4"]
-    assert torch.isfinite(g4).all()
-    assert torch.equal(g4[:, :, 2], g3[:, :, 2])  # dV: the same per-slice arithmetic
-    # dK: the same MFMAs; the compiler contracts the dS arithmetic differently in the two bodies
-    assert ((g4[:, :, 1] - g3[:, :, 1]).abs() <= 2 ** -7 * g3[:, :, 1].abs() + 1e-6).all()
-    err = (g4[:, :, 0] - g3[:, :, 0]).abs()
-    assert (err <= 2 ** -7 * g3[:, :, 0].abs() + 2 ** -7 * g3[:, :, 0].abs().mean()).all(), err.max().item()
-    assert rel_err(g4[:, :, 0], g3[:, :, 0]) < 4e-3
 
 
 @pytest.mark.parametrize("T", [320, 1024, 96])
