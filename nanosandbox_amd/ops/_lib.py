@@ -88,8 +88,8 @@ _SIGNATURES = {
     "nsa_rng_advance": [c_void_p],
     "nsa_rng_set": [c_uint64, c_void_p],
     "nsa_splitk_reduce": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
-    "nsa_embedding_bwd_det": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                              c_float, c_uint64, c_void_p],
+    "nsa_embedding_bwd_det": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                              c_int, c_int, c_int, c_float, c_uint64, c_void_p],
     "nsa_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "nsa_gemm": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                  c_int, c_int, c_int, c_int, c_void_p],

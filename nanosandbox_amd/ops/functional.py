@@ -290,8 +290,11 @@ class EmbeddingFn(torch.autograd.Function):
                 flat = idx.view(-1)
                 ids, order = torch.sort(flat, stable=True)
                 seg = torch.searchsorted(ids, torch.arange(V + 1, device=dx.device, dtype=ids.dtype))
-                _lib.call("nsa_embedding_bwd_det", _lib.ptr(order), _lib.ptr(seg), _lib.ptr(dx), _lib.ptr(gwte),
-                          _lib.ptr(gwpe), B, T, C, V, 1 if dx.dtype == F32 else 0, ctx.p, ctx.seed, _lib.stream())
+                # partial sums of the segments that cross a 16-position chunk (two slots a chunk)
+                part = torch.empty(2 * ((B * T + 15) // 16), C, device=dx.device, dtype=F32)
+                _lib.call("nsa_embedding_bwd_det", _lib.ptr(ids), _lib.ptr(order), _lib.ptr(seg), _lib.ptr(part),
+                          _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe), B, T, C, V, 1 if dx.dtype == F32 else 0, ctx.p,
+                          ctx.seed, _lib.stream())
             else:
                 _lib.call("nsa_embedding_bwd_x32" if dx.dtype == F32 else "nsa_embedding_bwd", _lib.ptr(idx),
                           _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe), B, T, C, ctx.p, ctx.seed, _lib.stream())
@@ -312,7 +315,11 @@ class EmbeddingFn(torch.autograd.Function):
         return None, _accumulate(wte, gwte), _accumulate(wpe, gwpe), None, None, None
 
 
-_EMB_SORTED_MIN_TOKENS = 4096  # below this the fp32-atomic embedding backward (no sort launches)
+# below this the fp32-atomic embedding backward (no sort launches) unless deterministic:
+# the sort + searchsorted cost ~60 us flat, the atomics ~3 us per 1K tokens against ~2 for
+# the sorted kernels (scripts/emb_bwd_ab.py: 16K tokens 55.5 vs 96.2 us, GPT-2 122880
+# tokens 369.5 vs 313.6 us, profiles/r5_emb_bwd.md) -> crossover near 64K tokens
+_EMB_SORTED_MIN_TOKENS = 65536
 
 
 def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32, cdtype=None):

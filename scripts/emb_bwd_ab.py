@@ -36,8 +36,9 @@ def main():
     def sorted_():
         ids, order = torch.sort(idx.view(-1), stable=True)
         seg = torch.searchsorted(ids, torch.arange(V + 1, device="cuda", dtype=ids.dtype))
-        _lib.call("nsa_embedding_bwd_det", _lib.ptr(order), _lib.ptr(seg), _lib.ptr(dx), _lib.ptr(gw["sorted"]),
-                  _lib.ptr(gp["sorted"]), B, T, C, V, 1, 0.0, 0, _lib.stream())
+        part = torch.empty(2 * ((B * T + 15) // 16), C, device="cuda")
+        _lib.call("nsa_embedding_bwd_det", _lib.ptr(ids), _lib.ptr(order), _lib.ptr(seg), _lib.ptr(part),
+                  _lib.ptr(dx), _lib.ptr(gw["sorted"]), _lib.ptr(gp["sorted"]), B, T, C, V, 1, 0.0, 0, _lib.stream())
 
     atomic()
     sorted_()

@@ -140,10 +140,15 @@ def test_gelu(kernels, n):
 
 
 # --------------------------------------------------------------- embedding
-@pytest.mark.parametrize("B,T,V,C", [(4, 128, 1000, 768), (3, 77, 65, 384),
-                                     (8, 1024, 50304, 768), (4, 1024, 65, 384)])  # >= 4096 tokens: sorted backward
-def test_embedding(kernels, B, T, V, C):
+@pytest.mark.parametrize("B,T,V,C,sorted_bwd", [(4, 128, 1000, 768, False), (3, 77, 65, 384, False),
+                                                (8, 1024, 50304, 768, True), (4, 1024, 65, 384, True),
+                                                (4, 1024, 65, 384, False)])
+def test_embedding(kernels, monkeypatch, B, T, V, C, sorted_bwd):
     from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+
+    # the sorted (atomic-free) backward runs from _EMB_SORTED_MIN_TOKENS tokens up
+    monkeypatch.setattr(Fn, "_EMB_SORTED_MIN_TOKENS", 0 if sorted_bwd else 1 << 40)
 
     torch.manual_seed(0)
     idx = torch.randint(0, V, (B, T), device=DEV)
@@ -184,6 +189,46 @@ def test_embedding_noncontiguous_idx(kernels, fused):
     gwte = torch.zeros(V, C, device=DEV).index_add_(0, ic.reshape(-1), dx.float().reshape(-1, C))
     got = wte.main_grad if fused else wte.grad.float()
     assert rel_err(got, gwte) < (1e-5 if fused else 1e-2)
+
+
+@pytest.mark.parametrize("case", ["char_skew", "one_id", "ragged", "wide"])
+def test_embedding_bwd_sorted_chunks(kernels, monkeypatch, case):
+    """The sorted embedding backward cuts the sorted token list into 16-position chunks
+    for ids with more than 64 tokens and adds their partial sums in a second pass: a skewed
+    character-corpus distribution with dropout (the shakespeare_char shape), one id for
+    every token (one segment over all chunks), a token count that is not a multiple of
+    16, and C > 512 (two column passes per lane).  Against index_add in fp32, and bitwise
+    repeatable."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+
+    monkeypatch.setattr(Fn, "_EMB_SORTED_MIN_TOKENS", 0)
+    B, T, V, C, p = {"char_skew": (64, 256, 56, 384, 0.2), "one_id": (4, 1024, 65, 128, 0.0),
+                     "ragged": (5, 999, 300, 64, 0.0), "wide": (8, 512, 1000, 1600, 0.0)}[case]
+    torch.manual_seed(2)
+    if case == "one_id":
+        idx = torch.full((B, T), 7, device=DEV, dtype=torch.long)
+    else:
+        w = 1.0 / torch.arange(1, V + 1, dtype=torch.float32) ** 1.2  # Zipf-like frequencies
+        idx = torch.multinomial(w, B * T, replacement=True).view(B, T).to(DEV)
+    dx = torch.randn(B, T, C, device=DEV)
+    grads = []
+    for _ in range(2):
+        # positive weights: a kept x is never 0, so x != 0 recovers the dropout mask (with
+        # signed weights wte + wpe cancels exactly in bf16 for ~0.1% of the elements)
+        wte = param(torch.rand(V, C, device=DEV) * 0.02 + 0.01, fused=True)
+        wpe = param(torch.rand(T, C, device=DEV) * 0.02 + 0.01, fused=True)
+        torch.manual_seed(3)  # the same dropout seed both times
+        x = ops.embedding(idx, wte, wpe, p, True, dtype=torch.float32)
+        x.backward(dx)
+        grads.append((wte.main_grad.clone(), wpe.main_grad.clone()))
+    keep = (x != 0).float() / (1.0 - p) if p > 0 else torch.ones_like(dx)
+    g = (dx * keep).reshape(-1, C)
+    ref_wte = torch.zeros(V, C, device=DEV).index_add_(0, idx.reshape(-1), g)
+    ref_wpe = (dx * keep).sum(0)
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    assert rel_err(grads[0][0], ref_wte) < 1e-5
+    assert rel_err(grads[0][1], ref_wpe) < 1e-5
 
 
 # ------------------------------------------------------------ cross-entropy
