@@ -135,7 +135,7 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
 //   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4 | v5 | v6: D = 64 forward kernel;
-//         auto = v5 for bf16 / v4 for fp16 without dropout once the grid has >= 4096 v3
+//         auto = v5 without dropout once the grid has >= 4096 v3
 //         workgroups, else v1 (fwd_launch); v3 = 64 queries per wave, one K/V tile per
 //         barrier; v4 = two tiles per barrier; v5 = v4's geometry with fast tiles (no running
 //         max while scores stay in range); v6 = v1's geometry with fast tiles
@@ -781,8 +781,10 @@ __device__ __forceinline__ bool fwd_tile5(const char* kt, const char* vt, const 
     rs[blk] = half_swap_sum(acc[0] + acc[1]);
   }
   const float lA = l_i[0] + rs[0], lB = l_i[1] + rs[1];
-  // NaN-safe: a non-finite sum fails every comparison
-  const bool ok = rs[0] <= 0x1p64f && rs[1] <= 0x1p64f && lA >= 0x1p-60f && lB >= 0x1p-60f;
+  // NaN-safe: a non-finite sum fails every comparison.  bf16 P holds any fp32 value; fp16 P
+  // only up to 65504 and keeps 2^-11 relative precision down to 2^-14, hence its tighter range
+  const float hi = kFaH ? 0x1p15f : 0x1p64f, lo = kFaH ? 0x1p-8f : 0x1p-60f;
+  const bool ok = rs[0] <= hi && rs[1] <= hi && lA >= lo && lB >= lo;
   if (__builtin_amdgcn_ballot_w64(!ok)) return false;  // wave-uniform: redo this tile exactly
   l_i[0] = lA;
   l_i[1] = lB;
@@ -2151,10 +2153,10 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
     const int sel = flash_config().fwd;
     const bool v3 = sel == FWD_V3 || sel == FWD_V4 || sel == FWD_V5 ||
                     (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
-    // v5 (auto's pick for bf16: no running max while the scores stay in range): B120 T1024 H12
+    // v5 (auto's pick: no running max while the scores stay in range): B120 T1024 H12
     // 333.3 vs 338.1 us for v4, faster in 5 of 6 same-process A/Bs (profiles/r5_ab_*.log).
-    // fp16 P cannot hold v5's m = 0 range: v4 there.
-    if (v3 && (sel == FWD_V5 || sel == FWD_AUTO) && !th && !kFaH) {
+    // fp16 runs it with the fast tiles' row sums bounded to [2^-8, 2^15] (P <= 65504).
+    if (v3 && (sel == FWD_V5 || sel == FWD_AUTO) && !th) {
       flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                       scale * kLog2e, order);
       return hipGetLastError();

@@ -140,6 +140,45 @@ __device__ __forceinline__ void unsplit8(uint4 hi, uint4 lo, float (&f)[8]) {
   }
 }
 
+// The fp16-compute form (dtype float16): hi = fp16(g) rounded to nearest even (torch's cast:
+// the branch GEMMs' fp16 operand), lo = (g - hi) * 2^(39 - E) as int16, E = hi's exponent
+// field (at least 1).  g - hi is exact (Sterbenz) and, for a normal hi, an integer multiple of
+// 2^(E - 39) no larger than 2^13 of them, so hi + lo * 2^(E - 39) gives g back bit for bit for
+// every |g| >= 2^-14.  Below that, g is kept to 2^-39 absolute (a loss-scaled gradient that
+// small is < 2^-30 before unscaling).  |g| >= 65520 stores an fp16 inf and decodes to inf,
+// as does an infinity; a NaN stays NaN (the dynamic loss scale skips such a step either way,
+// as it does when autocast's fp16 branch gradient overflows).
+__device__ __forceinline__ void split8h(const float (&f)[8], uint4& hi, uint4& lo) {
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // g as an fp32 value first: without the barrier the compiler fuses the producing FMA and
+    // this cast into v_fma_mix (one rounding of the exact result, which differs from torch's
+    // cast of the fp32 gradient at fp32 values that are exact fp16 ties)
+    float g = f[j];
+    asm volatile("" : "+v"(g));
+    const _Float16 hv = (_Float16)g;
+    h[j] = __builtin_bit_cast(uint16_t, hv);
+    const int e = (int)((h[j] >> 10) & 31u);
+    const float r = g - (float)hv;
+    const int q = e == 31 ? 0 : (int)__builtin_rintf(__builtin_amdgcn_ldexpf(r, 39 - (e > 1 ? e : 1)));
+    l[j] = (uint32_t)q & 0xffffu;
+  }
+  hi = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+  lo = make_uint4(l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16));
+}
+__device__ __forceinline__ void unsplit8h(uint4 hi, uint4 lo, float (&f)[8]) {
+  const uint32_t hw[4] = {hi.x, hi.y, hi.z, hi.w}, lw[4] = {lo.x, lo.y, lo.z, lo.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t hb = (hw[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    const int q = (int)(int16_t)((lw[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+    const int e = (int)((hb >> 10) & 31u);
+    f[i] = (float)__builtin_bit_cast(_Float16, (uint16_t)hb) +
+           __builtin_amdgcn_ldexpf((float)q, (e > 1 ? e : 1) - 39);
+  }
+}
+
 // value as stored in the residual stream (bf16 rounding for a bf16 stream)
 __device__ __forceinline__ float as_stream(float v, bf16_t*) { return bf2f(f2bf(v)); }
 __device__ __forceinline__ float as_stream(float v, float*) { return v; }
@@ -221,8 +260,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
 // per row); !PIPE: one row at a time, memory parallelism from occupancy instead.
 // xhat and dy*w are recomputed from the raw words in the second pass rather than
 // kept in registers (VGPRs set this kernel's occupancy, VALU is idle).
-// SPLIT (fp32 stream, bf16 compute): bit 0 — dres is a split-plane gradient (split8);
-// bit 1 — dx is written split (its hi plane is the branch copy, dx_branch unused)
+// SPLIT (fp32 stream): bit 0 — dres is a split-plane gradient (split8, or split8h for
+// fp16 compute); bit 1 — dx is written split (its hi plane is the branch copy, dx_branch unused)
 template <int NK, bool PIPE, typename XT, bool NT = false, bool H = false, int SPLIT = 0>
 __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const XT* __restrict__ x,
                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
@@ -323,7 +362,8 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
         unpack8e<H>(wraw[k], wf);
         float rv[8];  // gradient arriving through the residual path of the fused add
         if (dres) {
-          if constexpr (SPLIT & 1) unsplit8(cr[k].u[0], cr[k].u[Raw8<XT>::W - 1], rv);
+          if constexpr ((SPLIT & 1) && H) unsplit8h(cr[k].u[0], cr[k].u[Raw8<XT>::W - 1], rv);
+          else if constexpr (SPLIT & 1) unsplit8(cr[k].u[0], cr[k].u[Raw8<XT>::W - 1], rv);
           else unpack_raw(cr[k], rv);
         } else {
 #pragma unroll
@@ -339,7 +379,8 @@ __global__ __launch_bounds__(256, NSA_LNB_MINW) void ln_bwd_kernel(const bf16_t*
         }
         if constexpr (SPLIT & 2) {  // hi plane: plain store (the branch GEMMs read it next)
           uint4 hi, lo;
-          split8(o, hi, lo);
+          if constexpr (H) split8h(o, hi, lo);
+          else split8(o, hi, lo);
           uint16_t* hp = reinterpret_cast<uint16_t*>(dx);
           *reinterpret_cast<uint4*>(hp + (int64_t)row * C + c) = hi;
           st16n<NT>(hp + (int64_t)N * C + (int64_t)row * C + c, lo);
@@ -395,7 +436,7 @@ hipError_t launch_bwd_split(int split, const void* dy, const void* x, const void
   ln_bwd_kernel<NK, PIPE, XT, NT, H, SP><<<nblk, 256, 8 * C * sizeof(float), s>>>(                      \
       (const bf16_t*)dy, (const XT*)x, (const bf16_t*)w, (const float*)mean, (const float*)rstd,         \
       (const XT*)dres, (XT*)dx, (bf16_t*)dx_branch, (float*)dw_part, (float*)db_part, N, C)
-  if constexpr (std::is_same<XT, float>::value && !H) {
+  if constexpr (std::is_same<XT, float>::value) {
     switch (split) {
       case 1: NSA_LNB_GO(1); return hipGetLastError();
       case 2: NSA_LNB_GO(2); return hipGetLastError();
@@ -416,7 +457,7 @@ hipError_t launch_bwd(const void* dy, const void* x, const void* w, const void* 
   const bool pipe = !(nblk & (1 << 30));
   const int split = (nblk >> 28) & 3;
   nblk &= (1 << 28) - 1;
-  if (split && (!std::is_same<XT, float>::value || H)) return hipErrorInvalidValue;
+  if (split && !std::is_same<XT, float>::value) return hipErrorInvalidValue;
   if ((split & 1) && dres == nullptr) return hipErrorInvalidValue;
   if (pipe && ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
     return launch_bwd_split<NK, true, XT, true, H>(split, dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
@@ -489,6 +530,18 @@ NSA_API hipError_t nsa_layernorm_bwd_x32s(const void* dy, const void* x, const v
   nblk |= split << 28;
   NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part, db_part,
                                                         N, C, nblk, s)));
+}
+
+// nsa_layernorm_bwd_x32s for fp16 compute (split8h planes: the hi plane is the fp16 branch gradient)
+NSA_API hipError_t nsa_layernorm_bwd_x32s_h(const void* dy, const void* x, const void* w, const void* mean,
+                                            const void* rstd, const void* dres, void* dx, void* dx_branch,
+                                            void* dw_part, void* db_part, int N, int C, int nblk, int split,
+                                            hipStream_t s) {
+  if (C % 8 != 0 || C > 8192 || split < 0 || split > 3 || (nblk & ~(1 << 30)) >= (1 << 28))
+    return hipErrorInvalidValue;
+  nblk |= split << 28;
+  NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float, true>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
+                                                              db_part, N, C, nblk, s)));
 }
 
 // fp16 branch / weights / output with the fp32 stream (dtype float16)

@@ -376,8 +376,40 @@ def unsplit_planes(t: torch.Tensor) -> torch.Tensor:
     return bits.view(torch.float32).view(t.shape)
 
 
+def split_planes_h(g: torch.Tensor) -> torch.Tensor:
+    """fp32 [.., C] -> the fp16-compute split-plane encoding (csrc/kernels/layernorm.hip
+    split8h): hi = fp16(g) (round to nearest even) in the first half of the bytes, the int16
+    q = (g - hi) * 2^(39 - max(E, 1)) (E = hi's exponent field) in the second; exact for
+    |g| >= 2^-14, 2^-39 absolute below, inf at |g| >= 65520."""
+    gd = g.detach().contiguous().reshape(-1)
+    hi = gd.to(torch.float16)
+    e = ((hi.view(torch.int16).to(torch.int32) >> 10) & 31).clamp(min=1)
+    r = gd - hi.float()
+    q = torch.round(torch.ldexp(r, (39 - e).float()))
+    q = torch.where(torch.isfinite(hi), q, torch.zeros_like(q)).to(torch.int16)
+    n = gd.numel()
+    out = torch.empty(2 * n, dtype=torch.int16, device=g.device)
+    out[:n] = hi.view(torch.int16)
+    out[n:] = q
+    return out.view(torch.float32).view(g.shape)
+
+
+def unsplit_planes_h(t: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``split_planes_h``."""
+    n = t.numel()
+    raw = t.detach().contiguous().reshape(-1).view(torch.int16)
+    hi = raw[:n].view(torch.float16)
+    e = ((raw[:n].to(torch.int32) >> 10) & 31).clamp(min=1)
+    return (hi.float() + torch.ldexp(raw[n:].float(), (e - 39).float())).view(t.shape)
+
+
 def _is_split(g) -> bool:
-    return g is not None and getattr(g, "_nsa_split", False)
+    return g is not None and getattr(g, "_nsa_split", None) is not None
+
+
+def _unsplit(g):
+    """A split-plane gradient decoded (the encoding is named by its ``_nsa_split`` dtype)."""
+    return unsplit_planes_h(g) if g._nsa_split == F16 else unsplit_planes(g)
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -414,7 +446,7 @@ class LayerNormFn(torch.autograd.Function):
         ctx.y_dtype = y.dtype if y is not None else None
         ctx.kern = x.is_cuda and out_dtype in KDT
         ctx.split_out = bool(split_grad and LN_SPLIT and ctx.kern and y is not None and x.dtype == F32
-                             and out_dtype == BF16)
+                             and out_dtype in (BF16, F16))
         if ctx.kern:
             assert C % 8 == 0 and C <= 8192, "layernorm kernel: C % 8 == 0 and C <= 8192"
             x32 = x.dtype == F32
@@ -465,8 +497,8 @@ class LayerNormFn(torch.autograd.Function):
             return None, None, None, None, None, None, None
         x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
         ds_split = _is_split(ds)
-        if ds_split and (dh is None or not ctx.kern or x2.dtype != F32 or dh.dtype != BF16):
-            ds, ds_split = unsplit_planes(ds), False  # a receiver the split kernel does not cover
+        if ds_split and (dh is None or not ctx.kern or x2.dtype != F32 or dh.dtype != ds._nsa_split):
+            ds, ds_split = _unsplit(ds), False  # a receiver the split kernel does not cover
         b = b_or_mean if ctx.has_bias else None
         C = x2.shape[-1]
         N = x2.shape[0]
@@ -482,11 +514,11 @@ class LayerNormFn(torch.autograd.Function):
             if ds2 is not None and ds2.dtype != x2.dtype:
                 ds2 = ds2.to(x2.dtype)
             dx = torch.empty_like(x2)
-            split_out = ctx.split_out and x32 and dy2.dtype == BF16
+            split_out = ctx.split_out and x32 and dy2.dtype in (BF16, F16)
             # the fused form also hands the branch (y) its gradient in y's dtype (split: the
             # hi plane of dx itself)
             if split_out:
-                dyb = dx.view(BF16).view(-1)[:N * C].view(N, C)
+                dyb = dx.view(dy2.dtype).view(-1)[:N * C].view(N, C)
             else:
                 dyb = (torch.empty(N, C, device=dh.device, dtype=ctx.y_dtype)
                        if (ctx.fused and x32 and not ctx.passthrough) else None)
@@ -495,7 +527,7 @@ class LayerNormFn(torch.autograd.Function):
             db_part = torch.empty(nblk, C, device=dh.device, dtype=F32) if b is not None else None
             wc = compute_weight(w, dy2.dtype)
             if x32 and (ds_split or split_out):
-                _lib.call("nsa_layernorm_bwd_x32s", _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
+                _lib.call(_sym("nsa_layernorm_bwd_x32s", dy2.dtype), _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(wc), _lib.ptr(mean),
                           _lib.ptr(rstd), _lib.ptr(ds2), _lib.ptr(dx), None, _lib.ptr(dw_part),
                           _lib.ptr(db_part), N, C, nblk, (1 if ds_split else 0) | (2 if split_out else 0),
                           _lib.stream())
@@ -511,7 +543,7 @@ class LayerNormFn(torch.autograd.Function):
             gb = _colsum_into(b, db_part) if b is not None else None
             dx = dx.view(shape)
             if split_out:
-                dx._nsa_split = True
+                dx._nsa_split = dy2.dtype
             if not ctx.fused or ctx.passthrough:
                 return dx, None, gw, gb, None, None, None
             return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None, None, None
@@ -1063,13 +1095,17 @@ def _fused_xent_ok(M, C, Vp):
             and C <= 8192)
 
 
-# The fused cross-entropy for fp16 compute (opt-in, NSA_XENT_F16=1): 13.5 ms/step faster at
-# GPT-2 124M (413.5 vs 427.0 ms; bf16 400.1), but dW = E^T (x g / S) carries the 1/S of a row
-# on the fp16 x operand, which lands in fp16's subnormal range for a row whose target logit
-# sits far below its max (S = exp(loss) large): ~1e-3..1e-2 relative error on those rows'
-# weight-gradient terms, where autocast's fp16 dlogits g (p - onehot) keep 2^-11.  The
-# default fp16 path is therefore autocast's: fp16 logits, the fp32 softmax pass, fp16 dlogits.
-XENT_F16 = os.environ.get("NSA_XENT_F16", "0") == "1"
+# The fused cross-entropy for fp16 compute (default; NSA_XENT_F16=0 selects autocast's form:
+# fp16 logits, the fp32 softmax pass, fp16 dlogits): 13.5 ms/step faster at GPT-2 124M
+# (413.5 vs 427.0 ms).  Its dW = E^T (x g / S) carries a row's 1/S on the fp16 x operand,
+# which for a large S (the target logit far below the row max) lands in fp16's subnormal
+# range: ~5e-3 relative error on the vocabulary rows no token targets at init-like logits,
+# against 4e-4 for autocast's form.  Everywhere else it is the more accurate of the two
+# (fp16 dlogits round every p - onehot to 2^-11 and go subnormal below p = 6e-5): against
+# fp32 on the same fp16 inputs at the bench's g, dW 5.4e-5 vs 2.1e-4 and dX 2.1e-4 vs
+# 2.9e-4 at init-like logits, dW 1.4e-4 vs 1.2e-3 and dX 2.1e-4 vs 1.2e-3 at sharp ones
+# (scripts/debug/xent_f16_vs_autocast.py, profiles/r5_xent16_vs_autocast.log).
+XENT_F16 = os.environ.get("NSA_XENT_F16", "1") == "1"
 
 
 def _xent_range(dtype):
@@ -1107,7 +1143,7 @@ class LMHeadLossFn(torch.autograd.Function):
             wp, _ = _lm_weight(w, x.dtype)
             Vp = wp.shape[0]
             row_loss = torch.empty(N, device=x.device, dtype=F32)
-            # E = exp(logit - target logit) in the compute dtype; fp16 only with XENT_F16 (see there)
+            # E = exp(logit - target logit) in the compute dtype; fp16 unless XENT_F16 is off (see there)
             ctx.fused = _fused_xent_ok(N, C, Vp) and (x.dtype == BF16 or XENT_F16)
             if ctx.fused:
                 shift, lo, hi = _xent_range(x.dtype)

@@ -149,6 +149,38 @@ def test_flash_fp16(kernels, B, T, H, D, p):
         assert rel_err(y, yb) < 3e-2
 
 
+@pytest.mark.parametrize("fwd", ["v4", "v5"])
+@pytest.mark.parametrize("pattern", ["plain", "rising", "spikes", "big", "overflow", "underflow"])
+def test_flash_fp16_fast_tile_range(kernels, fwd, pattern):
+    """The v5 forward's fast tiles (no running max) in fp16: P = 2^s must stay below 65504
+    and row sums above 2^-8, else the wave hands over to exact tiles.  Score patterns on
+    both sides of that range (up to ~+-140 log2 units) against fp32 SDPA, v4 alongside."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops.functional import flash_variant
+    torch.manual_seed(1)
+    B, T, H, D = 1, 512, 2, 64
+    C = H * D
+    q, k, v = (torch.randn(B, T, H, D, device=DEV) for _ in range(3))
+    u = torch.nn.functional.normalize(torch.randn(D, device=DEV), dim=0)
+    q = q + 4.0 * u
+    if pattern == "rising":
+        k = k + (torch.linspace(0, 1, T, device=DEV) * 40.0)[None, :, None, None] * u
+    elif pattern == "spikes":
+        k[:, torch.randint(0, T, (24,), device=DEV)] += 30.0 * u
+    elif pattern == "big":  # scores ~ +8 (log2 ~ 11.5): fast tiles near the fp16 bound
+        k = k + 16.0 * u
+    elif pattern == "overflow":
+        k = k + 200.0 * u
+    elif pattern == "underflow":
+        k = k - 200.0 * u
+    qkv = torch.cat([q.reshape(B, T, C), k.reshape(B, T, C), v.reshape(B, T, C)], -1).to(H16)
+    with flash_variant(fwd=fwd):
+        y = ops.attention(qkv, H, 0.0, True)
+    yr = attn_ref(qkv.float(), H)
+    assert torch.isfinite(y.float()).all()
+    assert rel_err(y, yr) < 4e-3, rel_err(y, yr)
+
+
 def test_flash_fp16_exact_structure(kernels):
     """Q = 0, V one-hot by 64-key tile: y[q, d] = (visible keys of tile d) / (q + 1)."""
     from nanosandbox_amd.ops import _lib
@@ -169,6 +201,50 @@ def test_flash_fp16_exact_structure(kernels):
     got = y.float().view(B, T, H, D)
     assert not torch.isnan(got).any() and not torch.isnan(lse).any()
     assert ((got - ref[None, :, None, :]).abs() <= 2 ** -11 * ref[None, :, None, :] + 1e-7).all()
+
+
+@pytest.mark.parametrize("split", [1, 2, 3])
+def test_layernorm_bwd_split_planes_fp16(kernels, split):
+    """nsa_layernorm_bwd_x32s_h (fp16 compute) against nsa_layernorm_bwd_x32_h on the same
+    inputs, NaN-prefilled outputs: a split dres (split8h, bit 0) is read back exactly, a split
+    dx (bit 1) decodes to the plain kernel's fp32 dx bit for bit for |dx| >= 2^-14 (2^-39
+    absolute below) and its hi plane is the plain kernel's fp16 branch copy exactly."""
+    from nanosandbox_amd.ops import _lib
+    from nanosandbox_amd.ops.functional import split_planes_h, unsplit_planes_h
+    torch.manual_seed(11)
+    N, C = 1100, 768
+    s = torch.randn(N, C, device=DEV) * 2 + 0.5
+    w = (torch.randn(C, device=DEV) * 0.5 + 1).to(H16)
+    mean = s.mean(-1)
+    rstd = torch.rsqrt(s.var(-1, unbiased=False) + 1e-5)
+    dh = torch.randn(N, C, device=DEV).to(H16)
+    dres = torch.randn(N, C, device=DEV) * 0.1
+    dres[0, :4] = torch.tensor([3e-39, -1e-6, 0.0, -0.0])  # denormal, tiny, signed zeros
+    nblk = 16
+    nan = lambda *sh, dt=torch.float32: torch.full(sh, float("nan"), device=DEV, dtype=dt)  # noqa: E731
+    din = unsplit_planes_h(split_planes_h(dres)) if split & 1 else dres  # what the split reader sees
+    dx0, dxb0, dwp0 = nan(N, C), nan(N, C, dt=H16), nan(nblk, C)
+    _lib.call("nsa_layernorm_bwd_x32_h", _lib.ptr(dh), _lib.ptr(s), _lib.ptr(w), _lib.ptr(mean), _lib.ptr(rstd),
+              _lib.ptr(din), _lib.ptr(dx0), _lib.ptr(dxb0), _lib.ptr(dwp0), None, N, C, nblk, _lib.stream())
+    enc_in = split_planes_h(dres) if split & 1 else dres
+    dx1, dwp1 = nan(N, C), nan(nblk, C)
+    _lib.call("nsa_layernorm_bwd_x32s_h", _lib.ptr(dh), _lib.ptr(s), _lib.ptr(w), _lib.ptr(mean), _lib.ptr(rstd),
+              _lib.ptr(enc_in), _lib.ptr(dx1), None, _lib.ptr(dwp1), None, N, C, nblk, split, _lib.stream())
+    torch.cuda.synchronize()
+    assert not torch.isnan(dx0).any()
+    if split & 2:
+        back = unsplit_planes_h(dx1)
+        normal = dx0.abs() >= 2 ** -14
+        assert torch.equal(back[normal], dx0[normal])
+        assert ((back - dx0).abs()[~normal] <= 2.0 ** -39).all()
+        hi = dx1.view(H16).reshape(-1)[:N * C].view(N, C)
+        bad = hi.view(torch.int16) != dxb0.view(torch.int16)
+        # (a fused FMA-to-fp16 conversion once rounded exact fp16 ties of dx the other way)
+        assert not bad.any(), (int(bad.sum()), dx0[bad][:6].tolist(), hi[bad][:6].tolist(), dxb0[bad][:6].tolist())
+        assert torch.equal(hi.view(torch.int16), dx0.to(H16).view(torch.int16))
+    else:
+        assert torch.equal(dx1, dx0)
+    assert torch.equal(dwp1, dwp0)
 
 
 @pytest.mark.parametrize("N,C,bias", [(300, 768, True), (33, 1600, False)])
@@ -222,13 +298,17 @@ def test_embedding_fp16_weights(kernels):
     assert rel_err(wte.grad, gwte) < 1e-5
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("N,V,C", [(1024, 50304, 768), (1024, 50257, 768), (200, 65, 64)])
-def test_lm_head_loss_fp16(kernels, N, V, C):
+def test_lm_head_loss_fp16(kernels, monkeypatch, N, V, C, fused):
     """fp16: the fused form (E = exp(logit - target logit) in fp16 from the lm_head GEMM's
-    epilogue; 1024-row shapes) and autocast's form (fp16 logits, fp32 softmax pass; the tiny
-    shape).  The loss is scaled as the dynamic loss scale scales it (fp16 gradients of an
-    unscaled mean loss sit in fp16's subnormal range, with or without the fused form)."""
+    epilogue; the default, 1024-row shapes) and autocast's form (fp16 logits, fp32 softmax
+    pass; NSA_XENT_F16=0, and the tiny shape either way).  The loss is scaled as the dynamic
+    loss scale scales it (fp16 gradients of an unscaled mean loss sit in fp16's subnormal
+    range, with or without the fused form)."""
     from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+    monkeypatch.setattr(Fn, "XENT_F16", fused)
     torch.manual_seed(0)
     x = torch.randn(N, C, device=DEV).to(H16).requires_grad_(True)
     w = torch.nn.Parameter(torch.randn(V, C, device=DEV) * 0.05)
@@ -250,7 +330,7 @@ def test_lm_head_loss_fp16(kernels, N, V, C):
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_lm_head_loss_fp16_fixup_rows(kernels, monkeypatch, graph):
-    """The fused fp16 cross-entropy (opt-in, ops.functional.XENT_F16) keeps a row while its
+    """The fused fp16 cross-entropy (the default, ops.functional.XENT_F16) keeps a row while its
     largest logit stays within ~11 nats of the target's; rows past that (here 100 rows at
     logits ~ +-1300, some with the last real vocabulary id as target, some ignored, and rows
     with gaps of tens of nats) go to the exact fix-up, under HIP-graph replay too.  Loss and
@@ -342,3 +422,35 @@ def test_gpt_fp16_matches_fp32_reference(kernels):
         if p.dim() >= 2:
             e = rel_err(p.grad.cpu(), gref[n].grad)
             assert e < 2e-2, (n, e)
+
+
+def test_gpt_fp16_split_residual_grad_matches_plain(kernels):
+    """fp16 compute: the GPT trunk with split-plane residual gradients (split8h, the default)
+    against plain fp32 + fp16-copy gradients, deterministic mode, a loss scaled as the dynamic
+    loss scale would: the hi plane is torch's fp16 cast and the residual path exact for
+    |g| >= 2^-14 (2^-39 absolute below), so the parameter gradients agree bit for bit except
+    where such a tiny residual-gradient element moved (at most a few fp32 ulps)."""
+    from nanosandbox_amd.models.gpt import GPT, GPTConfig
+    from nanosandbox_amd.ops import functional as Fn
+    torch.manual_seed(2)
+    cfg = GPTConfig(block_size=256, vocab_size=512, n_layer=3, n_head=4, n_embd=256, dropout=0.0, bias=True)
+    model = GPT(cfg).to(DEV).set_compute_dtype(H16)
+    idx = torch.randint(0, 512, (4, 256), device=DEV)
+    tgt = torch.randint(0, 512, (4, 256), device=DEV)
+    prev = (Fn.LN_SPLIT, Fn._gd.DETERMINISTIC)
+    grads = []
+    try:
+        Fn.set_deterministic(True)
+        for flag in (True, False, True):
+            Fn.LN_SPLIT = flag
+            model.zero_grad(set_to_none=True)
+            _, loss = model(idx, tgt)
+            (loss * 1024.0).backward()
+            grads.append({n: p.grad.clone() for n, p in model.named_parameters()})
+    finally:
+        Fn.LN_SPLIT, Fn._gd.DETERMINISTIC = prev
+    for n in grads[0]:
+        assert torch.isfinite(grads[0][n]).all(), n
+        assert torch.equal(grads[0][n], grads[2][n]), n
+        ref = grads[1][n]
+        assert ((grads[0][n] - ref).abs() <= 2 ** -20 * ref.abs().max() + 1e-12).all(), n

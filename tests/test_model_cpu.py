@@ -274,3 +274,31 @@ def test_split_planes_roundtrip_bitwise():
     back = unsplit_planes(enc)
     assert torch.equal(back.view(torch.int32)[fin], g.view(torch.int32)[fin])
     assert torch.isnan(back[~fin]).all()
+
+
+def test_split_planes_fp16_roundtrip():
+    """The fp16-compute split encoding (csrc/kernels/layernorm.hip split8h): the hi plane is
+    torch's fp16 cast; hi + lo give g back bit for bit for 2^-14 <= |g| < 65520 (binade
+    edges, values that round up into the next binade, ties), within 2^-39 below that
+    (subnormal and zero hi), an fp16 inf at and above 65520, infinities kept, NaN stays NaN."""
+    from nanosandbox_amd.ops.functional import split_planes_h, unsplit_planes_h
+    torch.manual_seed(0)
+    g = torch.randn(64, 48) * torch.logspace(-12, 4.8, 48)[None]  # up to ~6e4
+    special = torch.tensor([2.0 ** -14, -(2.0 ** -14), 2.0 ** -14 * (1 + 2 ** -20), 1.0 + 2 ** -11,
+                            1.0 + 3 * 2 ** -11, 2.0 - 2 ** -23, 65504.0, 65519.99, -65519.99, 1.0 + 2 ** -12,
+                            3e-5, -1e-8, 0.0, -0.0, 1e-30])
+    g[0, :special.numel()] = special
+    enc = split_planes_h(g)
+    n = g.numel()
+    hi = enc.reshape(-1).view(torch.float16)[:n].view(g.shape)
+    assert torch.equal(hi.view(torch.int16), g.to(torch.float16).view(torch.int16))
+    back = unsplit_planes_h(enc)
+    normal = (g.abs() >= 2 ** -14) & (g.abs() < 65520)
+    assert torch.equal(back.view(torch.int32)[normal], g.view(torch.int32)[normal])
+    tiny = g.abs() < 2 ** -14
+    assert ((back - g).abs()[tiny] <= 2.0 ** -39).all()
+    assert torch.isinf(back[g.abs() >= 65520]).all()
+    edge = torch.tensor([65520.0, -70000.0, float("inf"), float("-inf"), float("nan")])
+    be = unsplit_planes_h(split_planes_h(edge))
+    assert be[0].item() == float("inf") and be[1].item() == float("-inf")
+    assert be[2].item() == float("inf") and be[3].item() == float("-inf") and torch.isnan(be[4])
