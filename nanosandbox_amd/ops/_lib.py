@@ -116,6 +116,7 @@ _SIGNATURES = {
     "nsa_xent_dw_fix": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                         c_void_p],
     "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+    "nsa_gemm_strip": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
 }
 
 

@@ -1082,3 +1082,51 @@ def test_deterministic_kernels_match_default(kernels):
             ops.set_deterministic(False)
     assert torch.equal(grads[1][0], grads[2][0]) and torch.equal(grads[1][1], grads[2][1])
     assert rel_err(grads[1][0], grads[0][0]) < 1e-5 and rel_err(grads[1][1], grads[0][1]) < 1e-6
+
+
+@pytest.mark.parametrize("H", [False, True])
+@pytest.mark.parametrize("M,NS,K,bias", [(61440 // 16, 64, 1600, False), (1000, 64, 640, True), (777, 16, 128, True),
+                                         (300, 48, 64, False)])
+def test_gemm_strip_raw(kernels, H, M, NS, K, bias):
+    """nsa_gemm_strip into columns 0..NS of a NaN-prefilled [M, NS + 40] buffer (row stride
+    NS + 40): the strip matches fp32 per element (one output rounding), the other columns
+    stay untouched; ragged M (rows past a 64-row block), NS of 1-4 fragments, bias."""
+    from nanosandbox_amd.ops import _lib
+    dt = torch.float16 if H else BF
+    torch.manual_seed(4)
+    a = (torch.randn(M, K, device=DEV) * 0.5).to(dt)
+    b = (torch.randn(NS, K, device=DEV) * 0.5).to(dt)
+    bs = (torch.randn(NS, device=DEV)).to(dt) if bias else None
+    ldc = NS + 40
+    c = torch.full((M, ldc), float("nan"), device=DEV, dtype=dt)
+    _lib.call("nsa_gemm_strip_h" if H else "nsa_gemm_strip", _lib.ptr(a), K, _lib.ptr(b), K, _lib.ptr(c), ldc,
+              _lib.ptr(bs), M, NS, K, _lib.stream())
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t() + (bs.float() if bias else 0.0)
+    got = c[:, :NS].float()
+    assert not torch.isnan(got).any()
+    ulp = 2.0 ** (-10 if H else -7)
+    assert ((got - ref).abs() <= ulp * ref.abs() + 1e-3 * (a.float().abs() @ b.float().abs().t())).all()
+    assert torch.isnan(c[:, NS:].float()).all()
+
+
+@pytest.mark.parametrize("N", [1600, 1552, 1328])
+def test_nt_strip_dispatch(kernels, monkeypatch, N):
+    """NSA_NT_STRIP=1 (A/B form): N = 256 q + r (16 <= r <= 64) as the four-wave kernel over
+    256 q columns plus the strip kernel, one output; recorded as "nt4+strip"; equal to the
+    whole-width four-wave result."""
+    from nanosandbox_amd.ops import gemm, gemm_dispatch
+    monkeypatch.setattr(gemm_dispatch, "STRIP", True)
+    torch.manual_seed(5)
+    M, K = 1024, 640
+    a = (torch.randn(M, K, device=DEV) * 0.5).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.5).to(BF)
+    bias = torch.randn(N, device=DEV).to(BF)
+    gemm_dispatch._used.clear()
+    y = gemm_dispatch.fwd(a, w, bias)
+    assert gemm_dispatch.kernels_used()[("fwd", M, N, K)] == "nt4+strip"
+    full = gemm.nt(a, w, bias=bias)
+    ref = a.float() @ w.float().t() + bias.float()
+    assert rel_err(y, ref) < 1e-2
+    # same fp32 accumulation order per element up to the K-step grouping: within an ulp
+    assert ((y.float() - full.float()).abs() <= 2 ** -7 * full.float().abs() + 1e-3).all()
