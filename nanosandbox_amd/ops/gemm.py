@@ -248,6 +248,20 @@ def wgrad_splits(n_out, n_in, tokens, cus=256):
         return max(1, min(WGRAD_SPLITS, max(1, tokens // BK)))
     tiles = -(-n_out // TILE) * -(-n_in // TILE)
     nkb = max(1, tokens // BK)
+    s = _wgrad_splits_fill(tiles, nkb, cus)
+    if nkb < _WG_SHORT * s:
+        # short work items: each one's 256 KB fp32 atomic epilogue is no longer small next
+        # to its K loop (shakespeare_char, 16384 tokens: 384 x 384 at 64 splits = 41.3 us,
+        # 27.6 at 32; scripts/debug/wgrad_small_ab.py, profiles/r5_wgrad_small.log)
+        s = _wgrad_splits_cost(tiles, nkb, cus)
+    return s
+
+
+_WG_SHORT = 32  # K-tiles per work item below which the atomic epilogue enters the split rule
+_WG_TK, _WG_TA = 2.1, 0.2  # us: one 256 x 256 x 64 K-tile on a CU; one item's fp32 atomics (256 KB at ~1.3 TB/s)
+
+
+def _wgrad_splits_fill(tiles, nkb, cus):
     if tiles < cus and tiles * min(cus // tiles, nkb) >= 0.9 * cus:
         return max(1, min(cus // tiles, nkb))
     best, best_fill = 1, -1.0
@@ -258,6 +272,19 @@ def wgrad_splits(n_out, n_in, tokens, cus=256):
             return s
         if fill > best_fill + 1e-9:
             best, best_fill = s, fill
+    return best
+
+
+def _wgrad_splits_cost(tiles, nkb, cus):
+    """The split count minimising rounds x K-tiles per item x _WG_TK + items x _WG_TA (on the
+    124M / 350M shapes this model picks the round-fill rule's counts but for one; measured on
+    the short shapes only)."""
+    best, best_t = 1, None
+    for s in range(1, min(64, nkb) + 1):
+        items = tiles * s
+        t = -(-items // cus) * (nkb / s) * _WG_TK + items * _WG_TA
+        if best_t is None or t < best_t - 1e-9:
+            best, best_t = s, t
     return best
 
 
