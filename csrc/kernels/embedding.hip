@@ -15,6 +15,7 @@
 // The output (the residual stream) and its gradient are bf16 or fp32 (XT): fp32 is
 // nanoGPT's autocast contract (the embedding sum stays fp32), bf16 is opt-in.
 #include "common.h"
+#include "segsum.h"
 
 namespace {
 
@@ -131,169 +132,27 @@ __global__ __launch_bounds__(256) void emb_bwd_wpe_kernel(const XT* __restrict__
   g[1] = g1;
 }
 
-// Deterministic dwte without atomics (the sorted path: every micro-step of >= 4096 tokens,
-// and the deterministic mode).  The caller stably sorts the token positions by vocab id
-// (ids = sorted ids, order = their positions, seg = segment starts by id).  Two regimes,
-// one writer per row either way (cdna_hip_programming.md App. B, "scatter-add without
-// atomics": split long lists into chunks, add the partial sums in chunk order in a
-// further pass):
-//   short segments (<= kDetLong tokens; GPT-2's 50304 ids average 2.4 tokens a
-//     micro-step): one wave per id sums its tokens' rows in token order (row kernel).
-//   long segments (a character corpus: 56 ids, the space ~15% of all tokens): the sorted
-//     list is cut into chunks of kDetChunk positions, one wave each; a long segment
-//     always crosses a chunk boundary, so each chunk leaves the partial sum of its long
-//     runs in part[chunk][slot] (slot 0: the chunk's first run, 1: its last), and the
-//     chunk in which the segment ends adds its partials in chunk order (fix kernel).
-// Fixed summation order for any schedule: bitwise reproducible.  Rows are gathered four
-// (row kernel) or eight (chunk kernel) at a time so that many 16-byte loads per lane are in
-// flight (round 4's one-wave-per-id serial walk took 2.3 ms per micro-step on the character
-// config, its 5000-token space row).
-constexpr int kDetChunk = 16;
-constexpr int kDetLong = 64;
-
+// Atomic-free dwte (the sorted path: micro-steps of >= 64K tokens, and the deterministic
+// mode): the caller stably sorts the token positions by vocab id and segsum.h's passes add
+// each id's dropout-masked dx rows into its row of dwte, one writer per row (the chunked form
+// for frequent ids: round 4's one-wave-per-id serial walk took 2.3 ms per micro-step on the
+// character config, its 5000-token space row; profiles/r5_emb_bwd.md).
 template <typename XT>
-__global__ __launch_bounds__(256) void emb_bwd_wte_row_kernel(const int64_t* __restrict__ order,
-                                                             const int64_t* __restrict__ seg,
-                                                             const XT* __restrict__ dx, float* __restrict__ dwte,
-                                                             int V, int C, uint32_t thresh, float scale,
-                                                             uint64_t salt) {
-  const uint64_t seed = nsa_seed(salt);
-  const int lane = threadIdx.x & 63;
-  const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (v >= V) return;
-  const int64_t beg = seg[v], end = seg[v + 1];
-  if (beg == end || end - beg > kDetLong) return;  // empty, or the chunk kernels' segment
-  for (int c = lane * 8; c < C; c += 512) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t k = beg; k < end; k += 4) {
-      const int n = (int)min((int64_t)4, end - k);
-      int64_t rw[4];
-      float f[4][8];
+struct EmbRow {
+  const XT* dx;
+  int C;
+  uint32_t thresh;
+  float scale;
+  uint64_t salt;
+  __device__ __forceinline__ void load(int64_t row, int64_t, int c, float (&f)[8]) const {
+    ld8(dx + row * C + c, f);
+    if (thresh) {
+      const uint64_t seed = nsa_seed(salt);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) rw[u] = u < n ? order[k + u] : 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (u < n) ld8(dx + rw[u] * C + c, f[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (u < n) {
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            float x = f[u][jj];
-            if (thresh) x = nsa_keep(seed, (uint64_t)rw[u] * C + c + jj, thresh) ? x * scale : 0.0f;
-            acc[jj] += x;
-          }
-        }
+      for (int j = 0; j < 8; ++j) f[j] = nsa_keep(seed, (uint64_t)row * C + c + j, thresh) ? f[j] * scale : 0.0f;
     }
-    float4* g = reinterpret_cast<float4*>(dwte + (int64_t)v * C + c);
-    float4 g0 = g[0], g1 = g[1];
-    g0.x += acc[0]; g0.y += acc[1]; g0.z += acc[2]; g0.w += acc[3];
-    g1.x += acc[4]; g1.y += acc[5]; g1.z += acc[6]; g1.w += acc[7];
-    g[0] = g0;
-    g[1] = g1;
   }
-}
-
-template <typename XT>
-__global__ __launch_bounds__(256) void emb_bwd_wte_chunk_kernel(const int64_t* __restrict__ ids,
-                                                               const int64_t* __restrict__ order,
-                                                               const int64_t* __restrict__ seg,
-                                                               const XT* __restrict__ dx, float* __restrict__ part,
-                                                               int N, int C, uint32_t thresh, float scale,
-                                                               uint64_t salt) {
-  const uint64_t seed = nsa_seed(salt);
-  const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j * kDetChunk >= N) return;
-  const int p0 = j * kDetChunk, n = min(N - p0, kDetChunk);
-  int64_t id[kDetChunk], rw[kDetChunk];
-  uint32_t lmask = 0;  // positions of the chunk that belong to long segments
-#pragma unroll
-  for (int q = 0; q < kDetChunk; ++q) id[q] = q < n ? ids[p0 + q] : -1;
-#pragma unroll
-  for (int q = 0; q < kDetChunk; ++q)
-    if (q < n && seg[id[q] + 1] - seg[id[q]] > kDetLong) lmask |= 1u << q;
-  if (!lmask) return;
-#pragma unroll
-  for (int q = 0; q < kDetChunk; ++q) rw[q] = (lmask >> q) & 1 ? order[p0 + q] : 0;
-  for (int c = lane * 8; c < C; c += 512) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int rs = 0;  // start of the current run
-    // a long run crosses a chunk boundary by length: its partial sum always goes to part
-    auto flush = [&]() {
-      if (!((lmask >> rs) & 1)) return;
-      float4* g = reinterpret_cast<float4*>(part + ((int64_t)j * 2 + (rs == 0 ? 0 : 1)) * C + c);
-      g[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      g[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    };
-#pragma unroll
-    for (int b = 0; b < kDetChunk; b += 8) {
-      float f[8][8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((lmask >> (b + u)) & 1) ld8(dx + rw[b + u] * C + c, f[u]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = b + u;
-        if (q < n) {
-          if (id[q] != id[rs]) {
-            flush();
-            rs = q;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) acc[jj] = 0.0f;
-          }
-          if ((lmask >> q) & 1) {
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-              float x = f[u][jj];
-              if (thresh) x = nsa_keep(seed, (uint64_t)rw[q] * C + c + jj, thresh) ? x * scale : 0.0f;
-              acc[jj] += x;
-            }
-          }
-        }
-      }
-    }
-    flush();
-  }
-}
-
-__global__ __launch_bounds__(256) void emb_bwd_wte_fix_kernel(const int64_t* __restrict__ ids,
-                                                             const int64_t* __restrict__ seg,
-                                                             const float* __restrict__ part,
-                                                             float* __restrict__ dwte, int N, int C) {
-  const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j == 0 || j * kDetChunk >= N) return;
-  const int p0 = j * kDetChunk, pend = min(N, p0 + kDetChunk);
-  const int64_t u = ids[p0];
-  if (ids[p0 - 1] != u) return;            // the chunk's first run starts here: not a crossing segment
-  if (pend < N && ids[pend] == u) return;  // the segment goes on past this chunk
-  const int64_t s = seg[u];
-  if (seg[u + 1] - s <= kDetLong) return;  // a short segment: the row kernel's
-  const int js = (int)(s / kDetChunk);
-  const int s1 = s > (int64_t)js * kDetChunk ? 1 : 0;  // slot of the first piece
-  for (int c = lane * 8; c < C; c += 512) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i0 = js; i0 <= j; i0 += 8) {
-      float f[8][8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (i0 + q <= j) ld8(part + ((int64_t)(i0 + q) * 2 + (i0 + q == js ? s1 : 0)) * C + c, f[q]);
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (i0 + q <= j) {
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) acc[jj] += f[q][jj];
-        }
-    }
-    float4* g = reinterpret_cast<float4*>(dwte + u * C + c);
-    float4 g0 = g[0], g1 = g[1];
-    g0.x += acc[0]; g0.y += acc[1]; g0.z += acc[2]; g0.w += acc[3];
-    g1.x += acc[4]; g1.y += acc[5]; g1.z += acc[6]; g1.w += acc[7];
-    g[0] = g0;
-    g[1] = g1;
-  }
-}
+};
 
 template <typename XT, bool H = false>
 hipError_t launch_fwd(const void* idx, const void* wte, const void* wpe, void* out, int N, int T, int C, float p,
@@ -330,20 +189,9 @@ hipError_t launch_bwd_det(const void* ids, const void* order, const void* seg, v
   if (C % 8 != 0) return hipErrorInvalidValue;
   const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
   const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
-  const int N = B * T;
-  const int chunks = (N + kDetChunk - 1) / kDetChunk;
-  emb_bwd_wte_row_kernel<XT><<<(V + 3) / 4, 256, 0, s>>>((const int64_t*)order, (const int64_t*)seg,
-                                                          (const XT*)dx, (float*)dwte, V, C, th, scale, seed);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  emb_bwd_wte_chunk_kernel<XT><<<(chunks + 3) / 4, 256, 0, s>>>((const int64_t*)ids, (const int64_t*)order,
-                                                                (const int64_t*)seg, (const XT*)dx, (float*)part,
-                                                                N, C, th, scale, seed);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  emb_bwd_wte_fix_kernel<<<(chunks + 3) / 4, 256, 0, s>>>((const int64_t*)ids, (const int64_t*)seg,
-                                                          (const float*)part, (float*)dwte, N, C);
-  e = hipGetLastError();
+  const EmbRow<XT> f{(const XT*)dx, C, th, scale, seed};
+  hipError_t e = seg_scatter_add<int64_t, EmbRow<XT>>((const int64_t*)ids, (const int64_t*)order, (const int64_t*)seg,
+                                                      (float*)part, f, (float*)dwte, C, B * T, V, C, s);
   if (e != hipSuccess) return e;
   const int work = T * (C / 8);
   emb_bwd_wpe_kernel<XT><<<(work + 255) / 256, 256, 0, s>>>((const XT*)dx, (float*)dwpe, B, T, C, th, scale, seed);

@@ -13,6 +13,7 @@
 // Rows whose S leaves [0.5, 1e30] (a per-token loss beyond ~69 nats, or a target logit far
 // from the GEMM's) are recomputed exactly by nsa_xent_fixup (normally none: the kernel exits).
 #include "common.h"
+#include "segsum.h"
 
 namespace {
 
@@ -202,6 +203,33 @@ __global__ __launch_bounds__(256) void xent_dw_fix_kernel(const bf16_t* __restri
   }
 }
 
+// The same onehot term without atomics: the valid rows stably sorted by target (segsum.h;
+// the fp32 atomics above contend on the few rows of a small vocabulary and run at the chip's
+// atomic rate on GPT-2's)
+template <bool H>
+struct XentFixRow {
+  const bf16_t* x;
+  int ldx;
+  const bf16_t* E;
+  int lde;
+  const int* t32;
+  const float* invS;
+  const float* gsc;
+  // t = the row's target (the destination id): no dependent load of t32
+  __device__ __forceinline__ void load(int64_t row, int64_t t, int c, float (&f)[8]) const {
+    const float g = *gsc;
+    const float s = g * invS[row];
+    const float et = e2f<H>(E[row * lde + t]);
+    float a[8];
+    load8e<H>(x + row * ldx + c, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float p = s * a[j];
+      f[j] = et * (p - e2f<H>(f2e<H>(p))) - g * a[j];
+    }
+  }
+};
+
 }  // namespace
 
 namespace {
@@ -239,7 +267,32 @@ hipError_t dw_fix_entry(const void* x, int ldx, const void* E, int lde, const vo
                                                     (const float*)invS, (const float*)gsc, (float*)gW, ldg, M, C);
   return hipGetLastError();
 }
+template <bool H>
+hipError_t dw_fix_sorted_entry(const void* x, int ldx, const void* E, int lde, const void* t32, const void* invS,
+                               const void* gsc, const void* ids, const void* order, const void* seg, void* part,
+                               void* gW, int ldg, int M, int C, int V, hipStream_t s) {
+  if (C % 8 || ldx % 8) return hipErrorInvalidValue;
+  const XentFixRow<H> f{(const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32, (const float*)invS,
+                        (const float*)gsc};
+  return seg_scatter_add<int, XentFixRow<H>>((const int*)ids, (const int64_t*)order, (const int64_t*)seg,
+                                             (float*)part, f, (float*)gW, ldg, M, V, C, s);
+}
 }  // namespace
+
+// the onehot dW term, atomic-free: ids = t32 stably sorted (int32), order = their rows,
+// seg[V + 1] = segment starts, part = [2 * ceil(M / 16), C] fp32 workspace (segsum.h)
+NSA_API hipError_t nsa_xent_dw_fix_sorted(const void* x, int ldx, const void* E, int lde, const void* t32,
+                                          const void* invS, const void* gsc, const void* ids, const void* order,
+                                          const void* seg, void* part, void* gW, int ldg, int M, int C, int V,
+                                          hipStream_t s) {
+  return dw_fix_sorted_entry<false>(x, ldx, E, lde, t32, invS, gsc, ids, order, seg, part, gW, ldg, M, C, V, s);
+}
+NSA_API hipError_t nsa_xent_dw_fix_sorted_h(const void* x, int ldx, const void* E, int lde, const void* t32,
+                                            const void* invS, const void* gsc, const void* ids, const void* order,
+                                            const void* seg, void* part, void* gW, int ldg, int M, int C, int V,
+                                            hipStream_t s) {
+  return dw_fix_sorted_entry<true>(x, ldx, E, lde, t32, invS, gsc, ids, order, seg, part, gW, ldg, M, C, V, s);
+}
 
 // c = the target logit (+ shift; 0 for bf16 E), t32 = the target or -1 (ignored / out of range)
 NSA_API hipError_t nsa_xent_tlogit(const void* x, int ldx, const void* W, int ldw, const void* tgt, void* crow,

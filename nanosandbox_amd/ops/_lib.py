@@ -115,6 +115,8 @@ _SIGNATURES = {
                           c_void_p, c_int, c_int, c_void_p],
     "nsa_xent_dw_fix": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                         c_void_p],
+    "nsa_xent_dw_fix_sorted": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "nsa_gemm_strip": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
 }

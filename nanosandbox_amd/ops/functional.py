@@ -1091,8 +1091,11 @@ def _lm_grad_out(w, gw, scratch):
 
 
 def _fused_xent_ok(M, C, Vp):
-    return (not _gd.DETERMINISTIC and M % 4 == 0 and _gemm.nt_supported(M, Vp, C) and _gemm.nt_supported(M, C, Vp)
-            and C <= 8192)
+    # deterministic mode too once the onehot dW term is the sorted form: every other piece
+    # writes each output once (row-sum slots, ordered combine, per-row fix-up) and the dW GEMM
+    # reduces its K splits in order there
+    return ((not _gd.DETERMINISTIC or XENT_FIX_SORTED) and M % 4 == 0 and _gemm.nt_supported(M, Vp, C)
+            and _gemm.nt_supported(M, C, Vp) and C <= 8192)
 
 
 # The fused cross-entropy for fp16 compute (default; NSA_XENT_F16=0 selects autocast's form:
@@ -1106,6 +1109,8 @@ def _fused_xent_ok(M, C, Vp):
 # 2.9e-4 at init-like logits, dW 1.4e-4 vs 1.2e-3 and dX 2.1e-4 vs 1.2e-3 at sharp ones
 # (scripts/debug/xent_f16_vs_autocast.py, profiles/r5_xent16_vs_autocast.log).
 XENT_F16 = os.environ.get("NSA_XENT_F16", "1") == "1"
+# the lm_head dW onehot term by target-sorted rows (segsum.h) instead of fp32 atomics
+XENT_FIX_SORTED = os.environ.get("NSA_XENT_FIX_SORTED", "1") == "1"
 
 
 def _xent_range(dtype):
@@ -1208,8 +1213,17 @@ class LMHeadLossFn(torch.autograd.Function):
             ret = gwp is None
             gw = torch.zeros(Vp, C, device=x2.device, dtype=F32) if ret else gwp
             _gd.wgrad_acc(e, xs, gw)
-            _lib.call(_sym("nsa_xent_dw_fix", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),
-                      _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(gw), C, N, C, _lib.stream())
+            if XENT_FIX_SORTED:
+                # the onehot term atomic-free: rows sorted by target, one writer per vocab row
+                ids, order = torch.sort(t32, stable=True)
+                seg = torch.searchsorted(ids, torch.arange(Vp + 1, device=x2.device, dtype=ids.dtype))
+                part = torch.empty(2 * (-(-N // 16)), C, device=x2.device, dtype=F32)
+                _lib.call(_sym("nsa_xent_dw_fix_sorted", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),
+                          _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(ids), _lib.ptr(order), _lib.ptr(seg),
+                          _lib.ptr(part), _lib.ptr(gw), C, N, C, Vp, _lib.stream())
+            else:
+                _lib.call(_sym("nsa_xent_dw_fix", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),
+                          _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(gw), C, N, C, _lib.stream())
             return dx.view(ctx.xshape), _lm_grad_out(w, gw, ret), None, None
         x2, w, dlogits, n_valid = ctx.saved_tensors
         g = (gl.float() / n_valid)

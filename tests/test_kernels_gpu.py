@@ -234,12 +234,12 @@ def test_embedding_bwd_sorted_chunks(kernels, monkeypatch, case):
 # ------------------------------------------------------------ cross-entropy
 @pytest.mark.parametrize("N,V,C,det", [(256, 50304, 128, False), (200, 65, 64, False),  # separate CE pass
                                        (1024, 50304, 768, False), (1024, 50257, 768, False),  # fused into the GEMMs
-                                       (520, 1000, 256, False), (1024, 50304, 768, True)])    # deterministic: separate
+                                       (520, 1000, 256, False), (1024, 50304, 768, True)])    # deterministic: fused, sorted
 def test_lm_head_loss(kernels, N, V, C, det):
     """Tied lm_head + cross-entropy (ignore_index=-1) vs fp32 F.cross_entropy: the fused path
     (E = exp(logit - target logit) from the GEMM epilogue, softmax normalisation and onehot
-    in the backward GEMMs), the padded-vocabulary path (50257 -> 50304 rows) and the
-    separate pass (small C, deterministic mode)."""
+    in the backward GEMMs; also in deterministic mode), the padded-vocabulary path (50257 ->
+    50304 rows) and the separate pass (small shapes)."""
     from nanosandbox_amd import ops
 
     torch.manual_seed(0)
@@ -260,6 +260,52 @@ def test_lm_head_loss(kernels, N, V, C, det):
     assert abs(loss.item() - lr.item()) < 2e-3 * max(1.0, abs(lr.item()))
     assert rel_err(x.grad, xr.grad) < 2e-2
     assert rel_err(w.main_grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,V,C,skew", [(16384, 65, 384, True), (4096, 50304, 768, False), (3000, 1000, 256, True)])
+def test_lm_head_dw_fix_sorted_matches_atomic(kernels, monkeypatch, N, V, C, skew):
+    """The fused cross-entropy's onehot dW term by target-sorted rows (segsum.h, the default)
+    against its fp32-atomic form: a character vocabulary with Zipf-skewed targets (long
+    segments: the chunked passes), GPT-2's uniform one (short segments: the row pass), ignored
+    rows; equal to fp32 rounding, and bitwise repeatable in deterministic mode (which now
+    keeps the fused path)."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+    torch.manual_seed(3)
+    x0 = torch.randn(N, C, device=DEV).to(BF)
+    w0 = torch.randn(V, C, device=DEV) * 0.05
+    if skew:
+        pz = 1.0 / torch.arange(1, V + 1, dtype=torch.float32) ** 1.2
+        t = torch.multinomial(pz, N, replacement=True).to(DEV)
+    else:
+        t = torch.randint(0, V, (N,), device=DEV)
+    t[5::11] = -1
+    out = []
+    for sorted_fix in (True, False):
+        monkeypatch.setattr(Fn, "XENT_FIX_SORTED", sorted_fix)
+        x = x0.clone().requires_grad_(True)
+        w = param(w0, fused=True)
+        ops.lm_head_loss(x, w, t).backward()
+        out.append(w.main_grad.clone())
+    # (the default dW GEMM adds its K splits with fp32 atomics: equal to rounding only)
+    assert rel_err(out[0], out[1]) < 1e-6
+    # deterministic mode keeps the fused path (sorted term, ordered split-K dW): bitwise repeatable
+    det = []
+    ops.set_deterministic(True)
+    try:
+        for _ in range(2):
+            monkeypatch.setattr(Fn, "XENT_FIX_SORTED", True)
+            x = x0.clone().requires_grad_(True)
+            w = param(w0, fused=True)
+            ops.lm_head_loss(x, w, t).backward()
+            det.append((w.main_grad.clone(), x.grad.clone()))
+    finally:
+        ops.set_deterministic(False)
+    assert torch.equal(det[0][0], det[1][0]) and torch.equal(det[0][1], det[1][1])
+    assert rel_err(det[0][0], out[1]) < 1e-6
+    wr = w.compute.float().requires_grad_(True)
+    F.cross_entropy(x0.float() @ wr.t(), t, ignore_index=-1).backward()
+    assert rel_err(out[0], wr.grad) < 2e-2
 
 
 def test_lm_head_loss_fused_precision(kernels):
