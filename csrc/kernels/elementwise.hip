@@ -298,6 +298,8 @@ NSA_API hipError_t nsa_rng_advance_emb_set(uint64_t v, hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_attn_set(uint64_t v, hipStream_t s);
 NSA_API hipError_t nsa_rng_advance_attn_h(hipStream_t s);  // the fp16 attention build's counter
 NSA_API hipError_t nsa_rng_advance_attn_h_set(uint64_t v, hipStream_t s);
+NSA_API hipError_t nsa_rng_advance_ln(hipStream_t s);  // the LayerNorm's fused branch dropout
+NSA_API hipError_t nsa_rng_advance_ln_set(uint64_t v, hipStream_t s);
 
 // set every translation unit's dropout step counter (start of a run)
 NSA_API hipError_t nsa_rng_set(uint64_t v, hipStream_t s) {
@@ -305,6 +307,7 @@ NSA_API hipError_t nsa_rng_set(uint64_t v, hipStream_t s) {
   if (e == hipSuccess) e = nsa_rng_advance_emb_set(v, s);
   if (e == hipSuccess) e = nsa_rng_advance_attn_set(v, s);
   if (e == hipSuccess) e = nsa_rng_advance_attn_h_set(v, s);
+  if (e == hipSuccess) e = nsa_rng_advance_ln_set(v, s);
   return e;
 }
 
@@ -314,6 +317,7 @@ NSA_API hipError_t nsa_rng_advance(hipStream_t s) {
   if (e == hipSuccess) e = nsa_rng_advance_emb(s);
   if (e == hipSuccess) e = nsa_rng_advance_attn(s);
   if (e == hipSuccess) e = nsa_rng_advance_attn_h(s);
+  if (e == hipSuccess) e = nsa_rng_advance_ln(s);
   return e;
 }
 

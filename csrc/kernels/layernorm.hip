@@ -189,11 +189,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
                                                     XT* __restrict__ sum_out, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                    int N, int C, float eps) {
+                                                    int N, int C, float eps, uint32_t dthresh = 0u,
+                                                    float dscale = 1.0f, uint64_t dsalt = 0ull) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
   const XT* xr = x + (int64_t)row * C;
+  const uint64_t dseed = dthresh ? nsa_seed(dsalt) : 0ull;
   float v[NK][8];
   float s = 0.0f;
 #pragma unroll
@@ -204,6 +206,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const XT* __restrict__ x, c
       if (res) {  // fused residual add: s = x + res, written out (XT) and normalised
         float rv[8];
         load8n<NT, H>(res + (int64_t)row * C + c, rv);
+        if (dthresh) {
+          // the branch's resid dropout, fused: the mask and the 16-bit rounding of
+          // nsa_dropout (elementwise.hip) for the same [N, C] element index, so the sum is
+          // bit for bit x + dropout(res)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = rv[j] * dscale;
+            asm volatile("" : "+v"(t));  // an fp32 product first, as nsa_dropout (no v_mad_mix)
+            rv[j] = nsa_keep(dseed, (uint64_t)row * C + c + j, dthresh) ? e2f<H>(f2e<H>(t)) : 0.0f;
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = as_stream(v[k][j] + rv[j], (XT*)nullptr);
         store8xn<NT>(sum_out + (int64_t)row * C + c, v[k]);
@@ -416,15 +429,20 @@ bool ln_nt() { return ln_nt_flag() != 0; }
 
 template <int NK, typename XT, bool H = false>
 hipError_t launch_fwd(const void* x, const void* res, void* sum_out, const void* w, const void* b, void* y,
-                      void* mean, void* rstd, int N, int C, float eps, hipStream_t s) {
+                      void* mean, void* rstd, int N, int C, float eps, hipStream_t s, float p = 0.0f,
+                      uint64_t salt = 0ull) {
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float dscale = p > 0.0f && p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
   if (ln_nt() && (int64_t)N * C * (int64_t)sizeof(XT) >= NSA_NT_MIN_BYTES)
     ln_fwd_kernel<NK, XT, true, H><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
                                                             (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
-                                                            (float*)mean, (float*)rstd, N, C, eps);
+                                                            (float*)mean, (float*)rstd, N, C, eps, th, dscale,
+                                                            salt);
   else
     ln_fwd_kernel<NK, XT, false, H><<<(N + 3) / 4, 256, 0, s>>>((const XT*)x, (const bf16_t*)res, (XT*)sum_out,
                                                              (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y,
-                                                             (float*)mean, (float*)rstd, N, C, eps);
+                                                             (float*)mean, (float*)rstd, N, C, eps, th, dscale,
+                                                             salt);
   return hipGetLastError();
 }
 
@@ -543,6 +561,27 @@ NSA_API hipError_t nsa_layernorm_bwd_x32s_h(const void* dy, const void* x, const
   NSA_NK_SWITCH((C + 511) / 512, (launch_bwd<K_, float, true>(dy, x, w, mean, rstd, dres, dx, dx_branch, dw_part,
                                                               db_part, N, C, nblk, s)));
 }
+
+// nsa_layernorm_fwd_x32 with the branch's dropout fused (res must be given): sum_out =
+// x + dropout_p(res) with nsa_dropout's mask for `seed` (the branch gradient takes the same
+// mask through nsa_dropout in the backward)
+NSA_API hipError_t nsa_layernorm_fwd_x32d(const void* x, const void* res, void* sum_out, const void* w, const void* b,
+                                          void* y, void* mean, void* rstd, int N, int C, float eps, float p,
+                                          uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0 || res == nullptr) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512,
+                (launch_fwd<K_, float>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s, p, seed)));
+}
+NSA_API hipError_t nsa_layernorm_fwd_x32d_h(const void* x, const void* res, void* sum_out, const void* w,
+                                            const void* b, void* y, void* mean, void* rstd, int N, int C, float eps,
+                                            float p, uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0 || res == nullptr) return hipErrorInvalidValue;
+  NSA_NK_SWITCH((C + 511) / 512,
+                (launch_fwd<K_, float, true>(x, res, sum_out, w, b, y, mean, rstd, N, C, eps, s, p, seed)));
+}
+
+// dropout step counter of this translation unit (nsa_rng_advance / nsa_rng_set bump all of them)
+NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_ln)
 
 // fp16 branch / weights / output with the fp32 stream (dtype float16)
 NSA_API hipError_t nsa_layernorm_fwd_x32_h(const void* x, const void* res, void* sum_out, const void* w, const void* b,

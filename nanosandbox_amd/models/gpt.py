@@ -68,11 +68,14 @@ class CausalSelfAttention(nn.Module):
         self.dropout = config.dropout
         self.flash = True  # always: our flash kernel (gfx950) / fp32 reference on CPU
 
-    def forward(self, x):
-        """resid_dropout(c_proj(attn(c_attn(x)))) — the residual add is fused downstream."""
+    def forward(self, x, resid_drop=True):
+        """resid_dropout(c_proj(attn(c_attn(x)))) — the residual add is fused downstream
+        (``resid_drop=False``: without the resid dropout, which the fused add + LayerNorm
+        then applies)."""
         qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)
         y = ops.attention(qkv, self.n_head, self.dropout, self.training)
-        return ops.dropout(ops.linear(y, self.c_proj.weight, self.c_proj.bias), self.dropout, self.training)
+        y = ops.linear(y, self.c_proj.weight, self.c_proj.bias)
+        return ops.dropout(y, self.dropout, self.training) if resid_drop else y
 
 
 class MLP(nn.Module):
@@ -82,9 +85,9 @@ class MLP(nn.Module):
         self.c_proj = nn.Linear(4 * config.n_embd, config.n_embd, bias=config.bias)
         self.dropout = config.dropout
 
-    def forward(self, x):
+    def forward(self, x, resid_drop=True):
         y = ops.mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
-        return ops.dropout(y, self.dropout, self.training)
+        return ops.dropout(y, self.dropout, self.training) if resid_drop else y
 
 
 class Block(nn.Module):
@@ -103,20 +106,27 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(config.n_embd, bias=config.bias)
         self.mlp = MLP(config)
 
+    def resid_p(self):
+        """nanoGPT's resid_dropout probability, applied by the fused add + LayerNorm."""
+        return self.mlp.dropout if self.training else 0.0
+
     def fused_forward(self, x, h, split_grad=False):
-        x, h2 = ops.add_layer_norm(x, self.attn(h), self.ln_2.weight, self.ln_2.bias, split_grad=split_grad)
-        return x, self.mlp(h2)
+        """(x + drop(attn(h)), mlp(ln_2(...))): the MLP branch returned un-added and without
+        its resid dropout (the caller's add_layer_norm applies ``resid_p``)."""
+        x, h2 = ops.add_layer_norm(x, self.attn(h, resid_drop=False), self.ln_2.weight, self.ln_2.bias,
+                                   split_grad=split_grad, drop_p=self.resid_p())
+        return x, self.mlp(h2, resid_drop=False)
 
     def forward(self, x):
         x, y = self.fused_forward(x, self.ln_1(x))
-        return x + y
+        return x + ops.dropout(y, self.mlp.dropout, self.training)
 
 
 def _block_step(block, next_ln, x, h):
     # the trunk's residual stream runs from one fused LayerNorm to the next with no other
     # reader, so its gradient may travel split (ops.add_layer_norm split_grad)
     x, y = block.fused_forward(x, h, split_grad=True)
-    return ops.add_layer_norm(x, y, next_ln.weight, next_ln.bias, split_grad=True)
+    return ops.add_layer_norm(x, y, next_ln.weight, next_ln.bias, split_grad=True, drop_p=block.resid_p())
 
 
 class GPT(nn.Module):

@@ -48,6 +48,8 @@ _SIGNATURES = {
                               c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "nsa_layernorm_bwd_x32s": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_layernorm_fwd_x32d": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_int, c_int, c_float, c_float, c_uint64, c_void_p],
     "nsa_layernorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_float, c_void_p],
     "nsa_layernorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -434,8 +434,11 @@ class LayerNormFn(torch.autograd.Function):
     (torch's cast: to even), the one difference, at elements whose low 16 bits are 0x8000."""
 
     @staticmethod
-    def forward(ctx, x, y, w, b, out_dtype, passthrough=False, split_grad=False):
+    def forward(ctx, x, y, w, b, out_dtype, passthrough=False, split_grad=False, drop_p=0.0):
         ctx.set_materialize_grads(False)
+        # the branch's resid dropout fused into the kernel (add_layer_norm routes only the
+        # fp32-stream kernel case here): sum = x + dropout(y), y's gradient masked alike
+        ctx.drop = (float(drop_p), new_seed()) if drop_p > 0 else None
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         N = x2.shape[0]
@@ -462,12 +465,19 @@ class LayerNormFn(torch.autograd.Function):
             rstd = torch.empty(N, device=x.device, dtype=F32)
             wc = compute_weight(w, out_dtype)
             bc = compute_weight(b, out_dtype) if b is not None else None
-            _lib.call(_sym("nsa_layernorm_fwd_x32", out_dtype) if x32 else "nsa_layernorm_fwd", _lib.ptr(x2),
-                      _lib.ptr(y2),
-                      _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C,
-                      LN_EPS, _lib.stream())
+            if ctx.drop is not None:
+                assert x32 and y2 is not None
+                _lib.call(_sym("nsa_layernorm_fwd_x32d", out_dtype), _lib.ptr(x2), _lib.ptr(y2), _lib.ptr(s2),
+                          _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N, C, LN_EPS,
+                          ctx.drop[0], ctx.drop[1], _lib.stream())
+            else:
+                _lib.call(_sym("nsa_layernorm_fwd_x32", out_dtype) if x32 else "nsa_layernorm_fwd", _lib.ptr(x2),
+                          _lib.ptr(y2),
+                          _lib.ptr(s2), _lib.ptr(wc), _lib.ptr(bc), _lib.ptr(h), _lib.ptr(mean), _lib.ptr(rstd), N,
+                          C, LN_EPS, _lib.stream())
             inp = s2 if y is not None else x2
         else:
+            assert ctx.drop is None, "fused branch dropout is a kernel path (add_layer_norm applies it otherwise)"
             xf = x2.float()
             if y is not None:
                 xf = xf + y.reshape(-1, C).float()
@@ -494,7 +504,7 @@ class LayerNormFn(torch.autograd.Function):
         else:
             ds, dh = None, grads[0]
         if dh is None and ds is None:  # no output reached the loss (grads are not materialised)
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x2, w, b_or_mean, mean, rstd = ctx.saved_tensors
         ds_split = _is_split(ds)
         if ds_split and (dh is None or not ctx.kern or x2.dtype != F32 or dh.dtype != ds._nsa_split):
@@ -505,7 +515,7 @@ class LayerNormFn(torch.autograd.Function):
         shape = (*(dh if dh is not None else ds).shape[:-1], C)
         if dh is None:  # only the residual output was used
             dyb = ds.to(ctx.y_dtype) if (ctx.fused and not ctx.passthrough) else None
-            return ds, dyb, None, None, None, None, None
+            return ds, _drop_grad(ctx, dyb), None, None, None, None, None, None
         dy2 = dh.reshape(-1, C)
         if ctx.kern:
             x32 = x2.dtype == F32
@@ -545,8 +555,8 @@ class LayerNormFn(torch.autograd.Function):
             if split_out:
                 dx._nsa_split = dy2.dtype
             if not ctx.fused or ctx.passthrough:
-                return dx, None, gw, gb, None, None, None
-            return dx, (dyb.view(shape) if dyb is not None else dx), gw, gb, None, None, None
+                return dx, None, gw, gb, None, None, None, None
+            return dx, _drop_grad(ctx, dyb.view(shape) if dyb is not None else dx), gw, gb, None, None, None, None
         xf = x2.float()
         d = dy2.float()
         xhat = (xf - mean[:, None]) * rstd[:, None]
@@ -559,8 +569,20 @@ class LayerNormFn(torch.autograd.Function):
         gb = _accumulate(b, d.sum(0)) if b is not None else None
         dxs = dx.to(x2.dtype).view(shape)
         if not ctx.fused or ctx.passthrough:
-            return dxs, None, gw, gb, None, None, None
-        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None, None, None
+            return dxs, None, gw, gb, None, None, None, None
+        return dxs, dx.to(ctx.y_dtype).view(shape), gw, gb, None, None, None, None
+
+
+def _drop_grad(ctx, g):
+    """The branch gradient through the fused resid dropout: nsa_dropout's mask for the
+    forward's seed (a new tensor: with split planes g is a view of the residual gradient)."""
+    if ctx.drop is None or g is None:
+        return g
+    out = torch.empty_like(g)
+    gc = g.contiguous()
+    _lib.call(_sym("nsa_dropout", g.dtype), _lib.ptr(gc), _lib.ptr(out), g.numel(), ctx.drop[0], ctx.drop[1],
+              _lib.stream())
+    return out
 
 
 def _colsum_into(p, partial):
@@ -590,14 +612,25 @@ def layer_norm_pass(x, w, b, out_dtype=None):
     return LayerNormFn.apply(x, None, w, b, out_dtype, True)
 
 
-def add_layer_norm(x, y, w, b, out_dtype=None, split_grad=False):
+# NSA_LN_DROPOUT=0: the branch's resid dropout as its own pass before the fused add + LN
+LN_DROPOUT = os.environ.get("NSA_LN_DROPOUT", "1") != "0"
+
+
+def add_layer_norm(x, y, w, b, out_dtype=None, split_grad=False, drop_p=0.0):
     """Fused residual add + LayerNorm: returns (x + y, LN(x + y)).
 
     x + y keeps x's (residual-stream) dtype; LN(x + y) is in ``out_dtype``
     (default y's dtype, the compute dtype).  ``split_grad``: x is the residual output of
     another ``add_layer_norm`` / ``layer_norm_pass`` and nothing else reads it, so x's
-    gradient may travel in the split-plane encoding (see LayerNormFn)."""
-    return LayerNormFn.apply(x, y, w, b, out_dtype, False, split_grad)
+    gradient may travel in the split-plane encoding (see LayerNormFn).  ``drop_p``: the
+    branch's resid dropout (nanoGPT ``resid_dropout``), x + dropout(y): fused into the
+    LayerNorm kernel on the fp32-stream kernel path (the same mask and rounding as
+    ``dropout``), a separate ``dropout`` elsewhere."""
+    if drop_p > 0:
+        od = out_dtype or y.dtype
+        if not (LN_DROPOUT and x.is_cuda and x.dtype == F32 and od in KDT and y.dtype == od):
+            return LayerNormFn.apply(x, dropout(y, drop_p, True), w, b, out_dtype, False, split_grad)
+    return LayerNormFn.apply(x, y, w, b, out_dtype, False, split_grad, drop_p)
 
 
 # ----------------------------------------------------------------------------

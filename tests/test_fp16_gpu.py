@@ -454,3 +454,31 @@ def test_gpt_fp16_split_residual_grad_matches_plain(kernels):
         assert torch.equal(grads[0][n], grads[2][n]), n
         ref = grads[1][n]
         assert ((grads[0][n] - ref).abs() <= 2 ** -20 * ref.abs().max() + 1e-12).all(), n
+
+
+def test_add_layernorm_fused_dropout_fp16(kernels):
+    """fp16 compute: the resid dropout fused into the add + LayerNorm kernel matches
+    dropout() then the plain kernel bit for bit (mask, fp16 rounding of the scaled branch)."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+    N, C, p = 300, 768, 0.1
+    torch.manual_seed(0)
+    x0 = torch.randn(N, C, device=DEV)
+    y0 = torch.randn(N, C, device=DEV).to(H16)
+    w = torch.nn.Parameter(torch.randn(C, device=DEV) * 0.5 + 1)
+    w.compute = w.detach().to(H16)
+    dh = torch.randn(N, C, device=DEV).to(H16)
+    out = []
+    for fused in (True, False):
+        Fn.LN_DROPOUT = fused
+        try:
+            x = x0.clone().requires_grad_(True)
+            y = y0.clone().requires_grad_(True)
+            torch.manual_seed(7)
+            s, h = ops.add_layer_norm(x, y, w, None, drop_p=p)
+            h.backward(dh)
+            out.append((s.detach().clone(), h.detach().clone(), x.grad.clone(), y.grad.clone()))
+        finally:
+            Fn.LN_DROPOUT = True
+    for a, bb, name in zip(out[0], out[1], ("s", "h", "dx", "dy")):
+        assert torch.equal(a, bb), name

@@ -1176,3 +1176,68 @@ def test_nt_strip_dispatch(kernels, monkeypatch, N):
     assert rel_err(y, ref) < 1e-2
     # same fp32 accumulation order per element up to the K-step grouping: within an ulp
     assert ((y.float() - full.float()).abs() <= 2 ** -7 * full.float().abs() + 1e-3).all()
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_add_layernorm_fused_dropout(kernels, split):
+    """The branch's resid dropout fused into the add + LayerNorm kernel against dropout() and
+    then the plain fused add + LayerNorm, same seed: the sum and the normalised output bit for
+    bit, the residual and branch gradients bit for bit (split-plane and plain forms)."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.ops import functional as Fn
+    N, C, p = 512, 384, 0.2
+    torch.manual_seed(0)
+    x0 = torch.randn(N, C, device=DEV)
+    y0 = torch.randn(N, C, device=DEV).to(BF)
+    w = param(torch.randn(C, device=DEV) * 0.5 + 1)
+    b = param(torch.randn(C, device=DEV) * 0.1)
+    dh = torch.randn(N, C, device=DEV).to(BF)
+    ds = torch.randn(N, C, device=DEV) * 0.1
+    out = []
+    for fused in (True, False):
+        Fn.LN_DROPOUT = fused
+        try:
+            x = x0.clone().requires_grad_(True)
+            y = y0.clone().requires_grad_(True)
+            torch.manual_seed(7)
+            s, h = ops.add_layer_norm(x, y, w, b, split_grad=split, drop_p=p)
+            torch.autograd.backward([s, h], [ds, dh])
+            # (a leaf x receives the split-plane encoding as it is: compare bits, not floats)
+            out.append((s.detach().clone(), h.detach().clone(), x.grad.view(torch.int32).clone(), y.grad.clone()))
+        finally:
+            Fn.LN_DROPOUT = True
+    for a, bb, name in zip(out[0], out[1], ("s", "h", "dx", "dy")):
+        assert torch.equal(a, bb), name
+    kept = (out[0][0] != x0)  # dropped branch elements leave s == x exactly
+    frac = 1.0 - kept.float().mean().item()
+    assert abs(frac - p) < 0.02
+
+
+def test_gpt_fused_resid_dropout_matches_separate(kernels):
+    """A dropout-0.2 GPT (the shakespeare_char shape) with the resid dropout fused into the add
+    + LayerNorm kernels against separate dropout passes, deterministic mode: the same masks
+    (same seed draws in the same order), so the loss and every gradient agree bit for bit."""
+    from nanosandbox_amd.models.gpt import GPT, GPTConfig
+    from nanosandbox_amd.ops import functional as Fn
+    torch.manual_seed(2)
+    cfg = GPTConfig(block_size=256, vocab_size=65, n_layer=2, n_head=6, n_embd=384, dropout=0.2, bias=False)
+    model = GPT(cfg).to(DEV).set_compute_dtype(BF)
+    model.train()
+    idx = torch.randint(0, 65, (8, 256), device=DEV)
+    tgt = torch.randint(0, 65, (8, 256), device=DEV)
+    prev = (Fn.LN_DROPOUT, Fn._gd.DETERMINISTIC)
+    res = []
+    try:
+        Fn.set_deterministic(True)
+        for fused in (True, False):
+            Fn.LN_DROPOUT = fused
+            model.zero_grad(set_to_none=True)
+            torch.manual_seed(11)
+            _, loss = model(idx, tgt)
+            loss.backward()
+            res.append((loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()}))
+    finally:
+        Fn.LN_DROPOUT, Fn._gd.DETERMINISTIC = prev
+    assert res[0][0] == res[1][0]
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
