@@ -1241,3 +1241,35 @@ def test_gpt_fused_resid_dropout_matches_separate(kernels):
     assert res[0][0] == res[1][0]
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+def test_gpt_dropout_under_activation_checkpointing(kernels):
+    """Dropout 0.2 (attention, fused resid dropout, embedding) with activation checkpointing
+    against the resident forward, deterministic mode: the recomputed blocks draw the same
+    seeds (checkpoint restores the generator) and the device counter is not advanced inside
+    a micro-step, so loss and gradients agree bit for bit."""
+    from nanosandbox_amd.models.gpt import GPT, GPTConfig
+    from nanosandbox_amd.ops import functional as Fn
+    torch.manual_seed(4)
+    cfg = GPTConfig(block_size=256, vocab_size=65, n_layer=3, n_head=6, n_embd=384, dropout=0.2, bias=True)
+    model = GPT(cfg).to(DEV).set_compute_dtype(BF)
+    model.train()
+    idx = torch.randint(0, 65, (4, 256), device=DEV)
+    tgt = torch.randint(0, 65, (4, 256), device=DEV)
+    prev = Fn._gd.DETERMINISTIC
+    res = []
+    try:
+        Fn.set_deterministic(True)
+        for ckpt in (False, True):
+            model.grad_ckpt = ckpt
+            model.zero_grad(set_to_none=True)
+            torch.manual_seed(9)
+            _, loss = model(idx, tgt)
+            loss.backward()
+            res.append((loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()}))
+    finally:
+        Fn._gd.DETERMINISTIC = prev
+        model.grad_ckpt = False
+    assert res[0][0] == res[1][0]
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
