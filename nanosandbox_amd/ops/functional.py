@@ -284,9 +284,9 @@ class EmbeddingFn(torch.autograd.Function):
                 # atomic-free: token positions stably sorted by id, one writer per vocab row
                 # segment starts by binary search over the sorted ids: no host sync
                 # (torch.bincount reads its max back to the host, which HIP-graph
-                # capture forbids).  Also the faster form at training sizes: B120 T1024
-                # C768, wte + wpe grads 281.7 vs 390.3 us with fp32 atomics
-                # (scripts/emb_bwd_ab.py), and deterministic for free.
+                # capture forbids).  Also the faster form from ~64K tokens: B120 T1024
+                # C768, wte + wpe grads 313.6 vs 369.5 us with fp32 atomics
+                # (scripts/emb_bwd_ab.py, profiles/r5_emb_bwd.md), and deterministic for free.
                 flat = idx.view(-1)
                 ids, order = torch.sort(flat, stable=True)
                 seg = torch.searchsorted(ids, torch.arange(V + 1, device=dx.device, dtype=ids.dtype))
