@@ -200,6 +200,21 @@ hipError_t launch_bwd_det(const void* ids, const void* order, const void* seg, v
 
 }  // namespace
 
+template <typename XT>
+hipError_t launch_bwd_lds(const void* idx, const void* dx, void* dwte, void* dwpe, void* part, int B, int T, int C,
+                          int V, float p, uint64_t seed, hipStream_t s) {
+  if (C % 8 != 0) return hipErrorInvalidValue;
+  const uint32_t th = p > 0.0f ? nsa_drop_thresh(p) : 0u;
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  const EmbRow<XT> f{(const XT*)dx, C, th, scale, seed};
+  hipError_t e = seg_scatter_add_lds<int64_t, EmbRow<XT>>((const int64_t*)idx, f, (float*)part, (float*)dwte, C, B * T,
+                                                           V, C, s);
+  if (e != hipSuccess) return e;
+  const int work = T * (C / 8);
+  emb_bwd_wpe_kernel<XT><<<(work + 255) / 256, 256, 0, s>>>((const XT*)dx, (float*)dwpe, B, T, C, th, scale, seed);
+  return hipGetLastError();
+}
+
 // idx: dense int64 [B*T] (callers pass a contiguous tensor); out / dx: bf16
 NSA_DEFINE_RNG_ADVANCE(nsa_rng_advance_emb)
 
@@ -237,3 +252,15 @@ NSA_API hipError_t nsa_embedding_bwd_det(const void* ids, const void* order, con
   if (dx_fp32) return launch_bwd_det<float>(ids, order, seg, part, dx, dwte, dwpe, B, T, C, V, p, seed, s);
   return launch_bwd_det<bf16_t>(ids, order, seg, part, dx, dwte, dwpe, B, T, C, V, p, seed, s);
 }
+
+// small vocabularies (V x C fp32 <= 128 KB): the LDS-privatised scatter-add (segsum.h), not
+// per-row global atomics on a few hot rows; arrival order (not the deterministic mode's path)
+// part: nsa_seg_lds_parts(B * T) x V x C floats of scratch
+NSA_API hipError_t nsa_embedding_bwd_lds(const void* idx, const void* dx, void* dwte, void* dwpe, void* part, int B,
+                                         int T, int C, int V, int dx_fp32, float p, uint64_t seed, hipStream_t s) {
+  if (dx_fp32) return launch_bwd_lds<float>(idx, dx, dwte, dwpe, part, B, T, C, V, p, seed, s);
+  return launch_bwd_lds<bf16_t>(idx, dx, dwte, dwpe, part, B, T, C, V, p, seed, s);
+}
+
+// partial tables the LDS scatter-add over N rows writes (segsum.h seg_lds_parts)
+NSA_API int nsa_seg_lds_parts(int N) { return seg_lds_parts(N); }

@@ -158,6 +158,123 @@ __global__ __launch_bounds__(256) void seg_fix_kernel(const IT* __restrict__ ids
   }
 }
 
+// Small destination tables (V x C fp32 fits the LDS, e.g. a character vocabulary): each
+// workgroup adds its rows into an LDS copy of the table (ds_add_f32) and stores the copy as
+// its partial table (part[blockIdx]); seg_lds_reduce_kernel adds the partials into `out` in
+// workgroup order.  Unsorted ids (negative or >= V = skip); the LDS adds land in arrival
+// order, so not bitwise reproducible (the sorted passes above are).  Against per-row global
+// atomics on a 65-row table (every token hitting the same few rows: the chip serialises on
+// them) this moves the contention into the LDS.  The table is padded by one dword per 8
+// columns: a lane adds 8 consecutive columns, so unpadded lanes l and l + 4 of a 32-lane
+// group hit one bank (8-way conflicts); at stride 9 the 32 lanes take 32 banks.  The table
+// takes most of a CU's LDS (one workgroup per CU), so the rows are spread over every CU.
+// Measured at the char shape (16384 rows, 65 x 384): one global atomic per table element to
+// flush, 128 workgroups x 4 waves, unpadded: 80 us; partial tables, 64 x 16 waves: 130 us.
+constexpr int kSegLdsThreads = 256;
+constexpr int kSegLdsRows = 64;  // rows per workgroup (16 per wave)
+
+__device__ __forceinline__ int seg_lds_pad(int c) { return c + (c >> 3); }
+
+template <typename IT, class F>
+__global__ __launch_bounds__(kSegLdsThreads) void seg_lds_kernel(const IT* __restrict__ ids, F f,
+                                                                 float* __restrict__ part, int N, int V, int C) {
+  extern __shared__ __attribute__((aligned(16))) float tab[];  // [V][C + C / 8]
+  const int Cp = C + (C >> 3);
+  for (int i = threadIdx.x; i < V * Cp; i += kSegLdsThreads) tab[i] = 0.0f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  constexpr int kW = kSegLdsThreads / 64;
+  const int stride = gridDim.x * kW;
+  for (int r0 = blockIdx.x * kW + (threadIdx.x >> 6); r0 < N; r0 += 4 * stride) {
+    int64_t rw[4], id[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rw[u] = r0 + (int64_t)u * stride;
+      id[u] = rw[u] < N ? (int64_t)ids[rw[u]] : -1;
+    }
+    for (int c = lane * 8; c < C; c += 512) {
+      float x[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (id[u] >= 0 && id[u] < V) f.load(rw[u], id[u], c, x[u]);
+      const int pc = seg_lds_pad(c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (id[u] >= 0 && id[u] < V) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(&tab[id[u] * Cp + pc + j], x[u][j]);
+        }
+    }
+  }
+  __syncthreads();
+  float* pp = part + (int64_t)blockIdx.x * V * C;
+  for (int i = threadIdx.x; i < V * C; i += kSegLdsThreads) {
+    const int v = i / C, c = i - v * C;
+    pp[i] = tab[v * Cp + seg_lds_pad(c)];
+  }
+}
+
+// out[i / C][i % C] += sum over g < G of part[g][i], g in order; 4 waves per workgroup split
+// the G partials of 256 consecutive elements (a float4 per lane) and combine through LDS
+__global__ __launch_bounds__(256) void seg_lds_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                             int ldo, int G, int VC, int C) {
+  __shared__ float4 red[3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = (blockIdx.x * 64 + lane) * 4;
+  float4 a{0.f, 0.f, 0.f, 0.f};
+  if (i < VC) {
+    int g = w;
+    for (; g + 12 < G; g += 16) {  // 4 loads in flight per lane
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (int64_t)(g + 4 * u) * VC + i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+    for (; g < G; g += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)g * VC + i);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  if (w > 0) red[w - 1][lane] = a;
+  __syncthreads();
+  if (w == 0 && i < VC) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      a.x += red[u][lane].x; a.y += red[u][lane].y; a.z += red[u][lane].z; a.w += red[u][lane].w;
+    }
+    float* o = out + (int64_t)(i / C) * ldo + i % C;  // C % 4 == 0: the 4 stay in one row
+    o[0] += a.x; o[1] += a.y; o[2] += a.z; o[3] += a.w;
+  }
+}
+
+constexpr int kSegLdsBytes = 128 * 1024;  // LDS table budget of seg_lds_kernel (padded V x C fp32)
+
+// part: G x V x C floats (16-byte aligned), G = seg_lds_parts(N)
+inline int seg_lds_parts(int N) {
+  const int g = (N + kSegLdsRows - 1) / kSegLdsRows;
+  return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
+template <typename IT, class F>
+hipError_t seg_scatter_add_lds(const IT* ids, F f, float* part, float* out, int ldo, int N, int V, int C,
+                               hipStream_t s) {
+  if (C % 8 != 0 || (size_t)V * (C + C / 8) * 4 > (size_t)kSegLdsBytes || (uintptr_t)part % 16)
+    return hipErrorInvalidValue;
+  const int G = seg_lds_parts(N);
+  static bool attr = [] {  // dynamic LDS above 64 KB (one workgroup per CU)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&seg_lds_kernel<IT, F>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kSegLdsBytes) == hipSuccess;
+  }();
+  if (!attr) return hipErrorInvalidValue;
+  seg_lds_kernel<IT, F><<<G, kSegLdsThreads, (size_t)V * (C + C / 8) * 4, s>>>(ids, f, part, N, V, C);
+  const int VC = V * C;
+  seg_lds_reduce_kernel<<<(VC / 4 + 63) / 64, 256, 0, s>>>(part, out, ldo, G, VC, C);
+  return hipGetLastError();
+}
+
 // the three passes; part: 2 * ceil(N / kSegChunk) rows of C floats
 template <typename IT, class F>
 hipError_t seg_scatter_add(const IT* ids, const int64_t* order, const int64_t* seg, float* part, F f, float* out,

@@ -279,6 +279,25 @@ hipError_t dw_fix_sorted_entry(const void* x, int ldx, const void* E, int lde, c
 }
 }  // namespace
 
+// the onehot dW term for a small vocabulary (V x C fp32 <= 128 KB): LDS-privatised
+// scatter-add over the unsorted targets (segsum.h seg_lds_kernel)
+NSA_API hipError_t nsa_xent_dw_fix_lds(const void* x, int ldx, const void* E, int lde, const void* t32,
+                                       const void* invS, const void* gsc, void* part, void* gW, int ldg, int M, int C, int V,
+                                       hipStream_t s) {
+  if (C % 8 || ldx % 8) return hipErrorInvalidValue;
+  const XentFixRow<false> f{(const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32, (const float*)invS,
+                            (const float*)gsc};
+  return seg_scatter_add_lds<int, XentFixRow<false>>((const int*)t32, f, (float*)part, (float*)gW, ldg, M, V, C, s);
+}
+NSA_API hipError_t nsa_xent_dw_fix_lds_h(const void* x, int ldx, const void* E, int lde, const void* t32,
+                                         const void* invS, const void* gsc, void* part, void* gW, int ldg, int M, int C, int V,
+                                         hipStream_t s) {
+  if (C % 8 || ldx % 8) return hipErrorInvalidValue;
+  const XentFixRow<true> f{(const bf16_t*)x, ldx, (const bf16_t*)E, lde, (const int*)t32, (const float*)invS,
+                           (const float*)gsc};
+  return seg_scatter_add_lds<int, XentFixRow<true>>((const int*)t32, f, (float*)part, (float*)gW, ldg, M, V, C, s);
+}
+
 // the onehot dW term, atomic-free: ids = t32 stably sorted (int32), order = their rows,
 // seg[V + 1] = segment starts, part = [2 * ceil(M / 16), C] fp32 workspace (segsum.h)
 NSA_API hipError_t nsa_xent_dw_fix_sorted(const void* x, int ldx, const void* E, int lde, const void* t32,

@@ -119,6 +119,11 @@ _SIGNATURES = {
                         c_void_p],
     "nsa_xent_dw_fix_sorted": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "nsa_embedding_bwd_lds": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                              c_float, c_uint64, c_void_p],
+    "nsa_seg_lds_parts": [c_int],
+    "nsa_xent_dw_fix_lds": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_int, c_int, c_int, c_int, c_void_p],
     "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "nsa_gemm_strip": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
 }

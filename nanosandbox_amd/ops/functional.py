@@ -280,7 +280,13 @@ class EmbeddingFn(torch.autograd.Function):
             if ret_wpe:
                 gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
             assert dx.dtype in (F32, BF16)
-            if _gd.DETERMINISTIC or B * T >= _EMB_SORTED_MIN_TOKENS:
+            if not _gd.DETERMINISTIC and V * (C + C // 8) * 4 <= _SEG_LDS_BYTES:
+                # a small vocabulary (a character corpus): the LDS-privatised scatter-add
+                # (csrc/kernels/segsum.h); per-row global atomics pile onto a few hot rows
+                part = _seg_lds_part(B * T, V, C, dx.device)
+                _lib.call("nsa_embedding_bwd_lds", _lib.ptr(idx), _lib.ptr(dx), _lib.ptr(gwte), _lib.ptr(gwpe),
+                          _lib.ptr(part), B, T, C, V, 1 if dx.dtype == F32 else 0, ctx.p, ctx.seed, _lib.stream())
+            elif _gd.DETERMINISTIC or B * T >= _EMB_SORTED_MIN_TOKENS:
                 # atomic-free: token positions stably sorted by id, one writer per vocab row
                 # segment starts by binary search over the sorted ids: no host sync
                 # (torch.bincount reads its max back to the host, which HIP-graph
@@ -320,6 +326,12 @@ class EmbeddingFn(torch.autograd.Function):
 # the sorted kernels (scripts/emb_bwd_ab.py: 16K tokens 55.5 vs 96.2 us, GPT-2 122880
 # tokens 369.5 vs 313.6 us, profiles/r5_emb_bwd.md) -> crossover near 64K tokens
 _EMB_SORTED_MIN_TOKENS = 65536
+_SEG_LDS_BYTES = 128 * 1024  # segsum.h kSegLdsBytes: the padded V x (C + C/8) fp32 table of the LDS scatter-add
+
+
+def _seg_lds_part(n_rows, V, C, device):
+    """Scratch of the LDS scatter-add: one V x C fp32 partial table per workgroup."""
+    return torch.empty(_lib.call_ret("nsa_seg_lds_parts", n_rows), V * C, device=device, dtype=F32)
 
 
 def embedding(idx, wte, wpe, p: float, training: bool, dtype=F32, cdtype=None):
@@ -1246,7 +1258,12 @@ class LMHeadLossFn(torch.autograd.Function):
             ret = gwp is None
             gw = torch.zeros(Vp, C, device=x2.device, dtype=F32) if ret else gwp
             _gd.wgrad_acc(e, xs, gw)
-            if XENT_FIX_SORTED:
+            if not _gd.DETERMINISTIC and V * (C + C // 8) * 4 <= _SEG_LDS_BYTES:
+                # a small vocabulary: the LDS-privatised scatter-add over the targets
+                part = _seg_lds_part(N, V, C, x2.device)
+                _lib.call(_sym("nsa_xent_dw_fix_lds", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),
+                          _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(part), _lib.ptr(gw), C, N, C, V, _lib.stream())
+            elif XENT_FIX_SORTED:
                 # the onehot term atomic-free: rows sorted by target, one writer per vocab row
                 ids, order = torch.sort(t32, stable=True)
                 seg = torch.searchsorted(ids, torch.arange(Vp + 1, device=x2.device, dtype=ids.dtype))

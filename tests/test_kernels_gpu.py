@@ -140,15 +140,19 @@ def test_gelu(kernels, n):
 
 
 # --------------------------------------------------------------- embedding
-@pytest.mark.parametrize("B,T,V,C,sorted_bwd", [(4, 128, 1000, 768, False), (3, 77, 65, 384, False),
-                                                (8, 1024, 50304, 768, True), (4, 1024, 65, 384, True),
-                                                (4, 1024, 65, 384, False)])
-def test_embedding(kernels, monkeypatch, B, T, V, C, sorted_bwd):
+@pytest.mark.parametrize("B,T,V,C,path", [(4, 128, 1000, 768, "atomic"), (3, 77, 65, 384, "atomic"),
+                                          (8, 1024, 50304, 768, "sorted"), (4, 1024, 65, 384, "sorted"),
+                                          (4, 1024, 65, 384, "atomic"), (3, 77, 65, 384, "lds"),
+                                          (4, 1024, 65, 384, "lds"), (80, 1024, 65, 384, "lds")])
+def test_embedding(kernels, monkeypatch, B, T, V, C, path):
     from nanosandbox_amd import ops
     from nanosandbox_amd.ops import functional as Fn
 
-    # the sorted (atomic-free) backward runs from _EMB_SORTED_MIN_TOKENS tokens up
-    monkeypatch.setattr(Fn, "_EMB_SORTED_MIN_TOKENS", 0 if sorted_bwd else 1 << 40)
+    # the sorted (atomic-free) backward runs from _EMB_SORTED_MIN_TOKENS tokens up; a table
+    # that fits the LDS takes the LDS-privatised scatter-add first
+    monkeypatch.setattr(Fn, "_EMB_SORTED_MIN_TOKENS", 0 if path == "sorted" else 1 << 40)
+    if path != "lds":
+        monkeypatch.setattr(Fn, "_SEG_LDS_BYTES", 0)
 
     torch.manual_seed(0)
     idx = torch.randint(0, V, (B, T), device=DEV)
@@ -203,6 +207,7 @@ def test_embedding_bwd_sorted_chunks(kernels, monkeypatch, case):
     from nanosandbox_amd.ops import functional as Fn
 
     monkeypatch.setattr(Fn, "_EMB_SORTED_MIN_TOKENS", 0)
+    monkeypatch.setattr(Fn, "_SEG_LDS_BYTES", 0)  # the sorted passes, not the LDS table
     B, T, V, C, p = {"char_skew": (64, 256, 56, 384, 0.2), "one_id": (4, 1024, 65, 128, 0.0),
                      "ragged": (5, 999, 300, 64, 0.0), "wide": (8, 512, 1000, 1600, 0.0)}[case]
     torch.manual_seed(2)
@@ -281,14 +286,18 @@ def test_lm_head_dw_fix_sorted_matches_atomic(kernels, monkeypatch, N, V, C, ske
         t = torch.randint(0, V, (N,), device=DEV)
     t[5::11] = -1
     out = []
-    for sorted_fix in (True, False):
+    lds_bytes = Fn._SEG_LDS_BYTES
+    for sorted_fix, lds in ((True, False), (False, False), (True, True)):
         monkeypatch.setattr(Fn, "XENT_FIX_SORTED", sorted_fix)
+        monkeypatch.setattr(Fn, "_SEG_LDS_BYTES", lds_bytes if lds else 0)  # small V: the LDS table
         x = x0.clone().requires_grad_(True)
         w = param(w0, fused=True)
         ops.lm_head_loss(x, w, t).backward()
         out.append(w.main_grad.clone())
+    monkeypatch.setattr(Fn, "_SEG_LDS_BYTES", lds_bytes)
     # (the default dW GEMM adds its K splits with fp32 atomics: equal to rounding only)
     assert rel_err(out[0], out[1]) < 1e-6
+    assert rel_err(out[2], out[1]) < 1e-6
     # deterministic mode keeps the fused path (sorted term, ordered split-K dW): bitwise repeatable
     det = []
     ops.set_deterministic(True)
