@@ -280,7 +280,7 @@ class EmbeddingFn(torch.autograd.Function):
             if ret_wpe:
                 gwpe = torch.zeros(wpe.shape[0], C, device=dx.device, dtype=F32)
             assert dx.dtype in (F32, BF16)
-            if not _gd.DETERMINISTIC and V * (C + C // 8) * 4 <= _SEG_LDS_BYTES:
+            if not _gd.DETERMINISTIC and _seg_lds_fits(V, C):
                 # a small vocabulary (a character corpus): the LDS-privatised scatter-add
                 # (csrc/kernels/segsum.h); per-row global atomics pile onto a few hot rows
                 part = _seg_lds_part(B * T, V, C, dx.device)
@@ -327,6 +327,11 @@ class EmbeddingFn(torch.autograd.Function):
 # tokens 369.5 vs 313.6 us, profiles/r5_emb_bwd.md) -> crossover near 64K tokens
 _EMB_SORTED_MIN_TOKENS = 65536
 _SEG_LDS_BYTES = 128 * 1024  # segsum.h kSegLdsBytes: the padded V x (C + C/8) fp32 table of the LDS scatter-add
+
+
+def _seg_lds_fits(V, C):
+    """The LDS scatter-add's rule: the padded V x (C + C/8) fp32 table fits its LDS budget."""
+    return C % 8 == 0 and V * (C + C // 8) * 4 <= _SEG_LDS_BYTES
 
 
 def _seg_lds_part(n_rows, V, C, device):
@@ -1258,7 +1263,7 @@ class LMHeadLossFn(torch.autograd.Function):
             ret = gwp is None
             gw = torch.zeros(Vp, C, device=x2.device, dtype=F32) if ret else gwp
             _gd.wgrad_acc(e, xs, gw)
-            if not _gd.DETERMINISTIC and V * (C + C // 8) * 4 <= _SEG_LDS_BYTES:
+            if not _gd.DETERMINISTIC and _seg_lds_fits(V, C):
                 # a small vocabulary: the LDS-privatised scatter-add over the targets
                 part = _seg_lds_part(N, V, C, x2.device)
                 _lib.call(_sym("nsa_xent_dw_fix_lds", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),

@@ -70,6 +70,17 @@ def test_strip_split_rule():
         assert gemm.strip_split_n(n) == 0, n
 
 
+def test_small_vocab_lds_scatter_rule():
+    """The LDS-privatised scatter-add (segsum.h seg_lds_kernel) takes a table whose padded
+    V x (C + C/8) fp32 copy fits its 128 KB LDS budget: the char config's 65 x 384 (and the
+    reference's companion-notebook char model, 65 x 128), never a GPT-2 vocabulary."""
+    from nanosandbox_amd.ops import functional as Fn
+
+    fits = Fn._seg_lds_fits
+    assert fits(65, 384) and fits(65, 128)
+    assert not fits(50304, 768) and not fits(50257, 1600) and not fits(1000, 384)
+
+
 def test_wgrad_split_rule_matches_round3_race():
     """The fixed split rule reproduces the start-up race's picks (profiles/r3_bench_glds.log,
     r3_bench_gpt2_medium.log) and fills its last round of CUs."""
