@@ -14,7 +14,11 @@
 #   RDZV_BACKEND    static (MASTER_ADDR/PORT + node_rank) | c10d         [static]
 #   RDZV_ID         c10d job id                                        [disttrain]
 #   MAX_RESTARTS    torchrun --max-restarts (elastic recovery)         [0]
-#   NSA_RCCL_PRESET xgmi (single node, P2P) | socket (pods without shared IPC)
+#   NSA_RCCL_PRESET xgmi (single node, P2P) | xgmi-pods (one GPU per pod, every GPU of
+#                   the node mounted: P2P) | shm | socket (pods without shared IPC)
+#   NSA_DEVICE_SELECT ordinal: this pod's GPU is NODE_RANK mod NSA_GPUS_PER_NODE
+#                   (exported as NSA_LOCAL_DEVICE, read by init_distributed) instead of
+#                   LOCAL_RANK; for pods that see every GPU of the node (xgmi-pods)
 #   NSA_DRY_RUN=1   print the torchrun command instead of running it
 # Arguments: the training command after torchrun, e.g. train.py config/x.py --k=v
 set -euo pipefail
@@ -59,13 +63,23 @@ case "${NSA_RCCL_PRESET:-xgmi}" in
     export NCCL_IB_DISABLE="${NCCL_IB_DISABLE:-1}"
     export NCCL_SOCKET_IFNAME="${NCCL_SOCKET_IFNAME:-eth0}"
     ;;
-  shm)
+  shm|xgmi-pods)
     export NCCL_SHM_DISABLE="${NCCL_SHM_DISABLE:-0}"
     if [[ -z "${NCCL_HOSTID:-}" ]]; then
-      echo "entrypoint: WARNING NSA_RCCL_PRESET=shm without NCCL_HOSTID: RCCL will see each pod as its own host (NET transport)" >&2
+      echo "entrypoint: WARNING NSA_RCCL_PRESET=${NSA_RCCL_PRESET} without NCCL_HOSTID: RCCL will see each pod as its own host (NET transport)" >&2
     fi
     ;;
 esac
+# the pod's GPU by ordinal (Topology B over xGMI: every pod sees all GPUs of the node)
+if [[ "${NSA_DEVICE_SELECT:-}" == "ordinal" ]]; then
+  gpn="${NSA_GPUS_PER_NODE:-8}"
+  if (( NPROC_PER_NODE != 1 )); then
+    echo "entrypoint: NSA_DEVICE_SELECT=ordinal needs NPROC_PER_NODE=1 (got $NPROC_PER_NODE)" >&2
+    exit 2
+  fi
+  export NSA_LOCAL_DEVICE=$(( NODE_RANK % gpn ))
+  echo "entrypoint: device by ordinal: NSA_LOCAL_DEVICE=${NSA_LOCAL_DEVICE} (of ${gpn})" >&2
+fi
 # the transport facts that decide what RCCL can pick, for kubectl logs
 shm_fs="$(stat -f -c %T /dev/shm 2>/dev/null || echo '?')"
 echo "entrypoint: rccl preset=${NSA_RCCL_PRESET:-xgmi} NCCL_HOSTID=${NCCL_HOSTID:-<unset>} /dev/shm=${shm_fs}" >&2

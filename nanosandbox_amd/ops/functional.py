@@ -1115,8 +1115,9 @@ def _lm_weight(w, dtype=BF16):
     hit = getattr(w, "_nsa_lm_pad", None)
     if not capturing and hit is not None and hit[0] == key:
         return hit[1], None
-    reuse = hit is not None and not capturing and hit[1].dtype == dtype
-    wp = hit[1] if reuse else torch.zeros(Vp, C, device=w.device, dtype=dtype)
+    # a fresh buffer on every key change: a consumer still holding the operand of
+    # an earlier forward keeps the weights it was given
+    wp = torch.zeros(Vp, C, device=w.device, dtype=dtype)
     wp[:V] = compute_weight(w, dtype)
     if not capturing:
         try:

@@ -117,6 +117,13 @@ class FusedAdamW:
         self._clip_pending = True
         return self._norm
 
+    @property
+    def last_norm(self) -> torch.Tensor:
+        """Device norm of the last gradient check: the user's ``clip_grad_norm_`` or, with a
+        loss scale and no clipping, the inf check ``step()`` runs itself (inf on a step the
+        loss scale skipped).  No sync."""
+        return self._norm
+
     # ----------------------------------------------------------------- step
     @torch.no_grad()
     def step(self):

@@ -61,8 +61,13 @@ SOCKET_ENV = {
 SHM_ENV = {
     "NCCL_SHM_DISABLE": "0",
 }
+# Topology B over xGMI (k8s/statefulset/42-train-multipod-xgmi.yaml): one GPU per pod for the
+# scheduler, but every pod mounts all GPUs of its node and pins the one its ordinal names
+# (NSA_LOCAL_DEVICE); with one NCCL_HOSTID and shared IPC / PID namespaces RCCL connects the
+# pods peer to peer over xGMI.  SHM stays eligible (RCCL's fallback if P2P setup fails).
+XGMI_PODS_ENV = dict(SHM_ENV)
 # transport kind each preset expects (report_transport warns on a mismatch)
-PRESET_TRANSPORT = {"xgmi": "P2P", "shm": "SHM", "socket": "NET"}
+PRESET_TRANSPORT = {"xgmi": "P2P", "xgmi-pods": "P2P", "shm": "SHM", "socket": "NET"}
 
 
 def rccl_env_defaults(preset: str = "xgmi") -> dict:
@@ -71,6 +76,8 @@ def rccl_env_defaults(preset: str = "xgmi") -> dict:
         env.update(SOCKET_ENV)
     elif preset == "shm":
         env.update(SHM_ENV)
+    elif preset == "xgmi-pods":
+        env.update(XGMI_PODS_ENV)
     applied = {}
     for k, v in env.items():
         if k not in os.environ:
@@ -246,6 +253,14 @@ def _attempt_store(rank: int, world: int):
     return dist.PrefixStore(f"nsa/attempt_{restart}", store)
 
 
+def local_device_index(local_rank: int) -> int:
+    """GPU index this process pins: ``NSA_LOCAL_DEVICE`` when the launcher chose one (Topology
+    B over xGMI selects the pod's GPU by its StatefulSet ordinal, container/entrypoint.sh),
+    else LOCAL_RANK (nanoGPT's ``cuda:{LOCAL_RANK}``)."""
+    v = os.environ.get("NSA_LOCAL_DEVICE", "")
+    return int(v) if v.strip() else local_rank
+
+
 def init_distributed(backend: str, device: str) -> DistInfo:
     ddp = int(os.environ.get("RANK", -1)) != -1
     if not ddp:
@@ -268,7 +283,7 @@ def init_distributed(backend: str, device: str) -> DistInfo:
         torch.cuda.set_device(device)
         dist.init_process_group(backend="gloo", **kw)
     elif device.startswith("cuda"):
-        device = f"cuda:{local_rank}"
+        device = f"cuda:{local_device_index(local_rank)}"
         torch.cuda.set_device(device)
         dist.init_process_group(backend=backend, device_id=torch.device(device), **kw)
     else:

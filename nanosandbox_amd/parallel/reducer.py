@@ -37,6 +37,7 @@ flat fp32 master buffer.
 
 from __future__ import annotations
 
+import collections
 import time
 
 import torch
@@ -62,8 +63,12 @@ class _Bucket:
 
 
 class FlatBucketReducer:
+    # per-step records kept for ``exposed_ms``: a long training run that never drains them
+    # holds at most this many event pairs (they grew by two HIP events per step)
+    HISTORY = 256
+
     def __init__(self, store: FlatParamStore, process_group=None, bucket_cap_mb: int = 64,
-                 reduce_dtype: torch.dtype = torch.float32):
+                 reduce_dtype: torch.dtype = torch.float32, history: int = HISTORY):
         assert store.fused_grad, "FlatBucketReducer needs fused main_grad accumulation"
         self.store = store
         self.pg = process_group
@@ -83,9 +88,10 @@ class FlatBucketReducer:
         self._in_finish = False
         # per synchronised step: buckets launched during the backward, and the exposed
         # communication (HIP event pairs on the compute stream, read lazily; host wall
-        # time on the CPU)
-        self.launched_in_backward: list[int] = []
-        self._exposed: list = []
+        # time on the CPU), bounded to the last ``history`` steps
+        self._history = max(1, int(history))
+        self.launched_in_backward: collections.deque = collections.deque(maxlen=self._history)
+        self._exposed: collections.deque = collections.deque(maxlen=self._history)
         for s in store.slots:
             s.param._nsa_grad_hook = self._on_grad
 
@@ -107,8 +113,8 @@ class FlatBucketReducer:
             else:
                 out.append(float(e))
         if clear:
-            self._exposed = []
-            self.launched_in_backward = []
+            self._exposed.clear()
+            self.launched_in_backward.clear()
         return out
 
     # --------------------------------------------------------------- setup

@@ -63,6 +63,10 @@ class Trainer:
         self.device = info.device
         self.device_type = "cuda" if "cuda" in self.device else "cpu"
         self.master = info.master_process
+        if info.ddp and os.environ.get("NSA_LOCAL_DEVICE", "").strip():
+            # Topology B over xGMI: the launcher picked this pod's GPU by its ordinal
+            print(f"rank {info.rank}: device by ordinal NSA_LOCAL_DEVICE={os.environ['NSA_LOCAL_DEVICE']} -> "
+                  f"{self.device}", flush=True)
         gas = c["gradient_accumulation_steps"]
         if info.ddp:
             assert gas % info.world_size == 0
@@ -277,6 +281,8 @@ class Trainer:
         if c["grad_clip"] != 0.0:
             norm = self.optimizer.clip_grad_norm_(c["grad_clip"])
         self.optimizer.step()
+        if norm is None and self.scaler is not None and hasattr(self.optimizer, "last_norm"):
+            norm = self.optimizer.last_norm  # fp16 without clipping: the step's own inf check (inf = skipped)
         self.optimizer.zero_grad(set_to_none=True)
         return loss, norm, X, Y
 

@@ -251,3 +251,35 @@ def test_allreduce_sweep_rows(tmp_path):
         rows = json.load(open(tmp_path / f"sweep{r}.json"))
         assert [x["MiB"] for x in rows] == [1, 2]
         assert all(x["busbw_GBps"] > 0 and x["ms"] > 0 for x in rows)
+
+
+def _bounded_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    model, store, opt = _build(seed=100)
+    red = FlatBucketReducer(store, bucket_cap_mb=0.02, history=8)
+    d = torch.randint(0, 64, (MB, 17), generator=torch.Generator().manual_seed(7))
+    sizes = []
+    for _ in range(40):  # a training loop that never calls exposed_ms()
+        red.prepare(True)
+        _, loss = model(d[:, :-1], d[:, 1:])
+        loss.backward()
+        red.finish()
+        opt.zero_grad()
+        sizes.append((len(red._exposed), len(red.launched_in_backward)))
+    rec = {"sizes": sizes, "exposed": red.exposed_ms(), "after": (len(red._exposed), len(red.launched_in_backward))}
+    if rank == 0:
+        torch.save(rec, os.path.join(out_dir, "bounded0.pt"))
+    dist.destroy_process_group()
+
+
+def test_reducer_history_is_bounded(tmp_path):
+    """finish() records an event pair per synchronised step; a run that never
+    drains them through exposed_ms() (train.py) must not grow without bound."""
+    port = _free_port()
+    mp.spawn(_bounded_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    rec = torch.load(os.path.join(tmp_path, "bounded0.pt"), weights_only=True)
+    assert max(a for a, _ in rec["sizes"]) == 8 and max(b for _, b in rec["sizes"]) == 8
+    assert len(rec["exposed"]) == 8 and rec["after"] == (0, 0)

