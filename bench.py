@@ -108,6 +108,10 @@ def main():
     ap.add_argument("--rccl-sweep", default="4,16,64,256",
                     help="all-reduce sizes (MiB) timed once before the timed steps when WORLD_SIZE > 1 "
                          "(bus bandwidth by bucket size, printed to stderr); '' disables")
+    ap.add_argument("--calib-seconds", type=float, default=2.0,
+                    help="box calibration after the timed steps: our NT GEMM on a fixed shape for this many "
+                         "seconds (TF/s in the record's 'box' block, with the sclk/mclk DPM levels read before "
+                         "and after the timed loop); 0 disables")
     ap.add_argument("--profile", action="store_true",
                     help="nanoGPT bench.py profile mode: torch.profiler over the timed steps "
                          "(schedule wait 1 / warmup 1 / active rest), TensorBoard trace under ./bench_log")
@@ -190,6 +194,10 @@ def main():
                            on_trace_ready=tensorboard_trace_handler("./bench_log"), record_shapes=True,
                            profile_memory=False, with_stack=False)
             prof.start()
+        clk_before = None
+        if cuda:
+            from nanosandbox_amd.utils.boxcal import read_clocks
+            clk_before = read_clocks(torch.device(tr.device).index or 0)
         sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -217,6 +225,23 @@ def main():
         if prof is not None:
             prof.stop()
             print("profiler trace written under ./bench_log (not a clean timing: profiled steps)")
+        box = None
+        if cuda:
+            # outside the timed region: DPM clock levels after the loop, then the calibration GEMM
+            # (the same binary and shape on every box: its TF/s tells a slow box from slow code)
+            clk_after = read_clocks(torch.device(tr.device).index or 0)
+            cal = None
+            if args.calib_seconds > 0:
+                from nanosandbox_amd.utils.boxcal import calibration_gemm
+                del X, Y
+                cal = calibration_gemm(args.calib_seconds, tr.device)
+            box = {"clocks_before": clk_before, "clocks_after": clk_after, "calibration": cal}
+            if dist.is_initialized():
+                every = [None] * world
+                dist.all_gather_object(every, box)
+                box = {"rank0": every[0], "calibration_tflops_by_rank": [
+                    (b["calibration"] or {}).get("tflops") for b in every]}
+            print(f"box: {json.dumps(box)}")
 
     tokens_per_step = tokens_per_micro * tr.gas * world
     value = tokens_per_step * args.steps / dt
@@ -257,6 +282,9 @@ def main():
             # N > 1: RCCL's transport per rank (from its INIT log) + the 64 MiB all-reduce, and
             # the bus bandwidth by message size (docs/rccl.md bucket sizing)
             "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep, reducer, exposed, early),
+            # box calibration (not timed): DPM clock levels around the timed loop and a fixed
+            # calibration GEMM's TF/s, so a slow box can be told from a regression
+            "box": box,
         }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

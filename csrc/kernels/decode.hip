@@ -1003,9 +1003,10 @@ NSA_API hipError_t nsa_sample_topk(const void* logits, int B, int V, int ld, flo
 // ---------------------------------------------------------------------------
 // Decode linear for a batch of 2 .. 64 rows on the matrix cores ("skinny GEMM").
 // The vector GEMV keeps 8 x M fp32 partial dot products per lane and reduces them by
-// shuffles, so its VALU cost grows with M; from 2 rows on the library GEMM beat it,
-// and the library's small-M GEMMs themselves run at a few % of the MFMA rate (GPT-2
-// 1.5B batch 8 decoded at 4.2 ms/token against 1.9 at batch 1).  Here the weight is
+// shuffles, so its VALU cost grows with M; in round 2, from 2 rows on, the then-used
+// library GEMM beat it while running at a few % of the MFMA rate (GPT-2 1.5B batch 8
+// decoded at 4.2 ms/token against 1.9 at batch 1; no library GEMM is on this path any
+// more: M > SKINNY_MAX_ROWS goes to our small-tile / NT kernels).  Here the weight is
 // streamed once through v_mfma_f32_16x16x32_bf16 with the roles swapped:
 //   Y^T[n, m] = W[n, k] · X^T[k, m]      A = 16 weight rows (lane l: row n0 + (l & 15),
 //                                         16 contiguous bytes of it), B = X^T (lane l:

@@ -126,7 +126,13 @@ _SIGNATURES = {
                             c_int, c_int, c_int, c_int, c_void_p],
     "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "nsa_gemm_strip": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
+    "nsa_keysort": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "nsa_keysort_ws_bytes": [c_int],
+    "nsa_probe_spin": [c_int, c_uint64, c_void_p, c_void_p],
+    "nsa_probe_mark": [c_void_p, c_void_p],
 }
+# entry points whose return value is not a hipError_t
+_RESTYPES = {"nsa_keysort_ws_bytes": c_int64}
 
 
 class KernelLibraryMissing(RuntimeError):
@@ -153,7 +159,7 @@ def lib():
                 if fn is None:
                     continue  # optional entry points (checked at call time)
                 fn.argtypes = argtypes
-                fn.restype = c_int
+                fn.restype = _RESTYPES.get(name, c_int)
         _lib = L
         return _lib
 

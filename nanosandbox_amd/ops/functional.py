@@ -293,9 +293,7 @@ class EmbeddingFn(torch.autograd.Function):
                 # capture forbids).  Also the faster form from ~64K tokens: B120 T1024
                 # C768, wte + wpe grads 313.6 vs 369.5 us with fp32 atomics
                 # (scripts/emb_bwd_ab.py, profiles/r5_emb_bwd.md), and deterministic for free.
-                flat = idx.view(-1)
-                ids, order = torch.sort(flat, stable=True)
-                seg = torch.searchsorted(ids, torch.arange(V + 1, device=dx.device, dtype=ids.dtype))
+                ids, order, seg = sort_keys(idx.view(-1), V)
                 # partial sums of the segments that cross a 16-position chunk (two slots a chunk)
                 part = torch.empty(2 * ((B * T + 15) // 16), C, device=dx.device, dtype=F32)
                 _lib.call("nsa_embedding_bwd_det", _lib.ptr(ids), _lib.ptr(order), _lib.ptr(seg), _lib.ptr(part),
@@ -319,6 +317,32 @@ class EmbeddingFn(torch.autograd.Function):
         gwpe = torch.zeros(wpe.shape[0], C, dtype=F32, device=d.device)
         gwpe[:T] = d.sum(0)
         return None, _accumulate(wte, gwte), _accumulate(wpe, gwpe), None, None, None
+
+
+# our stable key sort (csrc/kernels/keysort.hip) instead of torch.sort + searchsorted for the
+# sorted scatter-adds; NSA_KEYSORT=0 falls back to torch's (rocprim) sort
+KEYSORT = os.environ.get("NSA_KEYSORT", "1") == "1"
+
+
+def sort_keys(keys, V):
+    """(ids, order, seg) of ``keys`` (int32 / int64, values -1 .. V-1): the stable ascending
+    sort, the positions it came from (int64), and seg[v] = #{keys < v} for v = 0 .. V --
+    torch.sort(stable=True) + searchsorted(arange(V + 1)), as one HIP radix pass per 8-bit
+    digit (no host sync: HIP-graph capturable)."""
+    flat = keys.reshape(-1)
+    if KEYSORT and flat.is_cuda and V + 1 <= 65536 and flat.dtype in (torch.int32, torch.int64) and flat.numel() > 0:
+        n = flat.numel()
+        flat = flat.contiguous()
+        ids = torch.empty_like(flat)
+        order = torch.empty(n, device=flat.device, dtype=torch.int64)
+        seg = torch.empty(V + 1, device=flat.device, dtype=torch.int64)
+        ws = torch.empty(_lib.call_ret("nsa_keysort_ws_bytes", n), device=flat.device, dtype=torch.uint8)
+        _lib.call("nsa_keysort", _lib.ptr(flat), 1 if flat.dtype == torch.int64 else 0, n, V, _lib.ptr(ids),
+                  _lib.ptr(order), _lib.ptr(seg), _lib.ptr(ws), _lib.stream())
+        return ids, order, seg
+    ids, order = torch.sort(flat, stable=True)
+    seg = torch.searchsorted(ids, torch.arange(V + 1, device=flat.device, dtype=ids.dtype))
+    return ids, order, seg
 
 
 # below this the fp32-atomic embedding backward (no sort launches) unless deterministic:
@@ -941,11 +965,12 @@ def decode_linear(x, w, b=None, gelu: bool = False, out_f32: bool = False):
     """act(x @ W^T + b) for a decode batch: with <= GEMV_MAX_ROWS rows one weight-streaming
     kernel with the bias / exact GELU in its epilogue on the GPU (bf16, K % 8 == 0);
     otherwise ``linear`` (+ ``gelu``).  Inference only.  Measured (GPT-2 124M / 1.5B
-    decode, HIP graph): batch 1 0.69 / 3.02 ms per token vs 0.90 / 4.70 with the library
-    GEMM + bias copy; from 2 rows on the library GEMM is faster (batch 4: 1.52 vs
-    < 0.9 ms at 124M), so the default cap is 1 row (``NSA_GEMV_MAX_ROWS``).  Batches of
-    2 .. ``NSA_SKINNY_MAX_ROWS`` (16) rows run on ``nsa_skinny_gemm`` (MFMA weight stream,
-    bias / GELU epilogue) when N % 16 == 0 and K % 32 == 0."""
+    decode, HIP graph): batch 1 0.69 / 3.02 ms per token vs 0.90 / 4.70 with the (round-2)
+    library GEMM + bias copy.  The vector GEMV's VALU grows with the rows (batch 4: 1.52 ms
+    per token at 124M in round 2), so the default cap is 1 row (``NSA_GEMV_MAX_ROWS``) and
+    batches of 2 .. ``NSA_SKINNY_MAX_ROWS`` (16) rows run on ``nsa_skinny_gemm`` (MFMA
+    weight stream, bias / GELU epilogue) when N % 16 == 0 and K % 32 == 0; larger batches go
+    to ``linear`` (our small-tile / NT kernels: no library GEMM on this path)."""
     N = w.shape[0]
     if isinstance(x, AttnPartials):  # one row; the attention combine runs in the GEMV prologue
         y = torch.empty(N, device=x.ws.device, dtype=F32 if out_f32 else BF16)
@@ -1271,8 +1296,7 @@ class LMHeadLossFn(torch.autograd.Function):
                           _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(part), _lib.ptr(gw), C, N, C, V, _lib.stream())
             elif XENT_FIX_SORTED:
                 # the onehot term atomic-free: rows sorted by target, one writer per vocab row
-                ids, order = torch.sort(t32, stable=True)
-                seg = torch.searchsorted(ids, torch.arange(Vp + 1, device=x2.device, dtype=ids.dtype))
+                ids, order, seg = sort_keys(t32, Vp)
                 part = torch.empty(2 * (-(-N // 16)), C, device=x2.device, dtype=F32)
                 _lib.call(_sym("nsa_xent_dw_fix_sorted", x2.dtype), _lib.ptr(x2), C, _lib.ptr(e), Vp, _lib.ptr(t32),
                           _lib.ptr(inv_s), _lib.ptr(g), _lib.ptr(ids), _lib.ptr(order), _lib.ptr(seg),

@@ -122,6 +122,18 @@ def _check_gp(u):
         raise ValueError("u must be gelu'(u) in fp16 (the NT_EPI_GELU epilogue's first output)")
 
 
+# Persistent-grid oversubscription: the four-wave NT kernel launches NT_GRID_MULT x #CUs
+# workgroups (one resident per CU).  1 = one static tile chain per CU (fastest alone); > 1 cuts
+# every chain into NT_GRID_MULT pieces, so a workgroup exits -- and frees its CU for a bucket
+# all-reduce's kernel, or hands the rest of the GEMM to the hardware dispatcher when a CU started
+# late -- every 1 / NT_GRID_MULT of the GEMM (scripts/debug/overlap_hazard.py).
+NT_GRID_MULT = int(os.environ.get("NSA_NT4_GRID_MULT", "1"))
+
+
+def nt_grid(device=None) -> int:
+    return num_cus(device) * max(1, NT_GRID_MULT)
+
+
 def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, gm=0, out=None, out2=None):
     """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the four-wave kernel.
 
@@ -148,7 +160,7 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, g
         u = gelu_table(a.device) if a.dtype == BF16 else None
     _lib.call(_sym("nsa_gemm_nt4", a), epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
               b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
-              grid or num_cus(a.device), _lib.stream())
+              grid or nt_grid(a.device), _lib.stream())
     return (c, c2) if epi == NT_EPI_GELU else c
 
 
@@ -212,7 +224,7 @@ def nt_xent(x, w, crow, part, nvalid, out=None):
     _check(w, "w")
     e = _out(M, N, x.device, out, x.dtype)
     _lib.call(_sym("nsa_gemm_nt4_xent", x), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(e), e.stride(0),
-              _lib.ptr(crow), _lib.ptr(part), M, N, int(nvalid), K, num_cus(x.device), _lib.stream())
+              _lib.ptr(crow), _lib.ptr(part), M, N, int(nvalid), K, nt_grid(x.device), _lib.stream())
     return e
 
 
@@ -225,7 +237,7 @@ def nt_xdx(e, wt, wrows, coef, out=None):
     _check(wrows, "wrows")
     c = _out(M, N, e.device, out, e.dtype)
     _lib.call(_sym("nsa_gemm_nt4_xdx", e), _lib.ptr(e), e.stride(0), _lib.ptr(wt), wt.stride(0), _lib.ptr(c), c.stride(0),
-              _lib.ptr(wrows), _lib.ptr(coef), M, N, K, num_cus(e.device), _lib.stream())
+              _lib.ptr(wrows), _lib.ptr(coef), M, N, K, nt_grid(e.device), _lib.stream())
     return c
 
 

@@ -69,3 +69,33 @@ def test_multirank_record_carries_rccl_block(tmp_path):
     assert len(rc["exposed_allreduce_ms_per_step"]) == 1
     assert all(n >= 1 for n in rc["buckets_launched_in_backward"])
     assert "gemm_kernels" in rec  # per GEMM shape the kernel that ran it (empty on the CPU)
+    assert "box" in rec and rec["box"] is None  # clocks + calibration GEMM: GPU runs only
+
+
+def test_read_clocks_parses_dpm_tables(tmp_path, monkeypatch):
+    """VERDICT r5 item 7: the bench record's clock fields come from the amdgpu DPM tables;
+    the '*' level is the one in use, the top level is the card's maximum."""
+    from nanosandbox_amd.utils import boxcal
+
+    dev = tmp_path / "card1" / "device"
+    dev.mkdir(parents=True)
+    (dev / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 1800Mhz *\n2: 2400Mhz\n")
+    (dev / "pp_dpm_mclk").write_text("0: 900Mhz\n1: 1900Mhz *\n")
+    monkeypatch.setattr(boxcal.glob, "glob", lambda pat: [str(dev)])
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    c = boxcal.read_clocks(0)
+    assert c["sclk"] == {"cur_mhz": 1800, "max_mhz": 2400} and c["mclk"] == {"cur_mhz": 1900, "max_mhz": 1900}
+    assert c["source"] == "sysfs:card1"
+    monkeypatch.setattr(boxcal.glob, "glob", lambda pat: [])
+    monkeypatch.setattr(boxcal.shutil, "which", lambda name: None)
+    assert boxcal.read_clocks(0) == {"sclk": None, "mclk": None, "source": None}
+
+
+def test_bench_record_has_box_block():
+    """The record carries a 'box' block (clocks before / after the timed loop + calibration
+    GEMM TF/s) next to the timing; bench.py's CLI exposes the calibration length."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "bench.py")).read()
+    assert '"box": box' in src and "--calib-seconds" in src
+    assert "clocks_before" in src and "clocks_after" in src and "calibration_gemm" in src

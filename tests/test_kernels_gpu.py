@@ -1282,3 +1282,36 @@ def test_gpt_dropout_under_activation_checkpointing(kernels):
     assert res[0][0] == res[1][0]
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+# ---------------------------------------------------------------- key sort
+@pytest.mark.parametrize("N,V,dtype,dist", [(122880, 50304, torch.int64, "uniform"),
+                                            (122880, 50304, torch.int32, "ignored"),
+                                            (61440, 50304, torch.int64, "skew"),
+                                            (16384, 65, torch.int64, "uniform"),
+                                            (16384, 65, torch.int32, "ignored"),
+                                            (4097, 300, torch.int64, "one_id"),
+                                            (1, 50304, torch.int32, "uniform"),
+                                            (5000, 65535, torch.int64, "uniform")])
+def test_keysort_matches_torch(kernels, N, V, dtype, dist):
+    """csrc/kernels/keysort.hip (no rocprim sort on the step) against
+    torch.sort(stable=True) + searchsorted: ids, positions (equal keys in position order) and
+    segment starts bit for bit, including -1 (ignored targets), one- and two-pass key ranges,
+    a heavily repeated id and partial chunks."""
+    from nanosandbox_amd.ops import functional as Fn
+
+    g = torch.Generator(device=DEV).manual_seed(N + V)
+    k = torch.randint(0, V, (N,), device=DEV, generator=g)
+    if dist == "ignored":
+        k[torch.rand(N, device=DEV, generator=g) < 0.1] = -1
+    elif dist == "skew":
+        k[torch.rand(N, device=DEV, generator=g) < 0.3] = 220  # one token a third of the batch
+    elif dist == "one_id":
+        k[:] = V - 1
+    k = k.to(dtype)
+    ids, order, seg = Fn.sort_keys(k, V)
+    torch.cuda.synchronize()
+    rid, rord = torch.sort(k, stable=True)
+    rseg = torch.searchsorted(rid, torch.arange(V + 1, device=DEV, dtype=rid.dtype))
+    assert ids.dtype == dtype and order.dtype == torch.int64 and seg.dtype == torch.int64
+    assert torch.equal(ids, rid) and torch.equal(order, rord) and torch.equal(seg, rseg)
