@@ -112,12 +112,25 @@ def main():
                     help="box calibration after the timed steps: our NT GEMM on a fixed shape for this many "
                          "seconds (TF/s in the record's 'box' block, with the sclk/mclk DPM levels read before "
                          "and after the timed loop); 0 disables")
+    ap.add_argument("--per-rank-of", type=int, default=0, metavar="N",
+                    help="PROJECTION (not the headline): run one rank's share of an N-GPU job on this one GPU "
+                         "-- the N-rank micro-batch plan (60 x 1 at N = 8), the flat reducer's hooks armed, each "
+                         "bucket all-reduce replaced by a collective-shaped kernel on a high-priority side stream "
+                         "for its modelled ring time (parallel/emulate.py) -- and report the per-rank step and "
+                         "the projected N-GPU tokens/s")
+    ap.add_argument("--emu-busbw", type=float, default=300.0,
+                    help="--per-rank-of: assumed RCCL all-reduce bus bandwidth, GB/s (not measured here)")
+    ap.add_argument("--emu-nwg", type=int, default=32,
+                    help="--per-rank-of: workgroups of the emulated collective kernel (RCCL channels)")
     ap.add_argument("--profile", action="store_true",
                     help="nanoGPT bench.py profile mode: torch.profiler over the timed steps "
                          "(schedule wait 1 / warmup 1 / active rest), TensorBoard trace under ./bench_log")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    emu = args.per_rank_of if args.per_rank_of > 1 else 0
+    if emu and (world != 1 or args.device != "cuda"):
+        raise SystemExit("--per-rank-of runs one process on one GPU")
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N bench.py ...")
@@ -144,8 +157,10 @@ def main():
         if os.environ.get("NSA_REHEARSAL_ONE_GPU") == "1":
             hbm //= world  # the ranks share the one GPU's HBM
         args.micro_batch, _ = choose_micro_batch(dims[0], dims[2], dims[1], 50304, args.block_size,
-                                                 480 // world, hbm, fp32_residual=not args.bf16_residual)
-    args.micro_batch, total_micro = batch_plan(world, args.micro_batch)
+                                                 480 // (emu or world), hbm, fp32_residual=not args.bf16_residual)
+    args.micro_batch, total_micro = batch_plan(emu or world, args.micro_batch)
+    if emu:
+        total_micro //= emu  # this process runs one rank's micro-steps (the Trainer's world is 1)
     tokens_per_micro = args.micro_batch * args.block_size
     cfg = dict(TRAIN_DEFAULTS)
     dataset, data_dir = "synthetic", ""
@@ -165,6 +180,12 @@ def main():
 
     with contextlib.redirect_stdout(sys.stderr):
         tr = Trainer(cfg)
+        if emu:
+            from nanosandbox_amd.parallel.emulate import EmulatedAllReduce
+            tr.reducer = EmulatedAllReduce(tr.store, emu, bucket_cap_mb=args.bucket_mb, busbw_GBps=args.emu_busbw,
+                                           nwg=args.emu_nwg)
+            print(f"per-rank-of {emu}: {tr.gas} micro-step(s) of {args.micro_batch} x {args.block_size}, "
+                  f"emulated all-reduce {json.dumps(tr.reducer.model())}")
         for g in tr.optimizer.param_groups:
             g["lr"] = cfg["learning_rate"]
         X, Y = tr.batches.get_batch("train")
@@ -178,8 +199,9 @@ def main():
         if world > 1 and args.rccl_sweep:
             from nanosandbox_amd.parallel import allreduce_sweep
             sweep = allreduce_sweep(tr.info, [int(v) for v in args.rccl_sweep.split(",") if v])
+        multi = dist.is_initialized() and world > 1
         sync()
-        if dist.is_initialized():
+        if multi:
             dist.barrier()
         reducer = getattr(tr, "reducer", None)
         if reducer is not None:
@@ -205,12 +227,12 @@ def main():
             if prof is not None:
                 prof.step()
         sync()
-        if dist.is_initialized():
+        if multi:
             dist.barrier()
         sync()
         dt = time.perf_counter() - t0
         dt_t = torch.tensor([dt], device=tr.device, dtype=torch.float64)
-        if dist.is_initialized():
+        if multi:
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         dt = float(dt_t.item())
         exposed, early = None, None
@@ -218,7 +240,7 @@ def main():
             early = list(reducer.launched_in_backward)
             exposed = reducer.exposed_ms(clear=True)
             ex_t = torch.tensor(exposed or [0.0], device=tr.device, dtype=torch.float64)
-            if dist.is_initialized():
+            if multi:
                 dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)
             exposed = [float(v) for v in ex_t.tolist()] if exposed else []
         lossf = float(loss.item()) * tr.gas
@@ -236,7 +258,7 @@ def main():
                 del X, Y
                 cal = calibration_gemm(args.calib_seconds, tr.device)
             box = {"clocks_before": clk_before, "clocks_after": clk_after, "calibration": cal}
-            if dist.is_initialized():
+            if multi:
                 every = [None] * world
                 dist.all_gather_object(every, box)
                 box = {"rank0": every[0], "calibration_tflops_by_rank": [
@@ -245,47 +267,71 @@ def main():
 
     tokens_per_step = tokens_per_micro * tr.gas * world
     value = tokens_per_step * args.steps / dt
+    if emu:
+        # one rank's share of the N-GPU step, measured; the job's rate is N x that share per step
+        # time (every rank runs the same schedule), the collectives' time being the model's
+        proj = {"projection": True, "per_rank_of": emu, "per_rank_ms": round(dt / args.steps * 1000.0, 3),
+                "per_rank_tokens_per_step": tokens_per_step,
+                "projected_tokens_per_s": round(emu * tokens_per_step * args.steps / dt, 1),
+                "projected_global_batch": tokens_per_step * emu // args.block_size,
+                "allreduce_model": tr.reducer.model(),
+                "exposed_allreduce_ms": round(sum(exposed) / len(exposed), 3) if exposed else None,
+                "buckets_launched_in_backward": list(early or [])}
+        print(f"per-rank-of {emu} (PROJECTION): {json.dumps(proj)}", file=sys.stderr)
     ms = dt / args.steps * 1000.0
     flops_per_token = tr.raw_model.flops_per_token(args.block_size)
     mfu = value * flops_per_token / (world * 2.5e15)
     if tr.info.rank == 0:
         # nanoGPT bench.py's summary line (stderr; stdout carries only the JSON record)
         print(f"time per iteration: {ms:.4f}ms, MFU: {mfu * 100:.2f}%", file=sys.stderr)
-        print(json.dumps({
-            "metric": METRIC if args.model == "gpt2" else f"tokens/sec (whole node) {args.model} DDP",
-            "value": round(value, 1),
-            "unit": "tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": ({"bfloat16": "bf16", "float16": "fp16"}[args.dtype]) if cuda else "fp32",
-            "data": (f"real ({dataset}); random-init weights" if args.real_data else
-                     "synthetic (uniform random tokens, vocab 50304); random-init weights"),
-            "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,
-                       "global_batch": tokens_per_step // args.block_size, "seq_len": args.block_size,
-                       "tokens_per_step": tokens_per_step, "micro_batch": args.micro_batch,
-                       "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
-                       "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
-                       "residual_dtype": "bf16" if args.bf16_residual else "fp32",
-                       "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt),
-                       "bias": args.bias},
-            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1) if cuda else None,
-            "mfu_vs_2.5PF": round(mfu, 4),
-            "loss": round(lossf, 4),
-            # every GEMM shape of the step and the kernel that ran it (fixed rule,
-            # ops/gemm_dispatch.py): a vendor-library pick would read "torch"
-            "gemm_kernels": gemm_kernels,
-            # N > 1: RCCL's transport per rank (from its INIT log) + the 64 MiB all-reduce, and
-            # the bus bandwidth by message size (docs/rccl.md bucket sizing)
-            "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep, reducer, exposed, early),
-            # box calibration (not timed): DPM clock levels around the timed loop and a fixed
-            # calibration GEMM's TF/s, so a slow box can be told from a regression
-            "box": box,
-        }), flush=True)
+        if emu:
+            # a different record: the projected N-GPU rate, never the headline metric
+            print(json.dumps({
+                "metric": f"PROJECTED tokens/sec ({emu} GPUs) {args.model} DDP from one rank's share on 1 GPU",
+                "value": proj["projected_tokens_per_s"], "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": proj["per_rank_ms"], "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.dtype == "bfloat16" else "fp16",
+                "data": "synthetic (uniform random tokens, vocab 50304); random-init weights",
+                "config": {"model": args.model, "micro_batch": args.micro_batch, "grad_accum_per_rank": tr.gas,
+                           "seq_len": args.block_size, "parallelism": f"dp{emu} (emulated, one rank)",
+                           "bucket_mb": args.bucket_mb},
+                "projection": proj, "box": box}), flush=True)
+        else:
+            print(json.dumps({
+                "metric": METRIC if args.model == "gpt2" else f"tokens/sec (whole node) {args.model} DDP",
+                "value": round(value, 1),
+                "unit": "tokens/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(ms, 3),
+                "higher_is_better": True,
+                "scaling": "strong",
+                "vs_baseline": None,
+                "dtype": ({"bfloat16": "bf16", "float16": "fp16"}[args.dtype]) if cuda else "fp32",
+                "data": (f"real ({dataset}); random-init weights" if args.real_data else
+                         "synthetic (uniform random tokens, vocab 50304); random-init weights"),
+                "config": {"model": "GPT-2 124M" if args.model == "gpt2" else args.model,
+                           "global_batch": tokens_per_step // args.block_size, "seq_len": args.block_size,
+                           "tokens_per_step": tokens_per_step, "micro_batch": args.micro_batch,
+                           "grad_accum_per_rank": tr.gas, "parallelism": f"dp{world}",
+                           "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
+                           "residual_dtype": "bf16" if args.bf16_residual else "fp32",
+                           "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt),
+                           "bias": args.bias},
+                "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1) if cuda else None,
+                "mfu_vs_2.5PF": round(mfu, 4),
+                "loss": round(lossf, 4),
+                # every GEMM shape of the step and the kernel that ran it (fixed rule,
+                # ops/gemm_dispatch.py): a vendor-library pick would read "torch"
+                "gemm_kernels": gemm_kernels,
+                # N > 1: RCCL's transport per rank (from its INIT log) + the 64 MiB all-reduce, and
+                # the bus bandwidth by message size (docs/rccl.md bucket sizing)
+                "rccl": rccl_summary(getattr(tr, "rccl_report", None), sweep, reducer, exposed, early),
+                # box calibration (not timed): DPM clock levels around the timed loop and a fixed
+                # calibration GEMM's TF/s, so a slow box can be told from a regression
+                "box": box,
+            }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

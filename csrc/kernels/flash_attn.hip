@@ -30,6 +30,12 @@
 // which is conflict-free both for the 16-row ds_read_b128 groups and for the
 // 4-row x 4-chunk blocks of ds_read_b64_tr_b16 (checked for D = 32, 64, 128).
 //
+// Built with -fno-slp-vectorize (nanosandbox_amd/build.py FILE_FLAGS): hipcc's SLP pass packed
+// adjacent f32 multiplies / adds of the softmax (score scaling, row sums, dS) into v_pk_mul_f32
+// / v_pk_add_f32, which cost more issue cycles beside MFMAs than two scalar ops
+// (MI355X_MICROARCH.md 'price of one filler': 1 v_pk_fma_f32 +22 cycles vs 2 v_fma_f32); the
+// fast-tile score scaling is written as scalar multiplies for the same reason.
+//
 // Softmax uses exp2 with log2(e)/sqrt(D) folded into one multiplier; the LSE
 // (natural log) is saved per query for the backward recompute of P.
 // Dropout (char config, p = 0.2) uses the counter-based hash of common.h on
@@ -355,11 +361,7 @@ __device__ __forceinline__ bool fwd_tile_fast(const char* kt, const char* vt, co
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {  // one v_pk_mul_f32 per score pair
-      nsa_f32x2 v2 = nsa_f32x2{st[sb][i], st[sb][i + 1]} * scale_log2;
-      st[sb][i] = v2.x;
-      st[sb][i + 1] = v2.y;
-    }
+    for (int i = 0; i < 16; ++i) st[sb][i] *= scale_log2;  // scalar v_mul_f32 (see NSA_FA_NOSLP)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float sv = st[sb][i];
@@ -741,11 +743,7 @@ __device__ __forceinline__ bool fwd_tile5(const char* kt, const char* vt, const 
     for (int sb = 0; sb < 2; ++sb) {
       if constexpr (!NSA_FWD5_QSCALE) {
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {  // one v_pk_mul_f32 per score pair
-          nsa_f32x2 v2 = nsa_f32x2{st[blk][sb][i], st[blk][sb][i + 1]} * scale_log2;
-          st[blk][sb][i] = v2.x;
-          st[blk][sb][i + 1] = v2.y;
-        }
+        for (int i = 0; i < 16; ++i) st[blk][sb][i] *= scale_log2;  // scalar v_mul_f32 (see NSA_FA_NOSLP)
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {

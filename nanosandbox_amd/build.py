@@ -54,10 +54,18 @@ def _run(cmd):
     return r
 
 
-def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL_LIB, obj_dir=BUILD_DIR):
+# per-source compiler flags.  The attention kernels without the SLP vectorizer: it packed the
+# softmax's adjacent f32 multiplies / adds into v_pk_*_f32, an anti-lever beside MFMAs
+# (MI355X_MICROARCH.md 'price of one filler'; A/B: scripts/attn_ab.py against a variant
+# library built with file_flags={}).
+FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"], "flash_attn_f16.hip": ["-fno-slp-vectorize"]}
+
+
+def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL_LIB, obj_dir=BUILD_DIR,
+                  file_flags=None):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
-    if not force and not _newer(lib_path, srcs + headers):
+    if not force and not _newer(lib_path, srcs + headers + [os.path.abspath(__file__)]):
         return lib_path
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
@@ -74,10 +82,12 @@ def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL
                 out.append(os.path.join(os.path.dirname(src), line.split('"')[1]))
         return out
 
+    ff = FILE_FLAGS if file_flags is None else file_flags
+
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-        if force or _newer(obj, [src] + headers + deps(src)):
-            _run([hipcc, *flags, "-c", src, "-o", obj])
+        if force or _newer(obj, [src] + headers + deps(src) + [os.path.abspath(__file__)]):
+            _run([hipcc, *flags, *ff.get(os.path.basename(src), []), "-c", src, "-o", obj])
             if verbose:
                 print(f"  [hipcc {ARCH}] {os.path.relpath(src, ROOT)}")
         return obj
@@ -92,7 +102,7 @@ def build_kernels(force=False, jobs=8, verbose=True, defines=(), lib_path=KERNEL
     return lib_path
 
 
-def build_variant(name, defines, force=False, jobs=8, verbose=True):
+def build_variant(name, defines, force=False, jobs=8, verbose=True, file_flags=None):
     """Build the kernel library with extra -D flags into ``build/variants/<name>/``.
 
     Used for A/B probes (``NSA_KERNEL_LIB=<path>`` selects it at import time), e.g.
@@ -101,7 +111,8 @@ def build_variant(name, defines, force=False, jobs=8, verbose=True):
     """
     vdir = os.path.join(ROOT, "build", "variants", name)
     return build_kernels(force=force, jobs=jobs, verbose=verbose, defines=defines,
-                         lib_path=os.path.join(vdir, "libnsa_kernels.so"), obj_dir=os.path.join(vdir, "obj"))
+                         lib_path=os.path.join(vdir, "libnsa_kernels.so"), obj_dir=os.path.join(vdir, "obj"),
+                         file_flags=file_flags)
 
 
 def build_runtime(force=False, verbose=True):
@@ -150,9 +161,12 @@ def main(argv=None):
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--variant", nargs="+", metavar=("NAME", "DEFINE"),
                     help="build an A/B probe variant: NAME followed by preprocessor defines")
+    ap.add_argument("--no-file-flags", action="store_true",
+                    help="with --variant: compile every source with the common flags only (no FILE_FLAGS)")
     a = ap.parse_args(argv)
     if a.variant:
-        print(build_variant(a.variant[0], a.variant[1:], force=a.force, jobs=a.jobs))
+        print(build_variant(a.variant[0], a.variant[1:], force=a.force, jobs=a.jobs,
+                            file_flags={} if a.no_file_flags else None))
         return 0
     build_all(force=a.force, jobs=a.jobs)
 

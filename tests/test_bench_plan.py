@@ -99,3 +99,31 @@ def test_bench_record_has_box_block():
     src = open(os.path.join(root, "bench.py")).read()
     assert '"box": box' in src and "--calib-seconds" in src
     assert "clocks_before" in src and "clocks_after" in src and "calibration_gemm" in src
+
+
+def test_per_rank_emulation_model_and_record():
+    """--per-rank-of N: one rank's micro-batch plan of an N-GPU job, the
+    flat reducer's buckets with each all-reduce modelled as a ring at an assumed bus bandwidth,
+    and a record that says it is a projection (never the headline metric)."""
+    import torch
+
+    import bench
+    from nanosandbox_amd.models import GPT, GPTConfig
+    from nanosandbox_amd.optim import FlatParamStore
+    from nanosandbox_amd.parallel.emulate import EmulatedAllReduce
+
+    assert bench.batch_plan(8, 60) == (60, 8)  # 60 x 1 per rank: the N = 8 share of 480 sequences
+    cfg = GPTConfig(n_layer=12, n_head=12, n_embd=768, block_size=1024, vocab_size=50304, bias=False)
+    store = FlatParamStore(GPT(cfg), "cpu")
+    emu = EmulatedAllReduce(store, 8, bucket_cap_mb=64, busbw_GBps=300.0, nwg=32)
+    m = emu.model()
+    assert m["world"] == 8 and m["busbw_GBps"] == 300.0 and m["nwg"] == 32
+    assert len(m["allreduce_us_by_bucket"]) == len(emu.buckets) == 7
+    b = emu.buckets[0]
+    want = 2 * 7 / 8 * (b.end - b.start) * 4 / 300e3
+    assert abs(m["allreduce_us_by_bucket"][0] - round(want, 1)) < 0.11
+    assert emu.grad_scale == 1.0
+    torch.distributed.destroy_process_group()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "bench.py")).read()
+    assert "--per-rank-of" in src and '"projection": True' in src and "PROJECTED tokens/sec" in src
