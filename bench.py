@@ -91,6 +91,9 @@ def main():
     ap.add_argument("--ddp-impl", default="flat", choices=["flat", "torch"])
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--grad-ckpt", action="store_true")
+    ap.add_argument("--recompute-mlp", action="store_true",
+                    help="selective recomputation: each MLP keeps only its input and recomputes c_fc + GELU in "
+                         "the backward (config key recompute_mlp)")
     ap.add_argument("--bias", action="store_true",
                     help="Linear / LayerNorm biases (nanoGPT bias=True, the GPT-2 checkpoints' layout)")
     ap.add_argument("--deterministic", action="store_true",
@@ -147,7 +150,7 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
-    if args.micro_batch <= 0 and not args.grad_ckpt and cuda:
+    if args.micro_batch <= 0 and not args.grad_ckpt and not args.recompute_mlp and cuda:
         # HBM-sized micro-batch: the largest divisor of the per-rank batch whose activations
         # stay resident next to the model state (utils/memory.py); 120 for GPT-2 124M / 350M
         from nanosandbox_amd.utils.memory import choose_micro_batch
@@ -174,6 +177,7 @@ def main():
                dropout=0.0, bias=args.bias, compile=False, device=args.device, dtype=args.dtype,
                backend="nccl" if cuda else "gloo",
                ddp_impl=args.ddp_impl, ddp_bucket_mb=args.bucket_mb, grad_ckpt=args.grad_ckpt,
+               recompute_mlp=args.recompute_mlp,
                fp32_residual=not args.bf16_residual, deterministic=args.deterministic,
                out_dir="/tmp/nsa_bench_out", metrics_jsonl=False, learning_rate=6e-4, warmup_iters=0,
                decay_lr=False)
@@ -318,6 +322,7 @@ def main():
                            "ddp_impl": args.ddp_impl, "bucket_mb": args.bucket_mb,
                            "residual_dtype": "bf16" if args.bf16_residual else "fp32",
                            "deterministic": args.deterministic, "grad_ckpt": bool(tr.raw_model.grad_ckpt),
+                       "recompute_mlp": bool(tr.raw_model.recompute_mlp),
                            "bias": args.bias},
                 "peak_hbm_gib": round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 1) if cuda else None,
                 "mfu_vs_2.5PF": round(mfu, 4),

@@ -59,6 +59,7 @@ TRAIN_DEFAULTS = dict(
     grad_reduce_dtype="float32",  # 'float32' | 'bfloat16' (compressed all-reduce)
     rccl_report=True,  # at DDP start: per-peer RCCL transport (P2P/SHM/NET) + 64 MiB all-reduce bus bandwidth
     grad_ckpt=False,  # recompute each Block in backward (activation checkpointing)
+    recompute_mlp=False,  # selective recomputation: MLPs keep only their input, redo c_fc + GELU in backward
     hbm_plan=True,  # grad_ckpt=False: turn checkpointing on only if the activation estimate exceeds free HBM
     fp32_residual=True,  # residual stream + its gradient in fp32 (nanoGPT autocast contract); False: bf16
     deterministic=False,  # bitwise-reproducible steps: no fp32 atomics (fixed-order split-K, sorted embedding bwd)

@@ -125,7 +125,6 @@ _SIGNATURES = {
     "nsa_xent_dw_fix_lds": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_int, c_int, c_void_p],
     "nsa_colsum_bf16_partial": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
-    "nsa_gemm_strip": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "nsa_keysort": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "nsa_keysort_ws_bytes": [c_int],
     "nsa_probe_spin": [c_int, c_uint64, c_void_p, c_void_p],

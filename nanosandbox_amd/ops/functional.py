@@ -731,7 +731,7 @@ class MLPFn(torch.autograd.Function):
     gradients from the same kernel's dY fragments (``weight_bias_grad``)."""
 
     @staticmethod
-    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
+    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj, recompute=False):
         C = x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
         wf = compute_weight(w_fc, x.dtype)
@@ -739,25 +739,38 @@ class MLPFn(torch.autograd.Function):
         bp = compute_weight(b_proj, x.dtype) if b_proj is not None else None
         gp, g = _gd.fwd_gelu(x2, wf, bf)
         y = _gd.fwd(g, compute_weight(w_proj, x.dtype), bp)
-        ctx.save_for_backward(x2, gp, g, w_fc, b_fc, w_proj, b_proj)
+        # recompute (selective recomputation, config key recompute_mlp): keep only the block's
+        # input x2; the backward re-runs the c_fc GEMM and its GELU epilogue for gelu(u) /
+        # gelu'(u) -- 16 of the ~36 bytes per token and channel a block keeps (utils/memory.py)
+        ctx.recompute = bool(recompute)
+        if ctx.recompute:
+            ctx.save_for_backward(x2, w_fc, b_fc, w_proj, b_proj)
+        else:
+            ctx.save_for_backward(x2, gp, g, w_fc, b_fc, w_proj, b_proj)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w_proj.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, gp, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
+        if ctx.recompute:
+            x2, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
+            bf = compute_weight(b_fc, x2.dtype) if b_fc is not None else None
+            gp, g = _gd.fwd_gelu(x2, compute_weight(w_fc, x2.dtype), bf)
+        else:
+            x2, gp, g, w_fc, b_fc, w_proj, b_proj = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         gw_proj, gb_proj = weight_bias_grad(w_proj, b_proj, dy2, g)
         du = _gd.dgrad_dgelu(dy2, compute_weight(w_proj, dy.dtype), gp)
         gw_fc, gb_fc = weight_bias_grad(w_fc, b_fc, du, x2)
         dx = _gd.dgrad(du, compute_weight(w_fc, dy.dtype))
-        return dx.view(ctx.xshape), gw_fc, gb_fc, gw_proj, gb_proj
+        return dx.view(ctx.xshape), gw_fc, gb_fc, gw_proj, gb_proj, None
 
 
-def mlp(x, w_fc, b_fc, w_proj, b_proj):
-    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X (bf16 / fp16)."""
+def mlp(x, w_fc, b_fc, w_proj, b_proj, recompute=False):
+    """c_proj(gelu(c_fc(x))): one fused autograd node on MI355X (bf16 / fp16).  ``recompute``:
+    the node keeps only its input and redoes the c_fc GEMM + GELU in the backward."""
     if x.is_cuda and x.dtype in KDT:
-        return MLPFn.apply(x, w_fc, b_fc, w_proj, b_proj)
+        return MLPFn.apply(x, w_fc, b_fc, w_proj, b_proj, recompute)
     return linear(gelu(linear(x, w_fc, b_fc)), w_proj, b_proj)
 
 
@@ -814,7 +827,7 @@ def _attn_reference(q, k, v, p, seed):
     return att @ v
 
 
-_FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6}
+_FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6, "v7": 7}
 _FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3}
 
 

@@ -164,39 +164,6 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, g
     return (c, c2) if epi == NT_EPI_GELU else c
 
 
-def strip_split_n(N: int) -> int:
-    """Columns the four-wave kernel takes when the rest of N goes to the strip kernel (0: no
-    split).  N = 256 q + r with 16 <= r <= 64, r % 16 == 0, q >= 1: the persistent kernel's
-    last column tile would be a 256-wide tile shifted back for r new columns (GPT-2 1.5B:
-    N = 1600 = 6 x 256 + 64; scripts/debug/nt_tail_probe.py: 1536 columns 237 vs 278 us
-    for all 1600 at M = 61440, K = 1600)."""
-    r = N % TILE
-    return N - r if (N > TILE and 16 <= r <= 64 and r % 16 == 0) else 0
-
-
-def nt_strip(a, b, bias=None):
-    """C = a @ b^T (+ bias) as the four-wave kernel over the first ``strip_split_n(N)``
-    columns plus the column-strip kernel (``gemm_strip.hip``) over the rest, both writing
-    one [M, N] output."""
-    M, K = a.shape
-    N = b.shape[0]
-    N0 = strip_split_n(N)
-    _check(a, "a")
-    _check(b, "b")
-    if bias is not None:
-        _check(bias, "bias")
-    if not N0 or K % BK:
-        raise ValueError(f"nt_strip: N = {N}, K = {K} outside the split rule")
-    c = torch.empty(M, N, device=a.device, dtype=a.dtype)
-    b0 = b[:N0]
-    _lib.call(_sym("nsa_gemm_nt4", a), NT_EPI_BF16 | (NT_VAR << 12), _lib.ptr(a), a.stride(0), _lib.ptr(b0), b.stride(0),
-              _lib.ptr(c), N, None, None, _lib.ptr(bias), M, N0, K, num_cus(a.device), _lib.stream())
-    _lib.call(_sym("nsa_gemm_strip", a), _lib.ptr(a), a.stride(0), _lib.ptr(b[N0:]), b.stride(0),
-              _lib.ptr(c[:, N0:]), N, _lib.ptr(bias[N0:]) if bias is not None else None, M, N - N0, K,
-              _lib.stream())
-    return c
-
-
 def small(a, b, epi=NT_EPI_BF16, u=None, bias=None, out=None, out2=None):
     """The ``nt`` contract on the bounds-checked small-tile kernel (any M, N; K % 8 == 0)."""
     M, K = a.shape

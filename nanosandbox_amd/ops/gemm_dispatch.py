@@ -46,13 +46,9 @@ DETERMINISTIC = False
 
 F16 = torch.float16
 
-# NSA_NT_STRIP=1 (A/B only): N = 256 q + r (16 <= r <= 64) as the four-wave kernel over 256 q
-# columns plus the column-strip kernel over r (gemm.nt_strip).  Not the default: the strip
-# re-reads all of A from HBM for r columns (GPT-2 1.5B, M = 61440, N = 1600: 1536 columns
-# 230 us + strip 52 us vs 268 us whole width at K = 1600, 800 + 241 vs 923 at K = 6400;
-# profiles/r5_strip_v2.log), and the step ran 5074 vs 4604 ms with the first strip kernel
-# (profiles/r5_strip_v1.log)
-STRIP = os.environ.get("NSA_NT_STRIP", "0") == "1"
+# (round 5 tried GPT-2 1.5B's N = 1600 as 1536 columns on the four-wave kernel plus a
+# 64-column strip kernel: the strip re-reads all of A from HBM and the step ran slower,
+# 5074 vs 4604 ms; profiles/r5_strip_v1.log, r5_strip_v2.log.  Removed in round 6.)
 
 
 def _ok(*ts):
@@ -94,9 +90,6 @@ def _nt(a, b, epi=_gemm.NT_EPI_BF16, u=None, bias=None, op="fwd"):
     M, K = a.shape
     N = b.shape[0]
     k = kernel_for("fwd", M, N, K) if _ok(a, b, *([] if bias is None else [bias])) else "torch"
-    if k == "nt4" and epi == _gemm.NT_EPI_BF16 and STRIP and _gemm.strip_split_n(N):
-        _used.setdefault((op, M, N, K), "nt4+strip")
-        return _gemm.nt_strip(a, b, bias=bias)
     _used.setdefault((op, M, N, K), k)
     if k == "nt4":
         return _gemm.nt(a, b, epi=epi, u=u, bias=bias)

@@ -135,6 +135,7 @@ class Trainer:
         model.set_compute_dtype(self.compute_dtype,
                                 torch.float32 if c["fp32_residual"] else self.compute_dtype)
         model.grad_ckpt = c["grad_ckpt"]
+        model.recompute_mlp = c["recompute_mlp"]
         from . import ops as _ops
         _ops.set_deterministic(c["deterministic"])
         # the dropout kernels' device step counter: a fresh run starts its stream at 0, a
@@ -165,8 +166,10 @@ class Trainer:
             free, _ = torch.cuda.mem_get_info(torch.device(self.device))
             self.activation_plan = plan_grad_ckpt(
                 model.config.n_layer, model.config.n_embd, model.config.n_head, model.config.vocab_size,
-                c["batch_size"] * c["block_size"], free, fp32_residual=c["fp32_residual"], requested=c["grad_ckpt"])
+                c["batch_size"] * c["block_size"], free, fp32_residual=c["fp32_residual"], requested=c["grad_ckpt"],
+                recompute_mlp=c["recompute_mlp"])
             model.grad_ckpt = self.activation_plan.grad_ckpt
+            model.recompute_mlp = self.activation_plan.recompute_mlp
             if self.master:
                 print(self.activation_plan.describe())
         # compile=True: no Triton/Inductor on this stack; the micro-step (forward +

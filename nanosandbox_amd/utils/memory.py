@@ -47,24 +47,31 @@ class ActivationPlan:
     budget_bytes: int        # memory available for activations (0 = unknown)
     grad_ckpt: bool          # the decision
     reason: str
+    recompute_mlp: bool = False  # selective recomputation of the MLPs (between the two)
+    mlp_recompute_bytes: int = 0
 
     def describe(self) -> str:
         return (f"activation plan: {self.tokens} tokens/micro-step, resident {self.resident_bytes / GiB:.1f} GiB, "
-                f"checkpointed {self.ckpt_bytes / GiB:.1f} GiB, budget {self.budget_bytes / GiB:.1f} GiB -> "
-                f"grad_ckpt={self.grad_ckpt} ({self.reason})")
+                f"MLP-recompute {self.mlp_recompute_bytes / GiB:.1f} GiB, checkpointed {self.ckpt_bytes / GiB:.1f} "
+                f"GiB, budget {self.budget_bytes / GiB:.1f} GiB -> grad_ckpt={self.grad_ckpt} "
+                f"recompute_mlp={self.recompute_mlp} ({self.reason})")
 
 
-def layer_bytes_per_token(n_embd: int, n_head: int, fp32_residual: bool = True) -> int:
-    """Bytes one transformer block keeps per token for its backward (see module doc)."""
+def layer_bytes_per_token(n_embd: int, n_head: int, fp32_residual: bool = True, recompute_mlp: bool = False) -> int:
+    """Bytes one transformer block keeps per token for its backward (see module doc); with
+    ``recompute_mlp`` the MLP keeps only its input (the c_fc output and GELU output, 16C, are
+    recomputed in the backward: ops.functional.MLPFn)."""
     C = n_embd
     resid = 4 if fp32_residual else 2
-    return 2 * resid * C + 2 * 2 * C + 6 * C + 2 * C + 8 * C + 8 * C + 4 * n_head + 16
+    mlp = 0 if recompute_mlp else 8 * C + 8 * C
+    return 2 * resid * C + 2 * 2 * C + 6 * C + 2 * C + mlp + 4 * n_head + 16
 
 
 def activation_bytes(n_layer: int, n_embd: int, n_head: int, vocab_size: int, tokens: int,
-                     fp32_residual: bool = True, grad_ckpt: bool = False, calibration: float = 1.0) -> int:
+                     fp32_residual: bool = True, grad_ckpt: bool = False, calibration: float = 1.0,
+                     recompute_mlp: bool = False) -> int:
     """Estimated peak activation memory (bytes) of one forward + backward micro-step."""
-    per_layer = layer_bytes_per_token(n_embd, n_head, fp32_residual)
+    per_layer = layer_bytes_per_token(n_embd, n_head, fp32_residual, recompute_mlp and not grad_ckpt)
     resid = 4 if fp32_residual else 2
     head = 2 * 2 * vocab_size + (resid + 2) * n_embd  # logits + loss-gradient buffers, ln_f in/out
     if grad_ckpt:
@@ -76,25 +83,35 @@ def activation_bytes(n_layer: int, n_embd: int, n_head: int, vocab_size: int, to
 
 def plan_grad_ckpt(n_layer: int, n_embd: int, n_head: int, vocab_size: int, tokens: int, free_bytes: int,
                    fp32_residual: bool = True, requested: bool = False, headroom: float = 0.9,
-                   calibration: float = 1.0) -> ActivationPlan:
-    """Checkpoint only if the resident estimate exceeds ``headroom`` x the free memory.
+                   calibration: float = 1.0, recompute_mlp: bool = False) -> ActivationPlan:
+    """Resident if it fits ``headroom`` x the free memory; else selective recomputation of the
+    MLPs (one extra c_fc GEMM per layer) if that fits; else per-block checkpointing (a whole
+    extra forward).
 
-    ``requested`` (config ``grad_ckpt=True``) is always honoured; ``free_bytes`` = 0
-    means unknown (CPU runs): no automatic change."""
+    ``requested`` (config ``grad_ckpt=True``) and ``recompute_mlp`` (config key of the same
+    name) are always honoured; ``free_bytes`` = 0 means unknown (CPU runs): no automatic
+    change."""
     kw = dict(n_layer=n_layer, n_embd=n_embd, n_head=n_head, vocab_size=vocab_size, tokens=tokens,
               fp32_residual=fp32_residual, calibration=calibration)
     res = activation_bytes(grad_ckpt=False, **kw)
+    sel = activation_bytes(grad_ckpt=False, recompute_mlp=True, **kw)
     ck = activation_bytes(grad_ckpt=True, **kw)
     budget = int(headroom * free_bytes)
+
+    def plan(gc, rm, why):
+        return ActivationPlan(tokens, res, ck, budget, gc, why, recompute_mlp=rm, mlp_recompute_bytes=sel)
     if requested:
-        return ActivationPlan(tokens, res, ck, budget, True, "requested by config")
+        return plan(True, False, "requested by config")
+    if recompute_mlp:
+        return plan(False, True, "MLP recompute requested by config")
     if free_bytes <= 0:
-        return ActivationPlan(tokens, res, ck, budget, False, "free memory unknown")
+        return plan(False, False, "free memory unknown")
     if res <= budget:
-        return ActivationPlan(tokens, res, ck, budget, False, "fits resident")
-    return ActivationPlan(tokens, res, ck, budget, True,
-                          "resident estimate exceeds the budget" + ("" if ck <= budget else
-                                                                    "; checkpointed may not fit either"))
+        return plan(False, False, "fits resident")
+    if sel <= budget:
+        return plan(False, True, "resident estimate exceeds the budget; MLP recompute fits")
+    return plan(True, False, "resident and MLP-recompute estimates exceed the budget" +
+                ("" if ck <= budget else "; checkpointed may not fit either"))
 
 
 def model_state_bytes(n_layer: int, n_embd: int, vocab_size: int, block_size: int) -> int:

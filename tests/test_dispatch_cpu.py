@@ -58,18 +58,6 @@ def test_gpt2_shapes_take_the_persistent_kernels():
     assert gemm_dispatch.kernel_for("fwd", 256, 192, 60) == "torch"  # K % 8 != 0: out of contract
 
 
-def test_strip_split_rule():
-    """N = 256 q + r with 16 <= r <= 64, r % 16 == 0: the four-wave kernel over 256 q columns
-    and the column-strip kernel over r (GPT-2 1.5B's 1600 = 1536 + 64); every other width
-    stays on one kernel."""
-    assert gemm.strip_split_n(1600) == 1536
-    assert gemm.strip_split_n(1552) == 1536
-    assert gemm.strip_split_n(1328) == 1280
-    assert gemm.strip_split_n(320) == 256
-    for n in (768, 1024, 2304, 3072, 4800, 6400, 50304, 1280, 256, 80, 1608, 1680, 1540):
-        assert gemm.strip_split_n(n) == 0, n
-
-
 def test_small_vocab_lds_scatter_rule():
     """The LDS-privatised scatter-add (segsum.h seg_lds_kernel) takes a table whose padded
     V x (C + C/8) fp32 copy fits its 128 KB LDS budget: the char config's 65 x 384 (and the

@@ -629,7 +629,7 @@ def flash_variant(kernels):
         stack.pop().__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6", "auto"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6", "v7", "auto"])
 @pytest.mark.parametrize("B,T,H,D", [(2, 256, 3, 64), (1, 200, 2, 64), (2, 128, 2, 32), (1, 1024, 2, 64),
                                      (1, 77, 1, 32), (1, 192, 2, 128)])
 def test_flash_attention(kernels, flash_variant, B, T, H, D, fwd):
@@ -677,7 +677,7 @@ def _flash_fwd_raw(qkv, H, out_nan=True):
     return y, lse
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6", "v7"])
 @pytest.mark.parametrize("T,D", [(1024, 64), (320, 64), (200, 64), (64, 64), (77, 32), (192, 128), (1024, 32)])
 @pytest.mark.parametrize("layout", ["tile", "row"])
 def test_flash_fwd_exact_structure(kernels, flash_variant, T, D, fwd, layout):
@@ -755,7 +755,7 @@ def test_flash_bwd_exact_structure(kernels, flash_variant, T, bwd):
         assert (err <= 2 ** -6 * m + 1e-5).all(), (name, err.max().item())
 
 
-@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6"])
+@pytest.mark.parametrize("fwd", ["v1", "v3", "v4", "v5", "v6", "v7"])
 @pytest.mark.parametrize("pattern", ["rising", "falling", "spikes", "negative", "overflow", "underflow"])
 def test_flash_attention_deferred_rescale(kernels, flash_variant, pattern, fwd):
     """Score patterns that drive the forward's deferred max-rescale branch.
@@ -861,7 +861,7 @@ def test_flash_bwd_v2_matches_v1(kernels, flash_variant, p, T):
         assert e < 1e-2, f"d{name}: v2 vs v1 rel err {e}"
 
 
-@pytest.mark.parametrize("fwd", ["v5", "v6"])
+@pytest.mark.parametrize("fwd", ["v5", "v6", "v7"])
 def test_flash_fwd_v5_fallback_mid_sequence(kernels, flash_variant, fwd):
     """v5 / v6 switch a wave from fast (m = 0) to exact tiles when a later tile overflows:
     the first tiles ran with m = 0 and are then rescaled by the exact path's max."""
@@ -1137,54 +1137,6 @@ def test_deterministic_kernels_match_default(kernels):
             ops.set_deterministic(False)
     assert torch.equal(grads[1][0], grads[2][0]) and torch.equal(grads[1][1], grads[2][1])
     assert rel_err(grads[1][0], grads[0][0]) < 1e-5 and rel_err(grads[1][1], grads[0][1]) < 1e-6
-
-
-@pytest.mark.parametrize("H", [False, True])
-@pytest.mark.parametrize("M,NS,K,bias", [(61440 // 16, 64, 1600, False), (1000, 64, 640, True), (777, 16, 128, True),
-                                         (300, 48, 64, False)])
-def test_gemm_strip_raw(kernels, H, M, NS, K, bias):
-    """nsa_gemm_strip into columns 0..NS of a NaN-prefilled [M, NS + 40] buffer (row stride
-    NS + 40): the strip matches fp32 per element (one output rounding), the other columns
-    stay untouched; ragged M (rows past a 64-row block), NS of 1-4 fragments, bias."""
-    from nanosandbox_amd.ops import _lib
-    dt = torch.float16 if H else BF
-    torch.manual_seed(4)
-    a = (torch.randn(M, K, device=DEV) * 0.5).to(dt)
-    b = (torch.randn(NS, K, device=DEV) * 0.5).to(dt)
-    bs = (torch.randn(NS, device=DEV)).to(dt) if bias else None
-    ldc = NS + 40
-    c = torch.full((M, ldc), float("nan"), device=DEV, dtype=dt)
-    _lib.call("nsa_gemm_strip_h" if H else "nsa_gemm_strip", _lib.ptr(a), K, _lib.ptr(b), K, _lib.ptr(c), ldc,
-              _lib.ptr(bs), M, NS, K, _lib.stream())
-    torch.cuda.synchronize()
-    ref = a.float() @ b.float().t() + (bs.float() if bias else 0.0)
-    got = c[:, :NS].float()
-    assert not torch.isnan(got).any()
-    ulp = 2.0 ** (-10 if H else -7)
-    assert ((got - ref).abs() <= ulp * ref.abs() + 1e-3 * (a.float().abs() @ b.float().abs().t())).all()
-    assert torch.isnan(c[:, NS:].float()).all()
-
-
-@pytest.mark.parametrize("N", [1600, 1552, 1328])
-def test_nt_strip_dispatch(kernels, monkeypatch, N):
-    """NSA_NT_STRIP=1 (A/B form): N = 256 q + r (16 <= r <= 64) as the four-wave kernel over
-    256 q columns plus the strip kernel, one output; recorded as "nt4+strip"; equal to the
-    whole-width four-wave result."""
-    from nanosandbox_amd.ops import gemm, gemm_dispatch
-    monkeypatch.setattr(gemm_dispatch, "STRIP", True)
-    torch.manual_seed(5)
-    M, K = 1024, 640
-    a = (torch.randn(M, K, device=DEV) * 0.5).to(BF)
-    w = (torch.randn(N, K, device=DEV) * 0.5).to(BF)
-    bias = torch.randn(N, device=DEV).to(BF)
-    gemm_dispatch._used.clear()
-    y = gemm_dispatch.fwd(a, w, bias)
-    assert gemm_dispatch.kernels_used()[("fwd", M, N, K)] == "nt4+strip"
-    full = gemm.nt(a, w, bias=bias)
-    ref = a.float() @ w.float().t() + bias.float()
-    assert rel_err(y, ref) < 1e-2
-    # same fp32 accumulation order per element up to the K-step grouping: within an ulp
-    assert ((y.float() - full.float()).abs() <= 2 ** -7 * full.float().abs() + 1e-3).all()
 
 
 @pytest.mark.parametrize("split", [False, True])

@@ -23,9 +23,21 @@ def test_plan_keeps_resident_when_it_fits_in_hbm():
     free = 255 * GiB  # MI355X after the 1.5B model's parameters, grads and Adam state
     p = plan_grad_ckpt(tokens=60 * 1024, free_bytes=free, **XL)
     assert not p.grad_ckpt and p.reason == "fits resident"
+    # 120 x 1024 no longer fits resident; the MLP-recompute tier does (one c_fc GEMM per
+    # layer recomputed instead of a whole extra forward)
     p = plan_grad_ckpt(tokens=120 * 1024, free_bytes=free, **XL)
-    assert p.grad_ckpt and p.ckpt_bytes <= p.budget_bytes
+    assert not p.grad_ckpt and p.recompute_mlp and p.mlp_recompute_bytes <= p.budget_bytes < p.resident_bytes
+    assert "recompute_mlp=True" in p.describe()
+    p = plan_grad_ckpt(tokens=240 * 1024, free_bytes=free, **XL)
+    assert p.grad_ckpt and not p.recompute_mlp and p.ckpt_bytes <= p.budget_bytes
     assert "grad_ckpt=True" in p.describe()
+
+
+def test_mlp_recompute_drops_the_mlp_activations():
+    C, H = 1600, 25
+    assert layer_bytes_per_token(C, H) - layer_bytes_per_token(C, H, recompute_mlp=True) == 16 * C
+    p = plan_grad_ckpt(tokens=1024, free_bytes=255 * GiB, recompute_mlp=True, **XL)
+    assert p.recompute_mlp and not p.grad_ckpt
 
 
 def test_plan_honours_request_and_unknown_memory():

@@ -206,3 +206,30 @@ def test_fp16_loss_scale_skips_overflowing_steps(kernels, tmp_path):
             break
     assert not torch.equal(tr.store.master, w0)  # a step went through once the scale fit
     assert tr.scaler.scale < 2.0 ** 59 and tr.scaler.skipped >= 1
+
+
+def test_recompute_mlp_matches_resident_bitwise(kernels, tmp_path):
+    """recompute_mlp=True (selective recomputation): the MLP keeps only its
+    input and re-runs c_fc + GELU in the backward.  The recomputed gelu(u) / gelu'(u) come from
+    the same kernel on the same operands, so with deterministic reductions the trained
+    parameters are bitwise those of the resident run; the planner reports the mode."""
+    from nanosandbox_amd import ops
+    from nanosandbox_amd.train import Trainer
+
+    def run(rm):
+        torch.manual_seed(0)
+        tr = Trainer(_cfg(tmp_path, compile=False, dropout=0.1, bias=True, max_iters=5, eval_interval=1000,
+                          out_dir=str(tmp_path / f"rm{int(rm)}"), seed=77, deterministic=True, recompute_mlp=rm))
+        assert tr.raw_model.recompute_mlp == rm
+        X, Y = tr.batches.get_batch("train")
+        for _ in range(3):
+            _, _, X, Y = tr.train_step(X, Y)
+        torch.cuda.synchronize()
+        return {k: v.detach().float().cpu().clone() for k, v in tr.raw_model.state_dict().items()}
+
+    try:
+        a, b = run(False), run(True)
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    finally:
+        ops.set_deterministic(False)
