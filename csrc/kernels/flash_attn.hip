@@ -140,18 +140,17 @@ __device__ __forceinline__ void attn_order(int n_tiles, int BH, int order, int& 
 
 // Kernel selection, resolved once (first launch) from the environment and changed only
 // through nsa_flash_set_variant (tests / A/B scripts):
-//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v3 | v4 | v5 | v6: D = 64 forward kernel;
-//         auto = v5 without dropout once the grid has >= 4096 v3
-//         workgroups, else v1 (fwd_launch); v3 = 64 queries per wave, one K/V tile per
-//         barrier; v4 = two tiles per barrier; v5 = v4's geometry with fast tiles (no running
-//         max while scores stay in range); v6 = v1's geometry with fast tiles
+//   fwd   NSA_FLASH_FWD = auto (default) | v1 | v5: D = 64 forward kernel; auto = v5 without
+//         dropout once the grid has >= 4096 workgroups, else v1 (fwd_launch); v5 = 64 queries
+//         per wave, two K/V tiles per barrier, fast tiles (no running max while scores stay in
+//         range); v1 = 32 queries per wave, exact online softmax, dropout
 //   bwd   NSA_FLASH_BWD = v3 (default) | v2 | v1: D = 64 backward; v3 = v2 with the dK/dV
 //         kernel taking two query slices per barrier; v1 = the generic kernels
 //         (software-pipelining the dQ tile's / the dK/dV slice pair's MFMAs under each
 //         other's VALU with sched_group_barrier measured no gain / a spilling kernel:
 //         docs/performance.md, round 5)
 //   order NSA_ATTN_ORDER = 0 (default) | 1: workgroup order (attn_order)
-enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V3 = 3, FWD_V4 = 4, FWD_V5 = 5, FWD_V6 = 6, FWD_V7 = 7 };
+enum { FWD_AUTO = 0, FWD_V1 = 1, FWD_V5 = 5 };
 enum { BWD_V1 = 1, BWD_V2 = 2, BWD_V3 = 3 };
 struct FlashConfig {
   int fwd, bwd, order;
@@ -167,7 +166,7 @@ FlashConfig& flash_config() {
   static FlashConfig c = [] {
     FlashConfig d{FWD_AUTO, BWD_V3, ATTN_ORDER_DEFAULT};
     if (const char* e = getenv("NSA_FLASH_FWD"))
-      d.fwd = (e[0] == 'v' && (e[1] == '1' || (e[1] >= '3' && e[1] <= '7'))) ? e[1] - '0' : FWD_AUTO;
+      d.fwd = (e[0] == 'v' && (e[1] == '1' || e[1] == '5')) ? e[1] - '0' : FWD_AUTO;
     if (const char* e = getenv("NSA_FLASH_BWD"))
       d.bwd = (e[0] == 'v' && e[1] >= '1' && e[1] <= '3') ? e[1] - '0' : BWD_V3;
     if (const char* e = getenv("NSA_ATTN_ORDER")) d.order = (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
@@ -353,56 +352,6 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
   }
 }
 
-// The v5 fast tile (scores without the row max while they stay in range, see
-// fwd_tile5 below) for ONE 32-query block per wave: the v1 kernel's geometry (4 waves per
-// SIMD), "v6".  Returns false (nothing accumulated) when the tile leaves range.
-template <bool MASK>
-__device__ __forceinline__ bool fwd_tile_fast(const char* kt, const char* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2],
-                                              float& l_i, int kv0, int qpos, int h, int r, int lane,
-                                              float scale_log2) {
-  constexpr int D = 64;
-  f32x16 st[2];
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[sb] = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-  }
-  bf16x8 pf[2][2];
-  float acc[2] = {0.0f, 0.0f};
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) st[sb][i] *= scale_log2;  // scalar v_mul_f32 (see NSA_FA_NOSLP)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float sv = st[sb][i];
-      if constexpr (MASK) {
-        if (kv0 + 32 * sb + acc_row(i, h) > qpos) sv = -INFINITY;
-      }
-      const float p = fast_exp2(sv);
-      acc[sb] += p;
-      pf[sb][i >> 3][i & 7] = fa_elt(p);
-    }
-  }
-  const float rs = half_swap_sum(acc[0] + acc[1]);
-  const float ln = l_i + rs;
-  // bf16 P holds any fp32 value; fp16 P only up to 65504 (the fp16 build's bound)
-  const float hi = kFaH ? 0x1p15f : 0x1p64f, lo = kFaH ? 0x1p-8f : 0x1p-60f;
-  if (__builtin_amdgcn_ballot_w64(!(rs <= hi && ln >= lo))) return false;
-  l_i = ln;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s], o[dt]);
-    }
-  }
-  return true;
-}
-
 // K/V tile staging through registers (T14 split: issue before compute, write after)
 #define NSA_FWD_STAGE_LOAD(J)                                                                   \
   _Pragma("unroll") for (int c = 0; c < CHUNKS_PER_THREAD; ++c) {                               \
@@ -428,10 +377,8 @@ __device__ __forceinline__ bool fwd_tile_fast(const char* kt, const char* vt, co
 // T14 split intends, but hipcc sinks the staging loads out of the loop head into the
 // latch, right before their LDS writes (the tile compute sits in branches), so every
 // tile waited out a full global-memory round trip.
-// FAST (D = 64 with DMA, no dropout): fast tiles (fwd_tile_fast) until a tile leaves range,
-// exact tiles from then on ("v6")
-template <int D, bool DROP, bool DMA = false, bool FAST = false>
-__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA && !FAST ? 4 : 3) : 2) void flash_fwd_kernel(
+template <int D, bool DROP, bool DMA = false>
+__global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA ? 4 : 3) : 2) void flash_fwd_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out, float* __restrict__ lse_out, int B, int T, int H,
     float scale_log2, uint32_t drop_thresh, float drop_scale, uint64_t seed, int order) {
   constexpr int BN = 64;
@@ -473,8 +420,7 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA && !FAST ? 4 : 3) : 
   f32x16 o[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
-  float m_i = FAST ? 0.0f : -1e30f, l_i = 0.0f;
-  bool fast = FAST;  // wave-uniform
+  float m_i = -1e30f, l_i = 0.0f;
 
   const int kv_end = min(T, q0 + 128);
   const int n_tiles = (kv_end + BN - 1) / BN;
@@ -520,34 +466,10 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA && !FAST ? 4 : 3) : 
       issue(min(j + 1, n_tiles - 1), cur ^ 1);
       const char* kt = smem + cur * TILE_BYTES;
       const char* vt = smem + (2 + cur) * TILE_BYTES;
-      if constexpr (FAST && D == 64 && !DROP) {
-        const bool full = kv0 + BN - 1 <= q0w, diag = !full && kv0 <= q0w + 31;
-        if (full || diag) {
-          const bool ok = fast && (full ? fwd_tile_fast<false>(kt, vt, qf, o, l_i, kv0, qpos, h, r, lane, scale_log2)
-                                        : fwd_tile_fast<true>(kt, vt, qf, o, l_i, kv0, qpos, h, r, lane, scale_log2));
-          if (!ok) {
-            if (fast) {  // hand-over to exact tiles: m' = log2(l) (see fwd5_to_exact)
-              if (l_i > 0.0f) {
-                const float mp = __log2f(l_i), f = fast_exp2(-mp);
-                l_i *= f;
-                o[0] *= f;
-                o[1] *= f;
-                m_i = mp / scale_log2;
-              } else {
-                m_i = -1e30f;
-              }
-              fast = false;
-            }
-            if (full) fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-            else fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-          }
-        }
-      } else {
-        if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
-          fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-        else if (kv0 <= q0w + 31)  // the wave's diagonal tile
-          fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
-      }
+      if (kv0 + BN - 1 <= q0w)  // wave-uniform: whole tile visible to every query of the wave
+        fwd_tile<D, false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
+      else if (kv0 <= q0w + 31)  // the wave's diagonal tile
+        fwd_tile<D, true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qpos, h, r, lane, scale_log2, dr);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -609,8 +531,7 @@ __global__ __launch_bounds__(256, (D <= 64 && !DROP) ? (DMA && !FAST ? 4 : 3) : 
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const bf16x8 (&qf)[2][4],
                                           f32x16 (&o)[2][2], float (&m_i)[2], float (&l_i)[2], int kv0, int qposA,
-                                          int h, int r, int lane, float scale_log2, const DropArgs& dr,
-                                          unsigned long long* stamp = nullptr) {
+                                          int h, int r, int lane, float scale_log2, const DropArgs& dr) {
   constexpr int D = 64;
   f32x16 st[2][2];  // [block][key sub-block]
 #pragma unroll
@@ -624,9 +545,6 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
       st[1][sb] = mfma(kf, qf[1][ks], st[1][sb]);
     }
   }
-#if NSA_FWD3_STAMPS
-  stamp[0] = __builtin_amdgcn_s_memtime();
-#endif
   float mt[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -677,9 +595,6 @@ __device__ __forceinline__ void fwd_tile2(const char* kt, const char* vt, const 
     }
     l_i[blk] += half_swap_sum(rs);
   }
-#if NSA_FWD3_STAMPS
-  stamp[1] = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
   for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
@@ -838,7 +753,13 @@ __device__ __forceinline__ void fwd5_to_exact(f32x16 (&o)[2][2], float (&m_i)[2]
 }
 
 // Workgroup = 4 waves x 64 queries, 4-slot K/V ring filled by LDS-DMA, two tiles per
-// barrier (flash_fwd3_kernel<false, 4, true>'s schedule).  No dropout (dropout runs v1/v3).
+// barrier (round 4's v4 schedule, whose exact pair tile fwd_tile2 is v5's fallback).
+// No dropout (dropout runs v1).
+// Probe build only (-DNSA_PROBE_SKIP_TILE=1, build_variant): skip key tile 1 of every
+// workgroup -- wrong output, used to show the test suite catches a dropped causal tile.
+#ifndef NSA_PROBE_SKIP_TILE
+#define NSA_PROBE_SKIP_TILE 0
+#endif
 #ifndef NSA_PROBE_KV_SHARED
 #define NSA_PROBE_KV_SHARED 0  // probe build: every (b, h) reads (0, 0)'s K/V (wrong output; traffic probe)
 #endif
@@ -930,6 +851,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int jj = j + u;
+      if (NSA_PROBE_SKIP_TILE && jj == 1) continue;  // test-suite probe: one causal tile dropped
       if (jj < n_tiles) {
         const int kv0 = jj * BN;
         const char* kt = smem + (jj % 4) * TILE_BYTES;
@@ -970,519 +892,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd5_kernel(const bf16_t* __rest
         }
       }
       if (h == 0) lse_out[(int64_t)bh * T + qp] = (m_i[blk] * sl_exact + __log2f(l_i[blk])) * 0.6931471805599453f;
-    }
-  }
-}
-
-// =============================================================================
-// forward v7 (D = 64): v5's fast tiles at ONE wave per SIMD, the wave's two 32-query
-// blocks software-pipelined one tile apart (cdna_hip_programming.md "4-wave,
-// one-wave-per-SIMD" structure).
-//
-// v5 runs two 254-VGPR waves per SIMD; each wave's tile is a serial chain (S MFMAs ->
-// softmax VALU -> P·V MFMAs) and the overlap is left to the other wave (28 % MFMA busy,
-// profiles/r5_attn_pmc.md).  Here a workgroup (4 waves x 64 queries) owns the CU and each
-// wave overlaps its OWN two chains: block A runs one K/V tile ahead of block B, so in
-// iteration j block A's scores for tile j+1 and block B's P·V of tile j (MFMA) sit beside
-// block B's softmax of tile j and block A's softmax of tile j+1 (VALU), with no branch
-// between them.  Ring: 4 K/V slots by LDS-DMA, one barrier per tile (tile j+1 landed for
-// every wave; tile j-1's slot free for tile j+3).  Fast tiles as v5 (m = 0 while the scores
-// stay in range); a tile that leaves the range contributes nothing (its P is zeroed, so no
-// branch sits between the softmax and the P·V), is redone exactly, and both blocks continue
-// on exact tiles (v1's fwd_tile, one per block and iteration).  No dropout.
-// =============================================================================
-// one 32-query block: S^T of one K tile (8 MFMAs)
-__device__ __forceinline__ void fwd7_scores(const char* kt, const bf16x8 (&qf)[4], f32x16 (&st)[2], int h, int r) {
-  constexpr int D = 64;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    st[sb] = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) st[sb] = mfma(as_frag(lds_b128(kt, swz<D>(32 * sb + r, 2 * ks + h))), qf[ks], st[sb]);
-  }
-}
-
-// one block's fast softmax: P fragments and the row sum; ok = the tile stayed in the fast
-// range (wave-uniform).  A tile that is not ok gets P = 0 (its P·V adds nothing) and leaves l.
-template <bool MASK>
-__device__ __forceinline__ bool fwd7_soft(const f32x16 (&st)[2], bf16x8 (&pf)[2][2], float& l_i, int kv0, int qpos,
-                                          int h, float scale_log2) {
-  float acc[2] = {0.0f, 0.0f};
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float s = st[sb][i] * scale_log2;
-      if constexpr (MASK) {
-        if (kv0 + 32 * sb + acc_row(i, h) > qpos) s = -INFINITY;
-      }
-      const float p = fast_exp2(s);
-      acc[sb] += p;
-      pf[sb][i >> 3][i & 7] = fa_elt(p);
-    }
-  }
-  const float rs = half_swap_sum(acc[0] + acc[1]);
-  const float ln = l_i + rs;
-  const float hi = kFaH ? 0x1p15f : 0x1p64f, lo = kFaH ? 0x1p-8f : 0x1p-60f;
-  const bool ok = __builtin_amdgcn_ballot_w64(!(rs <= hi && ln >= lo)) == 0;
-  // branch-free: a uniform branch here would split the block the scheduler interleaves
-  const uint32_t keep = ok ? 0xffffffffu : 0u;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      uint4 u = __builtin_bit_cast(uint4, pf[sb][s]);
-      u.x &= keep;
-      u.y &= keep;
-      u.z &= keep;
-      u.w &= keep;
-      pf[sb][s] = __builtin_bit_cast(bf16x8, u);
-    }
-  l_i = ok ? ln : l_i;
-  return ok;
-}
-
-// O accumulators pinned to AGPRs: an asm MFMA with a tied "+a" accumulator.  With the
-// builtin hipcc kept O in AGPRs but moved it through VGPRs around every P·V (96
-// v_accvgpr moves per iteration).  The s_nop 1 covers a VALU write of P (the B operand)
-// right before the MFMA; consumers of O outside these MFMAs wait with fwd7_drain().
-__device__ __forceinline__ void fwd7_mfma_acc(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  if constexpr (kFaH) asm("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// the asm MFMAs' results -> VALU / v_accvgpr_read: let the last ones drain (16 passes)
-__device__ __forceinline__ void fwd7_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-
-// one block: O^T += V^T · P^T of one V tile (8 MFMAs)
-__device__ __forceinline__ void fwd7_pv(const char* vt, const bf16x8 (&pf)[2][2], f32x16 (&o)[2], int h, int lane) {
-  constexpr int D = 64;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r0 = 32 * sb + 16 * s + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fwd7_mfma_acc(o[dt], tr_frag<D>(vt, r0, r0 + 8, 32 * dt, lane), pf[sb][s]);
-    }
-  }
-}
-
-// fast (m = 0) -> exact for one block (fwd5_to_exact for a single block)
-__device__ __forceinline__ void fwd7_to_exact(f32x16 (&o)[2], float& m_i, float& l_i, float sl) {
-  if (l_i > 0.0f) {
-    const float mp = __log2f(l_i);
-    const float f = fast_exp2(-mp);
-    l_i *= f;
-    o[0] *= f;
-    o[1] *= f;
-    m_i = mp / sl;
-  } else {
-    m_i = -1e30f;
-  }
-}
-
-__global__ __launch_bounds__(256, 1) void flash_fwd7_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2, int order) {
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int NS = 4;
-  constexpr int TILE_BYTES = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
-
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, order, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the loop bounds below depend on it
-  const int h = lane >> 5, r = lane & 31;
-  const int q0 = qt * 256;
-  const int q0w = q0 + 64 * w;
-  const int qA = q0w + r, qB = qA + 32;  // block A = queries q0w .. +31, block B the next 32
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-
-  bf16x8 qfA[4], qfB[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qfA[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)min(qA, T - 1) * row_stride + 16 * ks + 8 * h));
-    qfB[ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)min(qB, T - 1) * row_stride + 16 * ks + 8 * h));
-  }
-  f32x16 oA[2], oB[2];
-  oA[0] = oA[1] = oB[0] = oB[1] = f32x16{};
-  float mA = 0.0f, lA = 0.0f, mB = 0.0f, lB = 0.0f;
-
-  const int kv_end = min(T, q0 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-  const int jd = min(q0w / BN, n_tiles - 1);  // both blocks' diagonal tile (earlier tiles: fully visible)
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int prow = 16 * w + (lane >> 3);
-  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
-  const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
-  const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
-  auto issue = [&](int jt) {
-    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
-    uint32_t o0 = koff0, o8 = koff8;
-    if (jt * BN + BN > T) {
-      const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
-      o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
-      o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
-    }
-    const uint32_t kb = lds0 + (uint32_t)((jt % NS) * TILE_BYTES + 16 * w * 128);
-    const uint32_t vb = kb + NS * TILE_BYTES;
-    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
-    glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
-    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
-    glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
-  };
-  // top of iteration j: tile j+1 landed for every wave, tile j-1's slot free -> tile j+3 into it
-  auto top = [&](int j) {
-    vm_wait(4 * max(0, min(j + 2, n_tiles - 1) - (j + 1)));
-    __builtin_amdgcn_s_barrier();
-    if (j + 3 < n_tiles) issue(j + 3);
-  };
-  auto kslot = [&](int j) -> const char* { return smem + (j % NS) * TILE_BYTES; };
-  auto vslot = [&](int j) -> const char* { return smem + (NS + j % NS) * TILE_BYTES; };
-
-  asm volatile("" ::"v"(qfA[0]), "v"(qfA[1]), "v"(qfA[2]), "v"(qfA[3]), "v"(qfB[0]), "v"(qfB[1]), "v"(qfB[2]),
-               "v"(qfB[3]));  // Q landed before the DMA
-  const DropArgs dr{0u, 1.0f, 0ull, bh, T};
-  for (int t = 0; t < 3 && t < n_tiles; ++t) issue(t);
-  vm_wait(4 * min(2, n_tiles - 1));  // tile 0 landed (tiles 1, 2 may fly)
-  __builtin_amdgcn_s_barrier();
-
-  // Schedule (block A one tile ahead of block B), iteration j, two steps split by a
-  // sched_barrier (each step: VALU of one softmax beside 16 MFMAs of the other chain):
-  //   step 1: softmax B(j)        | scores A(j+1), P·V A(j)
-  //   step 2: softmax A(j+1)      | P·V B(j), scores B(j+1)
-  // Tiles read: K(j+1), V(j) -- both resident after top(j).  Block A's P of tile j comes
-  // from step 2 of iteration j-1 (the prologue for j = 0).
-  f32x16 sA[2], sB[2];
-  bf16x8 pA[2][2], pB[2][2];
-  bool okA = true, okB = true;
-  fwd7_scores(kslot(0), qfA, sA, h, r);
-  okA = jd == 0 ? fwd7_soft<true>(sA, pA, lA, 0, qA, h, scale_log2) : fwd7_soft<false>(sA, pA, lA, 0, qA, h, scale_log2);
-  fwd7_scores(kslot(0), qfB, sB, h, r);
-  const bool pro_ok = okA;
-  int j = 0;
-  // MASKA: block A's next tile (j+1) is its diagonal
-  auto body = [&](auto MASKA_) {
-    constexpr bool MASKA = decltype(MASKA_)::value;
-    okB = fwd7_soft<false>(sB, pB, lB, j * BN, qB, h, scale_log2);
-    fwd7_scores(kslot(j + 1), qfA, sA, h, r);
-    fwd7_pv(vslot(j), pA, oA, h, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    okA = fwd7_soft<MASKA>(sA, pA, lA, (j + 1) * BN, qA, h, scale_log2);
-    fwd7_pv(vslot(j), pB, oB, h, lane);
-    fwd7_scores(kslot(j + 1), qfB, sB, h, r);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  bool last_done = false;
-  if (pro_ok) {
-    for (; j + 1 < jd; ++j) {  // both blocks on fully visible tiles
-      top(j);
-      body(std::false_type{});
-      if (!(okA && okB)) break;
-    }
-    if (okA && okB && jd >= 1 && j == jd - 1) {  // block A's next tile is its diagonal
-      top(j);
-      body(std::true_type{});
-      if (okA && okB) ++j;
-    }
-    if (okA && okB && j == jd) {  // block A's diagonal P·V, block B's diagonal tile
-      top(j);
-      okB = fwd7_soft<true>(sB, pB, lB, j * BN, qB, h, scale_log2);
-      fwd7_pv(vslot(j), pA, oA, h, lane);
-      fwd7_pv(vslot(j), pB, oB, h, lane);
-      last_done = okB;
-      if (okB) ++j;
-    }
-  }
-  if (!pro_ok || !(okA && okB)) {
-    // a fast tile left the range in iteration j (its barrier passed; tiles j, j+1 resident):
-    // finish what was valid, then both blocks continue on exact tiles (block B on tile i,
-    // block A on tile i+1 in iteration i)
-    const bool prologue = !pro_ok;  // block A's tile 0 failed before the first iteration
-    const bool lastit = pro_ok && j == jd && !last_done && okA;  // only block B's diagonal failed
-    int ta, tb;
-    if (prologue) {
-      ta = 0;
-      tb = 0;
-    } else if (lastit) {
-      ta = jd + 1;  // block A finished (its diagonal P·V ran in this iteration)
-      tb = jd;
-    } else {
-      if (okA) fwd7_pv(vslot(j + 1), pA, oA, h, lane);  // block A's tile j+1 was good: its P·V
-      ta = okA ? j + 2 : j + 1;
-      tb = okB ? j + 1 : j;
-    }
-    fwd7_drain();
-    fwd7_to_exact(oA, mA, lA, scale_log2);
-    fwd7_to_exact(oB, mB, lB, scale_log2);
-    bool open = !prologue;  // iteration j's barrier is behind us (not for a prologue failure)
-    for (int i = prologue ? 0 : j; i < n_tiles; ++i) {
-      if (!open) top(i);
-      open = false;
-      if (tb == i && i <= jd) {
-        if (i < jd) fwd_tile<64, false, false>(kslot(i), vslot(i), qfB, oB, mB, lB, i * BN, qB, h, r, lane, scale_log2, dr);
-        else fwd_tile<64, true, false>(kslot(i), vslot(i), qfB, oB, mB, lB, i * BN, qB, h, r, lane, scale_log2, dr);
-        ++tb;
-      }
-      // block A: tile i (only after a prologue failure) and / or tile i + 1, both resident
-      for (int u = 0; u < 2; ++u) {
-        const int ti = i + u;
-        if (ta == ti && ti <= jd && ti < n_tiles && (u == 1 || prologue)) {
-          if (ti < jd)
-            fwd_tile<64, false, false>(kslot(ti), vslot(ti), qfA, oA, mA, lA, ti * BN, qA, h, r, lane, scale_log2, dr);
-          else
-            fwd_tile<64, true, false>(kslot(ti), vslot(ti), qfA, oA, mA, lA, ti * BN, qA, h, r, lane, scale_log2, dr);
-          ++ta;
-        }
-      }
-    }
-    j = n_tiles;
-  }
-  for (; j < n_tiles; ++j) top(j);  // tiles past this wave's diagonal: barriers and DMA only
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  fwd7_drain();
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qp = blk ? qB : qA;
-    if (qp < T) {
-      const float l = blk ? lB : lA, m = blk ? mB : mA;
-      const float inv_l = 1.0f / l;
-      bf16_t* orow = out + ((int64_t)b * T + qp) * C + hh * D;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const f32x16& od = blk ? oB[dt] : oA[dt];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = 32 * dt + 8 * g + 4 * h;
-          uint2 u;
-          u.x = pk2<kFaH>(od[4 * g + 0] * inv_l, od[4 * g + 1] * inv_l);
-          u.y = pk2<kFaH>(od[4 * g + 2] * inv_l, od[4 * g + 3] * inv_l);
-          *reinterpret_cast<uint2*>(orow + d) = u;
-        }
-      }
-      if (h == 0) lse_out[(int64_t)bh * T + qp] = (m * scale_log2 + __log2f(l)) * 0.6931471805599453f;
-    }
-  }
-}
-
-// Diagnostic build only (-DNSA_FWD3_STAMPS=1, scripts/fwd3_stamps.py): per-wave s_memtime
-// totals of the v3 tile loop -- [loop, S issue, S wait + softmax, P·V issue, DMA wait +
-// barrier, tiles] -- into a buffer of their own (no output is computed from them).
-#ifndef NSA_FWD3_STAMPS
-#define NSA_FWD3_STAMPS 0
-#endif
-#if NSA_FWD3_STAMPS
-__device__ unsigned long long g_fwd3_stamps[16384 * 4 * 6];
-#endif
-
-// NS = K/V ring slots: tile j + NS - 1 is fetched while tile j is computed, and the
-// end-of-tile wait only needs tile j + 1 (NS - 2 younger tiles stay in flight).  VGPRs,
-// not LDS, bound this kernel's occupancy (2 workgroups per CU), so the deeper ring is free.
-// Probe build only (-DNSA_PROBE_SKIP_TILE=1, build_variant): the v4 forward skips key tile
-// 1 of every workgroup -- wrong output, used to show the test suite catches a dropped tile.
-#ifndef NSA_PROBE_SKIP_TILE
-#define NSA_PROBE_SKIP_TILE 0
-#endif
-template <bool DROP, int NS, bool PAIR = false>
-__global__ __launch_bounds__(256, 2) void flash_fwd3_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse_out, int B, int T, int H,
-                                                            float scale_log2, uint32_t drop_thresh, float drop_scale,
-                                                            uint64_t seed) {
-  static_assert(NS >= 2 && NS <= 4, "ring slots");
-  constexpr int D = 64;
-  constexpr int BN = 64;
-  constexpr int TILE_BYTES = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE_BYTES];  // K[NS], V[NS]
-
-  const int C = H * D;
-  const int64_t row_stride = 3 * (int64_t)C;
-  const int BH = B * H;
-  const int n_qt = (T + 255) / 256;
-  int bh, qt;
-  attn_order(n_qt, BH, 0, bh, qt);
-  qt = n_qt - 1 - qt;  // heaviest (longest causal) tiles first
-  const int b = bh / H, hh = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int h = lane >> 5, r = lane & 31;
-  const int q0 = qt * 256;
-  const int q0w = q0 + 64 * w;  // block A = queries q0w .. q0w + 31, block B = the next 32
-  const int qposA = q0w + r;
-  const bf16_t* base = qkv + (int64_t)b * T * row_stride;
-  const bf16_t* qbase = base + hh * D;
-  const bf16_t* kbase = base + C + hh * D;
-  const DropArgs dr{drop_thresh, drop_scale, nsa_seed(seed), bh, T};
-
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qp = qposA + 32 * blk;
-    const int qc = qp < T ? qp : T - 1;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[blk][ks] = as_frag(*reinterpret_cast<const uint4*>(qbase + (int64_t)qc * row_stride + 16 * ks + 8 * h));
-  }
-  f32x16 o[2][2];
-  float m_i[2], l_i[2];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    o[blk][0] = f32x16{};
-    o[blk][1] = f32x16{};
-    m_i[blk] = -1e30f;
-    l_i[blk] = 0.0f;
-  }
-
-  const int kv_end = min(T, q0 + 256);
-  const int n_tiles = (kv_end + BN - 1) / BN;
-  // same DMA geometry as flash_fwd_kernel<64, *, true>: wave w fills rows 16w .. 16w+15
-  const uint32_t lds0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
-  const int prow = 16 * w + (lane >> 3);
-  const int pch0 = (lane & 7) ^ bitrev<3>((prow >> 1) & 7);
-  const int pch1 = (lane & 7) ^ bitrev<3>(((prow + 8) >> 1) & 7);
-  const uint32_t koff0 = (uint32_t)((prow * (int)row_stride + pch0 * 8) * 2);
-  const uint32_t koff8 = (uint32_t)(((prow + 8) * (int)row_stride + pch1 * 8) * 2);
-  auto issue = [&](int jt, int buf) {
-    const bf16_t* kt_base = kbase + (int64_t)jt * BN * row_stride;
-    uint32_t o0 = koff0, o8 = koff8;
-    if (jt * BN + BN > T) {
-      const int r0 = min(jt * BN + prow, T - 1) - jt * BN, r8 = min(jt * BN + prow + 8, T - 1) - jt * BN;
-      o0 = (uint32_t)((r0 * (int)row_stride + pch0 * 8) * 2);
-      o8 = (uint32_t)((r8 * (int)row_stride + pch1 * 8) * 2);
-    }
-    const uint32_t kb = lds0 + (uint32_t)(buf * TILE_BYTES + 16 * w * 128);
-    const uint32_t vb = kb + NS * TILE_BYTES;
-    glds16s(o0, kt_base, __builtin_amdgcn_readfirstlane(kb));
-    glds16s(o8, kt_base, __builtin_amdgcn_readfirstlane(kb + 1024));
-    glds16s(o0, kt_base + C, __builtin_amdgcn_readfirstlane(vb));
-    glds16s(o8, kt_base + C, __builtin_amdgcn_readfirstlane(vb + 1024));
-  };
-  // every wave issues 4 DMA pieces per tile; "tile j + 1 landed" = at most NS - 2 younger
-  // tiles' pieces outstanding (no other vector-memory op is in flight inside the loop)
-  auto wait_next = [&]() {
-    if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  };
-  asm volatile("" ::"v"(qf[0][0]), "v"(qf[0][1]), "v"(qf[0][2]), "v"(qf[0][3]), "v"(qf[1][0]), "v"(qf[1][1]),
-               "v"(qf[1][2]), "v"(qf[1][3]));  // Q landed before the DMA
-  if constexpr (PAIR && NS == 4 && !DROP) {
-    // two tiles per barrier: pair (j, j + 1) is computed while tiles j + 2, j + 3 fly into
-    // the slots of j - 2, j - 1 (freed by the barrier that opens the pair)
-    issue(0, 0);
-    issue(min(1, n_tiles - 1), 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int j = 0; j < n_tiles; j += 2) {
-      issue(min(j + 2, n_tiles - 1), (j + 2) % 4);
-      issue(min(j + 3, n_tiles - 1), (j + 3) % 4);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int jj = j + u;
-        if (NSA_PROBE_SKIP_TILE && jj == 1) continue;  // test-suite probe: one causal tile dropped
-        if (jj < n_tiles) {
-          const int kv0 = jj * BN;
-          const char* kt = smem + (jj % 4) * TILE_BYTES;
-          const char* vt = smem + (4 + jj % 4) * TILE_BYTES;
-          if (kv0 + BN - 1 <= q0w)
-            fwd_tile2<false, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
-          else if (kv0 <= q0w + 63)
-            fwd_tile2<true, false>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else {
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t) issue(min(t, n_tiles - 1), t);
-  wait_next();  // tile 0 landed
-  __syncthreads();
-#if NSA_FWD3_STAMPS
-  unsigned long long acc3[5] = {0, 0, 0, 0, 0};
-  const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
-#endif
-  for (int j = 0; j < n_tiles; ++j) {
-    const int cur = j % NS;
-    const int kv0 = j * BN;
-    // slot of tile j - 1 (finished by every wave at the last barrier); past the end the
-    // last tile is re-fetched into a slot that is never read again (branch-free count)
-    issue(min(j + NS - 1, n_tiles - 1), (j + NS - 1) % NS);
-    const char* kt = smem + cur * TILE_BYTES;
-    const char* vt = smem + (NS + cur) * TILE_BYTES;
-#if NSA_FWD3_STAMPS
-    unsigned long long st2[2] = {0, 0};
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    bool did = false;
-#else
-    unsigned long long* st2 = nullptr;
-#endif
-    if (kv0 + BN - 1 <= q0w) {  // wave-uniform: every key of the tile visible to all 64 queries
-      fwd_tile2<false, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr, st2);
-#if NSA_FWD3_STAMPS
-      did = true;
-#endif
-    } else if (kv0 <= q0w + 63) {  // the wave's diagonal tile
-      fwd_tile2<true, DROP>(kt, vt, qf, o, m_i, l_i, kv0, qposA, h, r, lane, scale_log2, dr, st2);
-#if NSA_FWD3_STAMPS
-      did = true;
-#endif
-    }
-#if NSA_FWD3_STAMPS
-    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-#endif
-    wait_next();
-    __syncthreads();
-#if NSA_FWD3_STAMPS
-    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
-    if (did) {
-      acc3[0] += st2[0] - t0;  // S MFMA issue (+ K fragment reads)
-      acc3[1] += st2[1] - st2[0];  // wait for S + softmax VALU
-      acc3[2] += t3 - st2[1];  // P·V issue (+ V fragment reads)
-      acc3[4] += 1;
-    }
-    acc3[3] += t4 - t3;  // DMA wait + barrier
-#endif
-  }
-#if NSA_FWD3_STAMPS
-  if (lane == 0) {
-    unsigned long long* g = g_fwd3_stamps + ((size_t)blockIdx.x * 4 + w) * 6;
-    g[0] = __builtin_amdgcn_s_memtime() - t_loop;
-    for (int k = 0; k < 5; ++k) g[1 + k] = acc3[k];
-  }
-#endif
-
-  }
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int qp = qposA + 32 * blk;
-    if (qp < T) {
-      const float inv_l = 1.0f / l_i[blk];
-      bf16_t* orow = out + ((int64_t)b * T + qp) * C + hh * D;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = 32 * dt + 8 * g + 4 * h;
-          uint2 u;
-          u.x = pk2<kFaH>(o[blk][dt][4 * g + 0] * inv_l, o[blk][dt][4 * g + 1] * inv_l);
-          u.y = pk2<kFaH>(o[blk][dt][4 * g + 2] * inv_l, o[blk][dt][4 * g + 3] * inv_l);
-          *reinterpret_cast<uint2*>(orow + d) = u;
-        }
-      }
-      if (h == 0)
-        lse_out[(int64_t)bh * T + qp] = (m_i[blk] * scale_log2 + __log2f(l_i[blk])) * 0.6931471805599453f;
     }
   }
 }
@@ -2446,45 +1855,22 @@ hipError_t fwd_launch(const void* qkv, void* out, void* lse, int B, int T, int H
   const float dscale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
   const int order = attn_order_env();
   if constexpr (D == 64) {
-    // v3 (64 queries per wave, 4-slot K/V ring) by default without dropout once the grid
-    // has >= 4096 workgroups.  B120 T1024 H12 (5760 v3 workgroups): v1 377, v3 344 us
-    // (step 465.3 -> 463.9 ms); v3 halves the K/V re-reads, which pays once qkv (566 MB)
-    // no longer sits in the 256 MB Infinity Cache.  B60: v1 159 vs v3 188 us; with
-    // dropout v1 (the per-element hash doubles v3's VALU chain: 109 vs 158 us at B16).
-    const int n_qt3 = (T + 255) / 256;
+    // v5 (64 queries per wave as two 32-query blocks, 4-slot K/V ring, two tiles per barrier,
+    // no running max while the scores stay in range) by default without dropout once the grid
+    // has >= 4096 workgroups: B120 T1024 H12 (5760 workgroups) 333 us vs v1's 377 -- v5 halves
+    // the K/V re-reads, which pays once qkv (566 MB) no longer sits in the 256 MB Infinity
+    // Cache (B60: v1 159 vs the 64-query form's 188 us); with dropout v1 (the per-element hash
+    // doubles the 64-query chain: 109 vs 158 us at B16).  fp16 runs v5 with the fast tiles'
+    // row sums bounded to [2^-8, 2^15] (P <= 65504).  Round 6 removed the variants that lost
+    // their A/Bs: v3 / v4 (v5's geometry with exact tiles; v4 338.1 vs v5 333.3 us,
+    // profiles/r5_ab_fwd45.log), v6 (v1's geometry with fast tiles, 375.4 vs 343.5,
+    // profiles/r5_ab_v6.log) and a one-wave-per-SIMD pipelined v7 (556 vs 341 us,
+    // docs/performance.md round 6).
+    const int n_qt5 = (T + 255) / 256;
     const int sel = flash_config().fwd;
-    if (sel == FWD_V7 && !th) {
-      flash_fwd7_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
+    if (!th && (sel == FWD_V5 || (sel == FWD_AUTO && (int64_t)n_qt5 * B * H >= 4096))) {
+      flash_fwd5_kernel<<<n_qt5 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
                                                       scale * kLog2e, order);
-      return hipGetLastError();
-    }
-    const bool v3 = sel == FWD_V3 || sel == FWD_V4 || sel == FWD_V5 || sel == FWD_V7 ||
-                    (sel == FWD_AUTO && !th && (int64_t)n_qt3 * B * H >= 4096);
-    // v5 (auto's pick: no running max while the scores stay in range): B120 T1024 H12
-    // 333.3 vs 338.1 us for v4, faster in 5 of 6 same-process A/Bs (profiles/r5_ab_*.log).
-    // fp16 runs it with the fast tiles' row sums bounded to [2^-8, 2^15] (P <= 65504).
-    if (v3 && (sel == FWD_V5 || sel == FWD_AUTO) && !th) {
-      flash_fwd5_kernel<<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H,
-                                                      scale * kLog2e, order);
-      return hipGetLastError();
-    }
-    if (v3) {
-      // v4 = v3 with two K/V tiles per barrier (auto's pick for fp16): B120 T1024 H12 335.5
-      // vs 350.9 us (profiles/r4_attn_ab_pair.log)
-      if (sel != FWD_V3 && !th)
-        flash_fwd3_kernel<false, 4, true><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse,
-                                                                        B, T, H, scale * kLog2e, th, dscale, seed);
-      else if (th)
-        flash_fwd3_kernel<true, 4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T,
-                                                                 H, scale * kLog2e, th, dscale, seed);
-      else
-        flash_fwd3_kernel<false, 4><<<n_qt3 * B * H, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B,
-                                                                  T, H, scale * kLog2e, th, dscale, seed);
-      return hipGetLastError();
-    }
-    if (sel == FWD_V6 && !th) {  // v1 geometry with the fast tiles
-      flash_fwd_kernel<D, false, true, true><<<n_qt * B * H, 256, 0, s>>>(
-          (const bf16_t*)qkv, (bf16_t*)out, (float*)lse, B, T, H, scale * kLog2e, th, dscale, seed, order);
       return hipGetLastError();
     }
     // v1 with LDS-DMA K/V staging
@@ -2603,12 +1989,6 @@ NSA_API hipError_t NSA_FA_SYM(nsa_flash_bwd2)(const void* qkv, const void* o, co
 #define NSA_FA_RNG(NAME) NSA_DEFINE_RNG_ADVANCE(NAME)
 NSA_FA_RNG(NSA_FA_SYM(nsa_rng_advance_attn))
 
-#if NSA_FWD3_STAMPS && !NSA_FA_F16
-NSA_API hipError_t nsa_fwd3_stamps(void* host, int64_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd3_stamps), (size_t)n * sizeof(unsigned long long), 0,
-                             hipMemcpyDeviceToHost);
-}
-#endif
 
 NSA_API hipError_t NSA_FA_SYM(nsa_flash_fwd)(const void* qkv, void* out, void* lse, int B, int T, int H, int D, float scale,
                                  float p, uint64_t seed, hipStream_t s) {
@@ -2623,12 +2003,12 @@ NSA_API hipError_t NSA_FA_SYM(nsa_flash_fwd)(const void* qkv, void* out, void* l
 #if !NSA_FA_F16
 NSA_API void* nsa_flash_config_ptr() { return &flash_config(); }
 
-// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 3 v3 / 4 v4 / 5 v5 / 6 v6, bwd 1 v1 / 2 v2 / 3 v3, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
+// Kernel selection (see FlashConfig): fwd 0 auto / 1 v1 / 5 v5, bwd 1 v1 / 2 v2 / 3 v3, order 0 / 1 / 2; a negative value keeps the current setting.  Returns the previous selection as
 // fwd | bwd << 4 | order << 8.
 NSA_API int nsa_flash_set_variant(int fwd, int bwd, int order) {
   FlashConfig& c = flash_config();
   const int prev = c.fwd | (c.bwd << 4) | (c.order << 8);
-  if (fwd == FWD_AUTO || fwd == FWD_V1 || (fwd >= FWD_V3 && fwd <= FWD_V7)) c.fwd = fwd;
+  if (fwd == FWD_AUTO || fwd == FWD_V1 || fwd == FWD_V5) c.fwd = fwd;
   if (bwd >= BWD_V1 && bwd <= BWD_V3) c.bwd = bwd;
   if (order >= 0 && order <= 2) c.order = order;
   return prev;

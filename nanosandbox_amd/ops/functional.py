@@ -827,7 +827,7 @@ def _attn_reference(q, k, v, p, seed):
     return att @ v
 
 
-_FLASH_FWD = {"auto": 0, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6, "v7": 7}
+_FLASH_FWD = {"auto": 0, "v1": 1, "v5": 5}
 _FLASH_BWD = {"v1": 1, "v2": 2, "v3": 3}
 
 

@@ -17,8 +17,6 @@ on it is labelled as one (bench.py ``--per-rank-of``).
 
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -39,9 +37,8 @@ class _SideWork:
 def ensure_single_process_group():
     """The reducer reads the world size from a process group: a gloo group of one."""
     if not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29541")
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        # an in-process store: no rendezvous address, nothing written to the environment
+        dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
 
 
 class EmulatedAllReduce(FlatBucketReducer):
