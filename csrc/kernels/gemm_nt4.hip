@@ -67,6 +67,13 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XDX = 4 };
 
+// Overlapped epilogue (OVL, plain bf16 outputs only): each tile's stores ride in the next
+// tile's first K-tile, one fragment row (8 accumulators) per 8 k-step-0 MFMAs, instead of
+// stalling the MFMA pipe between tiles.  Measured (profiles/r6_nt4_ovl.md): -1.2 to -2.4 % at
+// K = 3072, +0.5 to +0.8 % at K = 768 / 2304, where the store burst in the one K-tile costs
+// what it hides; the entry's automatic policy takes it from K = 3072.
+constexpr int Q_OVL_MIN_K = 3072;
+
 // GELU epilogue lookup table (built on the host by ops/gemm.py gelu_table with torch's exact-erf
 // GELU): entry i = gelu(u) as bf16 | gelu'(u) as fp16 << 16 for the bf16 u with bit pattern
 // (14208 + i % 2560) | (i >= 2560) << 15, i.e. every bf16 with 2^-16 <= |u| < 16.  The
@@ -77,6 +84,9 @@ enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XD
 constexpr int Q_GTAB_LO = 14208, Q_GTAB_N = 2560, Q_GTAB_BYTES = 2 * Q_GTAB_N * 4;
 #ifndef NSA_NT4_GTAB
 #define NSA_NT4_GTAB 1  // 0 (A/B builds only): the arithmetic GELU for every row
+#endif
+#ifndef NSA_NT4_GROW
+#define NSA_NT4_GROW 1  // 0 (A/B builds only): the lookups row by row (one ballot and LDS round trip per row)
 #endif
 
 // pieces a K-tile has issued when it waits for the previous K-tile's
@@ -127,6 +137,47 @@ template <bool H>
 __device__ __forceinline__ void q_mfma0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+// the overlapped epilogue's first-k-step MFMA: C = 0 like q_mfma0, but the accumulator operand
+// is tied ("+a"), so the restarted tile lands in the same AGPRs and the previous tile's values
+// are copied out (v_accvgpr_read) before it, not kept alive in other registers
+template <bool H>
+__device__ __forceinline__ void q_mfma0t(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  if constexpr (H) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "+a"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// a 16-byte row store pinned between the MFMAs (asm volatile statements keep their order):
+// buffer resource over the previous tile (num_records 0 before the first tile: dropped),
+// lane offset + row offset; the trailing nop keeps the next instruction off its data
+// registers until the store has read them
+template <bool NT>
+__device__ __forceinline__ void q_st16b(q_i32x4 rsrc, uint32_t voff, uint32_t soff, q_u32x4 v) {
+  if constexpr (NT)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory");
+  else
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory");
+}
+// copy-out of one accumulator tile (four AGPRs) into VGPRs, pinned between the MFMAs
+__device__ __forceinline__ void q_acc_rd(float (&t)[4], const f32x4& a) {
+  asm volatile(
+      "v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\t"
+      "v_accvgpr_read_b32 %2, %6\n\tv_accvgpr_read_b32 %3, %7"
+      : "=v"(t[0]), "=v"(t[1]), "=v"(t[2]), "=v"(t[3])
+      : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
+}
+// the next accumulator tile's copy-out packed with the previous one's values (lo = t, hi = a):
+// w[e] = bf16x2 {t[e], a[e]}
+__device__ __forceinline__ void q_acc_rdpk(uint32_t (&w)[4], const float (&t)[4], const f32x4& a) {
+  float x0, x1, x2, x3;
+  asm volatile(
+      "v_accvgpr_read_b32 %4, %12\n\tv_accvgpr_read_b32 %5, %13\n\t"
+      "v_accvgpr_read_b32 %6, %14\n\tv_accvgpr_read_b32 %7, %15\n\t"
+      "v_cvt_pk_bf16_f32 %0, %8, %4\n\tv_cvt_pk_bf16_f32 %1, %9, %5\n\t"
+      "v_cvt_pk_bf16_f32 %2, %10, %6\n\tv_cvt_pk_bf16_f32 %3, %11, %7"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+      : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
 }
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
@@ -345,6 +396,75 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
   // one base pointer per lane; a store's row offset (16 i + e) rows is wave-uniform
   bf16_t* const cb = g.C + (int64_t)row0 * g.ldc + col;
   bf16_t* const cb2 = EPI == Q_EPI_GELU ? g.C2 + (int64_t)row0 * g.ldc + col : nullptr;
+  if constexpr (EPI == Q_EPI_GELU && !H && !BIAS && NSA_NT4_GTAB && NSA_NT4_GROW) {
+    // GELU by lookup, one fragment row (4 output rows, 32 values per lane) at a time: one
+    // ballot for the group and its 32 table reads in flight together, instead of a branch
+    // and a dependent LDS round trip per output row (not with a bias: 44 B of spills)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint32_t w[4][4], ia[4][4], ib[4][4];
+      bool oob = false;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          float v0 = acc[i][2 * h][e], v1 = acc[i][2 * h + 1][e];
+          if constexpr (BIAS) {
+            v0 += bv[2 * h];
+            v1 += bv[2 * h + 1];
+          }
+          const uint32_t b = q_pk(v0, v1);
+          w[e][h] = b;
+          const uint32_t t0 = (b & 0x7fffu) - (uint32_t)Q_GTAB_LO, t1 = ((b >> 16) & 0x7fffu) - (uint32_t)Q_GTAB_LO;
+          oob |= (t0 >= (uint32_t)Q_GTAB_N) | (t1 >= (uint32_t)Q_GTAB_N);
+          ia[e][h] = 4u * (t0 + ((b >> 15) & 1u) * (uint32_t)Q_GTAB_N);
+          ib[e][h] = 4u * (t1 + (b >> 31) * (uint32_t)Q_GTAB_N);
+        }
+      }
+      uint32_t gg[4][4], gp[4][4];
+      if (__builtin_amdgcn_ballot_w64(oob) == 0) {
+        uint32_t ea[4][4], eb[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            ea[e][h] = *reinterpret_cast<const uint32_t*>(tab + ia[e][h]);
+            eb[e][h] = *reinterpret_cast<const uint32_t*>(tab + ib[e][h]);
+          }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            gg[e][h] = __builtin_amdgcn_perm(eb[e][h], ea[e][h], 0x05040100u);  // the two gelu(u) halves
+            gp[e][h] = __builtin_amdgcn_perm(eb[e][h], ea[e][h], 0x07060302u);  // the two gelu'(u) halves
+          }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            nsa_f32x2 gv, dv;
+            nsa_gelu_and_grad2(nsa_f32x2{lo2f<false>(w[e][h]), hi2f<false>(w[e][h])}, gv, dv);
+            gg[e][h] = q_pk(gv.x, gv.y);
+            gp[e][h] = nsa_pk_f16(dv.x, dv.y);
+          }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool skip = !full && (row0 + 16 * i + e < mlo || col < nlo);
+        if (skip) continue;
+        const int64_t off = (int64_t)(16 * i + e) * g.ldc;
+        if constexpr (NOSTORE) {
+          asm volatile("" ::"v"(gp[e][0]), "v"(gp[e][1]), "v"(gp[e][2]), "v"(gp[e][3]), "v"(gg[e][0]), "v"(gg[e][1]),
+                       "v"(gg[e][2]), "v"(gg[e][3]));
+        } else {
+          q_st16<NT>(cb + off, gp[e][0], gp[e][1], gp[e][2], gp[e][3]);
+          q_st16<NT>(cb2 + off, gg[e][0], gg[e][1], gg[e][2], gg[e][3]);
+        }
+      }
+    }
+    return;
+  }
   {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -475,16 +595,20 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 // build_variant library): 1 = no DMA after the prologue, 2 = no wait for the previous
 // K-tile's pieces, 3 = no barriers in the K-loop, 4 = no epilogue at all, 5 = epilogue
 // arithmetic without its stores
-template <int EPI, bool NT, int PROBE, bool BIAS = false, bool H = false>
+template <int EPI, bool NT, int PROBE, bool BIAS = false, bool H = false, bool OVLE = false>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
+  static_assert(!OVLE || (EPI == Q_EPI_BF16 && !BIAS && PROBE == 0 && !H), "OVL: plain bf16 outputs only");
   __shared__ __attribute__((aligned(16))) char smem[Q_SMEM + (EPI == Q_EPI_GELU && !H ? Q_GTAB_BYTES : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int G = gridDim.x;
   const int nk = g.K / Q_BK;
+  // GELU: the lookup table first (LDS address 0: an index is its own LDS address), then the
+  // operand buffers
+  constexpr int QT = EPI == Q_EPI_GELU && !H ? Q_GTAB_BYTES : 0;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem));
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem + QT));
 
   // XCD-aware virtual block id: blocks b, b+8, ... share an XCD and get consecutive ids
   int v = blockIdx.x;
@@ -495,7 +619,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   if (v >= g.tiles) return;
   if constexpr (EPI == Q_EPI_GELU && !H) {  // the GELU table into LDS (before any operand DMA is in flight)
     const uint4* src = reinterpret_cast<const uint4*>(g.U);
-    uint4* dst = reinterpret_cast<uint4*>(smem + Q_SMEM);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
     for (int k = threadIdx.x; k < Q_GTAB_BYTES / 16; k += Q_THR) dst[k] = src[k];
   }
 
@@ -592,16 +716,49 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   int seq = v;
   bool pend = false;  // the previous tile's epilogue left its vector-memory ops in flight
   // one 64-deep K-tile; FIRST: the tile's first, whose k-step 0 starts the accumulators at 0
-  auto ktile = [&](auto FIRST_) {
+  // OVL: the previous tile's accumulators leave fragment row by fragment row (i outer in
+  // k-step 0): each is read out just before the MFMA that restarts it, and a row's four
+  // 256-byte row stores go out after its eighth MFMA (pcb: the previous tile's base pointer)
+  float ovt[4];
+  uint32_t ovw[4][4];
+  q_i32x4 prs = q_rsrc(g.C, 0);  // the previous tile (none yet: every store out of range)
+  const uint32_t pvo = (uint32_t)(((wm * 128 + 4 * (lane >> 4)) * g.ldc + wn * 128 + 8 * (lane & 15)) * 2);
+  auto ktile = [&](auto FIRST_, auto OVL_) {
     constexpr bool FIRST = decltype(FIRST_)::value;
+    constexpr bool OVL = decltype(OVL_)::value;
+    static_assert(!OVL || FIRST, "the overlapped epilogue rides in a tile's first K-tile");
     constexpr bool dv = PROBE != 1;
     const uint32_t nb = buf ^ (uint32_t)Q_BUF;
     q_for([&](auto I) {
       constexpr int n = decltype(I)::value;
-      constexpr int kk = n >> 6, j = (n >> 3) & 7, i = n & 7;
+      constexpr int kk = n >> 6;
+      constexpr int j = OVL && kk == 0 ? n & 7 : (n >> 3) & 7;
+      constexpr int i = OVL && kk == 0 ? (n >> 3) & 7 : n & 7;
       if constexpr (kk == 0) {
-        if constexpr (FIRST) q_mfma0<H>(acc[i][j], a0[i], b0[j]);
-        else q_mfma<H>(acc[i][j], a0[i], b0[j]);
+        if constexpr (OVL) {
+          // the copy-out is itself pinned (volatile asm), so hipcc cannot hoist the 256
+          // copies ahead of the K-tile; odd j packs with the even j before it (bf16 pairs of
+          // adjacent columns, as one 16-byte row store wants them)
+          if constexpr (j % 2 == 0) q_acc_rd(ovt, acc[i][j]);
+          else q_acc_rdpk(ovw[j >> 1], ovt, acc[i][j]);
+          q_mfma0t<H>(acc[i][j], a0[i], b0[j]);
+        } else if constexpr (FIRST) {
+          q_mfma0<H>(acc[i][j], a0[i], b0[j]);
+        } else {
+          q_mfma<H>(acc[i][j], a0[i], b0[j]);
+        }
+        if constexpr (OVL && n == 63) {
+          // the A fragments stay allocated to the end of k-step 0: no copy-out temporary may
+          // take an A fragment's registers while an MFMA that reads them is still in flight
+          asm volatile("" ::"v"(a0[0]), "v"(a0[1]), "v"(a0[2]), "v"(a0[3]), "v"(a0[4]), "v"(a0[5]), "v"(a0[6]),
+                       "v"(a0[7]));
+        }
+        if constexpr (OVL && j == 7) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            q_st16b<NT>(prs, pvo, (uint32_t)((16 * i + e) * g.ldc * 2),
+                        q_u32x4{ovw[0][e], ovw[1][e], ovw[2][e], ovw[3][e]});
+        }
       } else {
         q_mfma<H>(acc[i][j], a1[i], b1[j]);
       }
@@ -625,7 +782,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         }
       }
       constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
-      if constexpr (n == VMS && PROBE != 2) q_vmw<dv ? issued : 0, EPI>(FIRST && pend);
+      if constexpr (n == VMS && PROBE != 2) q_vmw<dv ? issued : 0, EPI>(FIRST && (pend || OVL));
       if constexpr (n == VMS + 1 && PROBE != 3) q_barrier();
       if constexpr (n >= VMS + 2 && n < VMS + 2 + 16 * NSA_NT4_RS && (n - VMS - 2) % NSA_NT4_RS == 0) {
         constexpr int s = (n - VMS - 2) / NSA_NT4_RS;
@@ -637,13 +794,37 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     buf = nb;
     q_cur_next(g, c, nk, G);
   };
+  if constexpr (OVLE) {
+    // every tile's first K-tile stores the previous tile (the first tile's copy-out reads these
+    // zeros and its stores are dropped).  Tail tiles store all of their rows and columns: the
+    // ones another tile also covers get the same bits twice (same operands, same K order).
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int last;
+    while (true) {
+      ktile(std::true_type{}, std::true_type{});
+      for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{});
+      last = seq;
+      seq += G;
+      if (seq >= g.tiles) break;
+      int m0, n0, mlo, nlo;
+      q_tile_coords(g, last, m0, n0, mlo, nlo);
+      prs = q_rsrc(g.C + (int64_t)m0 * g.ldc + n0, 0x7fffffffu);
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    q_epilogue<EPI, NT, BIAS, false, H>(g, acc, last, wm, wn, lane, smem);
+    q_vmwait<0>();
+    return;
+  }
   while (true) {
-    ktile(std::true_type{});
-    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{});
+    ktile(std::true_type{}, std::false_type{});
+    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{});
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT, BIAS, PROBE == 5, H>(g, acc, seq, wm, wn, lane, smem + Q_SMEM);
+      q_epilogue<EPI, NT, BIAS, PROBE == 5, H>(g, acc, seq, wm, wn, lane, smem);
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -687,7 +868,14 @@ void nt4_geometry(Nt4Args& a, int gmsel) {
 }
 
 template <int E, bool B, bool H = false>
-void nt4_launch(const Nt4Args& a, dim3 gr, bool nt, int probe, hipStream_t s) {
+void nt4_launch(const Nt4Args& a, dim3 gr, bool nt, int probe, hipStream_t s, bool ovl = false) {
+  if constexpr (E == Q_EPI_BF16 && !B && !H) {
+    if (ovl && probe == 0) {
+      if (nt) gemm_nt4_kernel<E, true, 0, false, false, true><<<gr, Q_THR, 0, s>>>(a);
+      else gemm_nt4_kernel<E, false, 0, false, false, true><<<gr, Q_THR, 0, s>>>(a);
+      return;
+    }
+  }
 #ifdef NSA_PROBES
   switch (probe) {
     case 1: gemm_nt4_kernel<E, true, 1, B, H><<<gr, Q_THR, 0, s>>>(a); return;
@@ -711,7 +899,8 @@ bool nt4_store_nt(int stp, int64_t out_bytes) { return stp == 1 || (stp == 0 && 
 // C = A · B^T (bf16) with an optional bias[N] (bf16) added to every row.
 // epi: 0 bf16, 1 gelu'(u) (fp16) / gelu(u) into C / C2, 2 acc * U (U = gelu'(u), fp16); bits 8-11 timing probe (-DNSA_PROBES
 // builds only; 1 no DMA, 4 no stores, ...); bits 12-13 store policy: 0 nontemporal above the
-// Infinity Cache, 1 always, 2 never; bits 16-23 row-blocks per tile group, 0 = automatic.
+// Infinity Cache, 1 always, 2 never; bits 14-15 overlapped epilogue (plain bf16 without bias):
+// 0 from K = Q_OVL_MIN_K, 1 always, 2 never; bits 16-23 row-blocks per tile group, 0 = automatic.
 // grid = persistent workgroups.
 namespace {
 template <bool H>
@@ -720,6 +909,7 @@ hipError_t gemm_nt4_entry(int epi, const void* A, int lda, const void* B, int ld
   const int stp = (epi >> 12) & 0x3;
   const int probe = (epi >> 8) & 0xf;
   const int gmsel = (epi >> 16) & 0xff;
+  const int ovp = (epi >> 14) & 0x3;  // overlapped epilogue: 0 automatic (K >= Q_OVL_MIN_K), 1 always, 2 never
   epi &= 0xff;
   Nt4Args a{};
   a.A = (const bf16_t*)A;
@@ -744,7 +934,7 @@ hipError_t gemm_nt4_entry(int epi, const void* A, int lda, const void* B, int ld
   switch (epi) {
     case Q_EPI_BF16:
       if (bias) nt4_launch<Q_EPI_BF16, true, H>(a, gr, nt, probe, s);
-      else nt4_launch<Q_EPI_BF16, false, H>(a, gr, nt, probe, s);
+      else nt4_launch<Q_EPI_BF16, false, H>(a, gr, nt, probe, s, ovp == 1 || (ovp == 0 && K >= Q_OVL_MIN_K));
       break;
     case Q_EPI_GELU:
       if (bias) nt4_launch<Q_EPI_GELU, true, H>(a, gr, nt, probe, s);

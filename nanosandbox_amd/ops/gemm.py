@@ -81,6 +81,8 @@ def wgrad_supported(n_out, n_in, tokens) -> bool:
 
 
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
+# plain bf16 outputs: a tile's stores inside the next tile's first K-tile (0 from K = 3072, 1 always, 2 never)
+NT_OVL = int(os.environ.get("NSA_NT_OVL", "0"))
 
 
 def _out(M, N, device, out, dtype=BF16):  # noqa: D401
@@ -134,14 +136,15 @@ def nt_grid(device=None) -> int:
     return num_cus(device) * max(1, NT_GRID_MULT)
 
 
-def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, gm=0, out=None, out2=None):
+def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, gm=0, out=None, out2=None, ovl=None):
     """C = a @ b^T with a [M, K], b [N, K] (both K-contiguous, bf16) on the four-wave kernel.
 
     ``bias`` [N] (bf16) is added in the epilogue (before the GELU).  epi NT_EPI_GELU returns
     (gelu'(u) as fp16, gelu(u) as bf16) for u = bf16(a @ b^T + bias): the backward's only use of
     u is gelu'(u), so the forward stores that (fp16: 2^-11 relative rounding) and the
     NT_EPI_DGELU epilogue, given it as ``u``, is a single multiply: bf16(bf16(a @ b^T) * u).
-    ``probe`` needs a library built with -DNSA_PROBES (scripts/gemm_nt_ab.py)."""
+    ``probe`` needs a library built with -DNSA_PROBES (scripts/gemm_nt_ab.py).  ``ovl`` (plain bf16
+    outputs): 0 automatic, 1 / 2 force the overlapped epilogue on / off (csrc/kernels/gemm_nt4.hip)."""
     M, K = a.shape
     N = b.shape[0]
     _check(a, "a")
@@ -152,13 +155,14 @@ def nt(a, b, epi=NT_EPI_BF16, u=None, bias=None, grid=None, probe=0, var=None, g
         raise ValueError("a and b must have the same dtype")
     c = _out(M, N, a.device, out, torch.float16 if epi == NT_EPI_GELU else a.dtype)
     var = NT_VAR if var is None else var
+    ovl = NT_OVL if ovl is None else ovl
     c2 = (_out(M, N, a.device, out2, a.dtype)) if epi == NT_EPI_GELU else None
     if epi == NT_EPI_DGELU:
         _check_gp(u)
     if epi == NT_EPI_GELU:
         # rides in the U slot; the table is indexed by bf16 bits (fp16 computes the GELU)
         u = gelu_table(a.device) if a.dtype == BF16 else None
-    _lib.call(_sym("nsa_gemm_nt4", a), epi | (probe << 8) | (var << 12) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
+    _lib.call(_sym("nsa_gemm_nt4", a), epi | (probe << 8) | (var << 12) | (ovl << 14) | (gm << 16), _lib.ptr(a), a.stride(0), _lib.ptr(b),
               b.stride(0), _lib.ptr(c), c.stride(0), _lib.ptr(c2), _lib.ptr(u), _lib.ptr(bias), M, N, K,
               grid or nt_grid(a.device), _lib.stream())
     return (c, c2) if epi == NT_EPI_GELU else c

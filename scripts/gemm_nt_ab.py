@@ -5,7 +5,7 @@ Correctness: each shape is checked against an fp32 product of the same bf16 oper
 Timing: interleaved rounds in one process on uniform [-1, 1) operands
 (cdna_hip_programming.md §5.4 rules 24/25).
 
-    python scripts/gemm_nt_ab.py [--m 122880] [--rounds 5] [--probe] [--epi] [--gms 1,4] [--vars 1,2]
+    python scripts/gemm_nt_ab.py [--m 122880] [--rounds 5] [--probe] [--epi] [--gms 1,4] [--vars 1,2] [--ovls 1,2]
 
 ``--probe`` needs a library built with -DNSA_PROBES (the structure probes: no DMA, no vmcnt
 wait, no barrier, no epilogue, no stores).  ``--alt-lib PATH`` loads a second build of the
@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--epi", action="store_true", help="also time the GELU / GELU' epilogues")
     ap.add_argument("--gms", default="", help="extra tile-group sizes to time, e.g. 1,4,8")
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
+    ap.add_argument("--small", action="store_true", help="also time the bounds-checked small-tile kernel")
+    ap.add_argument("--ovls", default="", help="overlapped-epilogue policies to time beside auto, e.g. 1,2")
     ap.add_argument("--alt-lib", default="")
     a = ap.parse_args()
     alt = None
@@ -78,7 +80,7 @@ def main():
         print(json.dumps({"check_odd": [m_, n_, k_], "rel_err": rel(gemm.nt(x, w), ref),
                           "rel_err_small": rel(gemm.small(x, w), ref)}), flush=True)
     for name in a.shapes.split(","):
-        N, K = SHAPES[name]
+        N, K = SHAPES[name] if name in SHAPES else map(int, name.split("x"))  # or "NxK"
         fl = 2.0 * M * N * K
         x = uni(M, K)
         w = uni(N, K, scale=0.05)
@@ -93,6 +95,11 @@ def main():
             cands["nt4_alt"] = lambda: nt_alt(x, w)
         for gm_ in [int(t) for t in a.gms.split(",") if t]:
             cands[f"nt4_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_)
+        if a.small:
+            cands["small"] = lambda: gemm.small(x, w)
+        for ov in [int(t) for t in a.ovls.split(",") if t]:
+            cands[f"nt4_ovl{ov}"] = lambda ov=ov: gemm.nt(x, w, ovl=ov)
+            assert torch.equal(gemm.nt(x, w, ovl=ov), got), ov
         for v in [int(t) for t in a.vars.split(",") if t and t != "0"]:
             cands[f"nt4_v{v}"] = lambda v=v: gemm.nt(x, w, var=v)
             print(json.dumps({"check": f"{name}/v{v}", "rel_err": rel(gemm.nt(x, w, var=v)[rows], ref)}), flush=True)
@@ -143,8 +150,12 @@ def main():
             fn()
         torch.cuda.synchronize()
         samples = {k: [] for k in cands}
-        for _ in range(a.rounds):
-            for k, fn in cands.items():
+        names = list(cands)
+        for r in range(a.rounds):
+            # the starting candidate rotates every round: the same kernel timed in different
+            # slots of one round has measured up to ~4 % apart (profiles/r6_nt4_ovl.md)
+            for k in names[r % len(names):] + names[:r % len(names)]:
+                fn = cands[k]
                 e0.record()
                 for _ in range(a.reps):
                     fn()

@@ -73,6 +73,10 @@ def test_nt4_elementwise(kernels, M, N, K):
     assert exact > 0.999, f"gelu(u) bit-exact on only {exact:.5f} of the elements"
     for st in (1, 2):  # nontemporal / plain epilogue stores: identical results
         assert torch.equal(gemm.nt(x, w, var=st, out=nanbuf(M, N)), y)
+    # the overlapped epilogue forced on / off (each tile's stores inside the next tile's first
+    # K-tile; tail tiles store every row), also with many tiles per workgroup: identical results
+    for ov, grid in ((1, None), (2, None), (1, 7), (1, 1)):
+        assert torch.equal(gemm.nt(x, w, ovl=ov, grid=grid, out=nanbuf(M, N)), y), (ov, grid)
     uu = gelu_grad(torch.randn(M, N, device=DEV) * 2).half()
     d = gemm.nt(x, w, epi=gemm.NT_EPI_DGELU, u=uu, out=nanbuf(M, N))
     assert torch.equal(d, (y.float() * uu.float()).to(BF))  # bf16(bf16(acc) * gelu'(u)), bitwise
@@ -89,6 +93,7 @@ def test_nt4_exact_permutation(kernels, M, N, K):
     b = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K).remainder(251).sub(125).to(BF)
     c = gemm.nt(a, b, out=nanbuf(M, N))
     assert torch.equal(c.float(), b.float()[:, idx].t())
+    assert torch.equal(gemm.nt(a, b, ovl=1, out=nanbuf(M, N)), c)  # the overlapped epilogue
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 192, 64), (100, 72, 40), (2048, 64, 256), (17, 300, 128), (300, 17, 88)])
