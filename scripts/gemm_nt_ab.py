@@ -51,14 +51,18 @@ def main():
     ap.add_argument("--gms", default="", help="extra tile-group sizes to time, e.g. 1,4,8")
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
     ap.add_argument("--small", action="store_true", help="also time the bounds-checked small-tile kernel")
+    ap.add_argument("--xent", action="store_true", help="lm_head: also time the fused cross-entropy (XENT) GEMM")
     ap.add_argument("--ovls", default="", help="overlapped-epilogue policies to time beside auto, e.g. 1,2")
     ap.add_argument("--alt-lib", default="")
     a = ap.parse_args()
-    alt = None
+    alt = alt_xent = None
     if a.alt_lib:
         alt = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4
         alt.argtypes = _lib._SIGNATURES["nsa_gemm_nt4"]
         alt.restype = ctypes.c_int
+        alt_xent = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4_xent
+        alt_xent.argtypes = _lib._SIGNATURES["nsa_gemm_nt4_xent"]
+        alt_xent.restype = ctypes.c_int
 
     def nt_alt(x, w, epi=0, u=None):
         M_, K_ = x.shape
@@ -97,6 +101,28 @@ def main():
             cands[f"nt4_gm{gm_}"] = lambda gm_=gm_: gemm.nt(x, w, gm=gm_)
         if a.small:
             cands["small"] = lambda: gemm.small(x, w)
+        if a.xent and name == "lm_head":
+            nvalid = 50257
+            crow = (x[:, :64].float().sum(1) * 0.05).contiguous()  # a per-row shift of the logits' scale
+            part = torch.empty(2 * ((N + 255) // 256), M, device=x.device)
+            e_ref = gemm.nt_xent(x, w, crow, part, nvalid)
+            part_ref = part.clone()
+            cands["nt4_xent"] = lambda: gemm.nt_xent(x, w, crow, part, nvalid, out=e_ref)
+            if alt_xent is not None:
+                part2 = torch.empty_like(part)
+                e2 = torch.empty_like(e_ref)
+
+                def xent_alt():
+                    err = alt_xent(_lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(e2), e2.stride(0),
+                                   _lib.ptr(crow), _lib.ptr(part2), M, N, nvalid, K, gemm.num_cus(x.device),
+                                   _lib.stream())
+                    assert err == 0, err
+                xent_alt()
+                torch.cuda.synchronize()
+                print(json.dumps({"check": "lm_head/xent_vs_alt", "E_equal": torch.equal(e2, e_ref),
+                                  "part_maxrel": ((part2 - part_ref).abs() / part_ref.abs().clamp_min(1e-30)).max().item()}),
+                      flush=True)
+                cands["nt4_alt_xent"] = xent_alt
         for ov in [int(t) for t in a.ovls.split(",") if t]:
             cands[f"nt4_ovl{ov}"] = lambda ov=ov: gemm.nt(x, w, ovl=ov)
             assert torch.equal(gemm.nt(x, w, ovl=ov), got), ov
