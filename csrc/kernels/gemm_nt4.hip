@@ -396,6 +396,33 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
   // one base pointer per lane; a store's row offset (16 i + e) rows is wave-uniform
   bf16_t* const cb = g.C + (int64_t)row0 * g.ldc + col;
   bf16_t* const cb2 = EPI == Q_EPI_GELU ? g.C2 + (int64_t)row0 * g.ldc + col : nullptr;
+  if constexpr (EPI == Q_EPI_DGELU && NSA_NT4_GROW) {
+    // acc * gelu'(u) one fragment row at a time, with the U rows two fragment rows ahead
+    // loaded BEFORE this row's stores: vmcnt completes in order, so a U load issued after a
+    // row's stores made the next-but-one row wait for those stores' acknowledgements
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint32_t w[4][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t b = pk2<H>(acc[i][2 * h][e], acc[i][2 * h + 1][e]);
+          const nsa_f32x2 a = nsa_f32x2{lo2f<H>(b), hi2f<H>(b)} * nsa_unpk_f16(uv[i & 1][e][h]);
+          w[e][h] = pk2<H>(a.x, a.y);
+        }
+      if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool skip = !full && (row0 + 16 * i + e < mlo || col < nlo);
+        if (skip) continue;
+        const int64_t off = (int64_t)(16 * i + e) * g.ldc;
+        if constexpr (NOSTORE) asm volatile("" ::"v"(w[e][0]), "v"(w[e][1]), "v"(w[e][2]), "v"(w[e][3]));
+        else q_st16<NT>(cb + off, w[e][0], w[e][1], w[e][2], w[e][3]);
+      }
+    }
+    return;
+  }
   if constexpr (EPI == Q_EPI_GELU && !H && !BIAS && NSA_NT4_GTAB && NSA_NT4_GROW) {
     // GELU by lookup, one fragment row (4 output rows, 32 values per lane) at a time: one
     // ballot for the group and its 32 table reads in flight together, instead of a branch
