@@ -90,6 +90,14 @@ __global__ __launch_bounds__(256) void xent_combine_kernel(const float* __restri
 // Exact recompute of a flagged row: logits l_v = x_r · W_v (fp32), m = max, E = exp(l - m),
 // S = sum E, loss = m + log S - l_t (a flagged ignored row: E = 0).  One workgroup per listed row (grid-stride over the
 // device-side count: with no flagged row every workgroup exits at once).
+// Grid of the fix-up: every workgroup reads the device count and exits when it has no row, so
+// an empty list costs one short launch whatever the grid.  1024 (4 per CU, 33 KB of LDS each)
+// rather than round 5's 64: fp16 E flags every row whose largest logit passes its target's
+// by ~11 nats, a share that grows as a model trains, and each flagged row costs two V x C
+// passes (profiles/r6_xent_f16_cliff.md)
+#ifndef NSA_XENT_FIX_GRID
+#define NSA_XENT_FIX_GRID 1024
+#endif
 template <bool H>
 __global__ __launch_bounds__(256) void xent_fixup_kernel(const bf16_t* __restrict__ x, int ldx,
                                                          const bf16_t* __restrict__ W, int ldw, bf16_t* __restrict__ E,
@@ -246,7 +254,7 @@ hipError_t fixup_entry(const void* x, int ldx, const void* W, int ldw, void* E, 
                        const void* nfix, const void* fixlist, void* loss, void* invS, int C, int V, int Vpad,
                        hipStream_t s) {
   if (C > 8192 || C % 8 || ldw % 8 || Vpad % 8 || lde % 8) return hipErrorInvalidValue;
-  xent_fixup_kernel<H><<<64, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (bf16_t*)E, lde,
+  xent_fixup_kernel<H><<<NSA_XENT_FIX_GRID, 256, 0, s>>>((const bf16_t*)x, ldx, (const bf16_t*)W, ldw, (bf16_t*)E, lde,
                                           (const int*)t32, (const int*)nfix, (const int*)fixlist, (float*)loss,
                                           (float*)invS, C, V, Vpad);
   return hipGetLastError();

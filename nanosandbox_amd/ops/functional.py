@@ -1198,6 +1198,69 @@ def _fused_xent_ok(M, C, Vp):
 # 2.9e-4 at init-like logits, dW 1.4e-4 vs 1.2e-3 and dX 2.1e-4 vs 1.2e-3 at sharp ones
 # (scripts/debug/xent_f16_vs_autocast.py, profiles/r5_xent16_vs_autocast.log).
 XENT_F16 = os.environ.get("NSA_XENT_F16", "1") == "1"
+
+
+class XentF16Guard:
+    """Falls back from the fused fp16 cross-entropy when its exact fix-up gets expensive.
+
+    fp16 E flags every row whose largest logit passes its target's by ~11 nats, and each
+    flagged row costs two V x C passes in ``nsa_xent_fixup``: at GPT-2 124M shapes the loss
+    forward goes from 9.6 ms to 17.0 / 35.9 / 141.5 ms with 0.1 / 1 / 5 % of the rows flagged
+    (profiles/r6_xent_f16_cliff.md).  That share grows as a model trains, so the fused form is
+    only kept while the flagged share stays under ``max_frac``.
+
+    The forward adds each call's flagged count and row count into two device counters. Both
+    adds are stream-ordered, so they also happen inside a captured HIP graph. ``poll()`` runs
+    once per optimizer step. It copies the counters to pinned host memory without blocking
+    and reads the copy from the previous poll once that copy's event has completed. When the
+    share over at least ``min_rows`` rows exceeds ``max_frac``, the guard trips. Every later
+    fp16 call then takes autocast's form (fp16 logits and the fp32 softmax pass). ``poll()``
+    returns True on that step, so the trainer can drop a graph captured with the fused form.
+    """
+
+    def __init__(self, max_frac: float = 0.002, min_rows: int = 1 << 20):
+        self.max_frac = float(max_frac)
+        self.min_rows = int(min_rows)
+        self.active = True
+        self.counts = None  # device int64 [flagged, rows]
+        self._host = None
+        self._event = None
+        self.last = None  # (flagged, rows) as last read
+
+    def note(self, nfix, n_rows: int):
+        if self.counts is None or self.counts.device != nfix.device:
+            self.counts = torch.zeros(2, dtype=torch.int64, device=nfix.device)
+        self.counts[0:1].add_(nfix)
+        self.counts[1:2].add_(n_rows)
+
+    def poll(self) -> bool:
+        if not self.active or self.counts is None:
+            return False
+        if self.counts.device.type != "cuda":  # (CPU tests) a synchronous read
+            vals = self.counts.tolist()
+        else:
+            vals = None
+            if self._event is not None and self._event.query():
+                vals = self._host.tolist()
+            if self._host is None:
+                self._host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            if vals is not None or self._event is None:
+                self._host.copy_(self.counts, non_blocking=True)
+                self._event = torch.cuda.Event()
+                self._event.record()
+        if vals is None:
+            return False
+        self.last = (int(vals[0]), int(vals[1]))
+        flagged, rows = self.last
+        if rows >= self.min_rows and flagged > self.max_frac * rows:
+            self.active = False
+            print(f"[nanosandbox_amd] fused fp16 cross-entropy: {flagged} of {rows} rows needed the exact "
+                  f"fix-up (> {self.max_frac:.2%}); switching to autocast's form (fp16 logits, fp32 softmax)")
+            return True
+        return False
+
+
+XENT_F16_GUARD = XentF16Guard(float(os.environ.get("NSA_XENT_F16_MAXFIX", "0.002")))
 # the lm_head dW onehot term by target-sorted rows (segsum.h) instead of fp32 atomics
 XENT_FIX_SORTED = os.environ.get("NSA_XENT_FIX_SORTED", "1") == "1"
 
@@ -1238,7 +1301,7 @@ class LMHeadLossFn(torch.autograd.Function):
             Vp = wp.shape[0]
             row_loss = torch.empty(N, device=x.device, dtype=F32)
             # E = exp(logit - target logit) in the compute dtype; fp16 unless XENT_F16 is off (see there)
-            ctx.fused = _fused_xent_ok(N, C, Vp) and (x.dtype == BF16 or XENT_F16)
+            ctx.fused = _fused_xent_ok(N, C, Vp) and (x.dtype == BF16 or (XENT_F16 and XENT_F16_GUARD.active))
             if ctx.fused:
                 shift, lo, hi = _xent_range(x.dtype)
                 crow = torch.empty(N, device=x.device, dtype=F32)
@@ -1258,6 +1321,8 @@ class LMHeadLossFn(torch.autograd.Function):
                           _lib.ptr(t32),
                           _lib.ptr(nfix), _lib.ptr(fixlist), _lib.ptr(row_loss), _lib.ptr(inv_s), C, V, Vp,
                           _lib.stream())
+                if x.dtype == F16:
+                    XENT_F16_GUARD.note(nfix, N)
                 n_valid = (t32 >= 0).sum().to(F32)
                 ctx.save_for_backward(x2, w, e, t32, inv_s, n_valid)
             else:

@@ -30,6 +30,7 @@ import torch
 from .config import TRAIN_DEFAULTS, config_keys, parse_argv
 from .data import load_meta, make_batch_source, resolve_data_dir
 from .ops import rng_advance
+from .ops.functional import XENT_F16_GUARD as xent_f16_guard
 from .runtime import MicroStepGraph, graph_capture_supported
 from .models import GPT, GPTConfig
 from .optim import FlatParamStore
@@ -287,6 +288,8 @@ class Trainer:
         if norm is None and self.scaler is not None and hasattr(self.optimizer, "last_norm"):
             norm = self.optimizer.last_norm  # fp16 without clipping: the step's own inf check (inf = skipped)
         self.optimizer.zero_grad(set_to_none=True)
+        if self.scaler is not None and xent_f16_guard.poll():
+            self.graph = None  # captured with the fused fp16 cross-entropy: recapture on the next step
         return loss, norm, X, Y
 
     def fit(self):

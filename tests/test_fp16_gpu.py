@@ -482,3 +482,30 @@ def test_add_layernorm_fused_dropout_fp16(kernels):
             Fn.LN_DROPOUT = True
     for a, bb, name in zip(out[0], out[1], ("s", "h", "dx", "dy")):
         assert torch.equal(a, bb), name
+
+
+def test_xent_f16_guard_trips_and_falls_back(kernels, monkeypatch):
+    """With many rows past fp16 E's saturation edge the guard trips (after its pinned-memory
+    read lands) and the next calls take autocast's form; both forms match fp32."""
+    from nanosandbox_amd.ops import functional as Fn
+    guard = Fn.XentF16Guard(max_frac=0.01, min_rows=1)
+    monkeypatch.setattr(Fn, "XENT_F16_GUARD", guard)
+    torch.manual_seed(0)
+    N, C, V = 2048, 768, 50304
+    w = (torch.randn(V, C, device="cuda") * 0.02).half()
+    x = torch.randn(N, C, device="cuda") * 2.0
+    x[: N // 10] *= 6.0  # 10 % of the rows: the row max passes the target by far more than 11 nats
+    x = x.half()
+    t = torch.randint(0, 50257, (N,), device="cuda")
+    ref = torch.nn.functional.cross_entropy(x.float() @ w.float().t(), t).item()
+    with torch.no_grad():
+        fused = Fn.lm_head_loss(x, w, t).item()
+        assert guard.counts is not None and guard.counts[0].item() >= N // 20  # most pushed rows flag
+        assert guard.poll() is False  # the first poll only starts the copy
+        torch.cuda.synchronize()
+        assert guard.poll() is True and not guard.active
+        before = guard.counts.clone()
+        plain = Fn.lm_head_loss(x, w, t).item()
+        torch.cuda.synchronize()
+        assert torch.equal(guard.counts, before)  # the fused path (and its counter) is off
+    assert abs(fused - ref) < 2e-3 * abs(ref) and abs(plain - ref) < 2e-3 * abs(ref), (fused, plain, ref)

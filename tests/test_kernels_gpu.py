@@ -381,14 +381,14 @@ def _lm_loss_and_grads(x0, w0, t):
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_lm_head_loss_fixup_many_rows(kernels, graph):
-    """more flagged rows (100) than the fix-up grid (64 workgroups, so
-    workgroups take several rows), some with the last real vocabulary id as target (the
-    tile beside the 50257 -> 50304 padding), under HIP-graph capture and replay too.  Loss
+    """more flagged rows (1100) than the fix-up grid (1024 workgroups since
+    round 6, so some workgroups take two rows), some with the last real vocabulary id as target
+    (the tile beside the 50257 -> 50304 padding), under HIP-graph capture and replay too.  Loss
     and every gradient element against fp32, bounds scaled by the terms that form them."""
     torch.manual_seed(5)
-    N, V, C = 1024, 50257, 256
+    N, V, C = 4096, 50257, 256
     x0 = torch.randn(N, C, device=DEV)
-    flagged = torch.arange(0, 1000, 10, device=DEV)  # 100 rows
+    flagged = torch.arange(0, 3300, 3, device=DEV)  # 1100 rows
     x0[flagged] *= 400.0  # logits ~ +-1300: S = sum exp(l - l_t) overflows fp32
     x0 = x0.to(BF)
     w0 = torch.randn(V, C, device=DEV) * 0.05
