@@ -86,7 +86,7 @@ def main():
         for v, name in ((6, "1024x7"), (1, "256x25"), (2, "512x13"), (3, "1024x7_nt_ld_st"), (4, "1024x7_nt_st"),
                         (5, "1024x7_nt_ld"), (0, "default")):
             cands[f"xent/{name}"] = (
-                lambda v=v: _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(tgt), _lib.ptr(loss), N, V,
+                lambda v=v: _lib.call("nsa_xent_fwd", _lib.ptr(logits), _lib.ptr(tgt), _lib.ptr(loss), N, V, V,
                                       1 | (v << 8), S()), byts)
         print(json.dumps({"kernel": "xent", "res": run(cands, a.rounds)}), flush=True)
         del logits
