@@ -40,6 +40,7 @@
 // cursor runs straight on into the next tile, so the next tile's first two K-tiles load
 // while this tile's epilogue stores.  Tail tiles are shifted back inside the matrix and
 // store only their not-yet-covered rows / columns: M, N >= 256, N % 8 == 0, K % 64 == 0.
+#include <cstdlib>
 #include <utility>
 
 #include "common.h"
@@ -1011,7 +1012,13 @@ hipError_t nt4_xent_entry(const void* A, int lda, const void* B, int ldb, void* 
     return hipErrorInvalidValue;
   nt4_geometry(a, 0);
   const dim3 gr(grid < a.tiles ? grid : a.tiles);
-  nt4_launch<Q_EPI_XENT, false, H>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), 0, s);
+  int probe = 0;
+#ifdef NSA_PROBES
+  // timing probes of the XENT GEMM (probe builds only; see gemm_nt4_kernel): 4 no epilogue,
+  // 5 epilogue arithmetic without its stores
+  if (const char* e = getenv("NSA_PROBE_XENT")) probe = atoi(e);
+#endif
+  nt4_launch<Q_EPI_XENT, false, H>(a, gr, nt4_store_nt(0, (int64_t)M * N * 2), probe, s);
   return hipGetLastError();
 }
 }  // namespace
