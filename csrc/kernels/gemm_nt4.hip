@@ -69,11 +69,18 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XDX = 4 };
 
 // Overlapped epilogue (OVL, plain bf16 outputs only): each tile's stores ride in the next
-// tile's first K-tile, one fragment row (8 accumulators) per 8 k-step-0 MFMAs, instead of
-// stalling the MFMA pipe between tiles.  Measured (profiles/r6_nt4_ovl.md): -1.2 to -2.4 % at
-// K = 3072, +0.5 to +0.8 % at K = 768 / 2304, where the store burst in the one K-tile costs
-// what it hides; the entry's automatic policy takes it from K = 3072.
-constexpr int Q_OVL_MIN_K = 3072;
+// tile's first two K-tiles instead of stalling the MFMA pipe between tiles.  In the first
+// K-tile, k-step 0 runs fragment row by fragment row; each accumulator tile is copied out just
+// before the MFMA that restarts it, rows 0-3 go out as 256-byte row stores after their eighth
+// MFMA, rows 4-7 are held packed (64 VGPRs) and stored in the second K-tile (OVL2): 16 stores
+// per K-tile rather than 32, which the per-CU write path drains under the MFMAs.  Measured
+// (profiles/r6_nt4_ovl.md, same process): c_attn 333.8 -> 314.5 us, attn.c_proj 138.5 ->
+// 135.2, c_attn.dx 336.4 -> 329.9, mlp.c_proj / c_fc.dx -1.2 / -1.7 %; all 32 stores in the
+// first K-tile (OVL1) had gained only at K = 3072.  Needs two K-tiles (K >= 128).
+constexpr int Q_OVL_MIN_K = 2 * 64;
+#ifndef NSA_NT4_OVL2
+#define NSA_NT4_OVL2 1  // 0 (A/B builds only): all 32 stores in the first K-tile (OVL1)
+#endif
 
 // GELU epilogue lookup table (built on the host by ops/gemm.py gelu_table with torch's exact-erf
 // GELU): entry i = gelu(u) as bf16 | gelu'(u) as fp16 << 16 for the bf16 u with bit pattern
@@ -749,12 +756,16 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
   // 256-byte row stores go out after its eighth MFMA (pcb: the previous tile's base pointer)
   float ovt[4];
   uint32_t ovw[4][4];
+  uint32_t ovd[4][4][4];  // OVL2: fragment rows 4-7, [i - 4][e][h], stored by the next K-tile
   q_i32x4 prs = q_rsrc(g.C, 0);  // the previous tile (none yet: every store out of range)
   const uint32_t pvo = (uint32_t)(((wm * 128 + 4 * (lane >> 4)) * g.ldc + wn * 128 + 8 * (lane & 15)) * 2);
-  auto ktile = [&](auto FIRST_, auto OVL_) {
+  auto ktile = [&](auto FIRST_, auto OVL_, auto DEF_) {
     constexpr bool FIRST = decltype(FIRST_)::value;
     constexpr bool OVL = decltype(OVL_)::value;
+    constexpr bool DEF = decltype(DEF_)::value;  // OVL2: this K-tile stores the deferred rows
     static_assert(!OVL || FIRST, "the overlapped epilogue rides in a tile's first K-tile");
+    static_assert(!DEF || !FIRST, "the deferred rows go out in a tile's second K-tile");
+    constexpr bool OV2 = OVL && NSA_NT4_OVL2;
     constexpr bool dv = PROBE != 1;
     const uint32_t nb = buf ^ (uint32_t)Q_BUF;
     q_for([&](auto I) {
@@ -782,13 +793,25 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
                        "v"(a0[7]));
         }
         if constexpr (OVL && j == 7) {
+          if constexpr (OV2 && i >= 4) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            q_st16b<NT>(prs, pvo, (uint32_t)((16 * i + e) * g.ldc * 2),
-                        q_u32x4{ovw[0][e], ovw[1][e], ovw[2][e], ovw[3][e]});
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int h = 0; h < 4; ++h) ovd[i - 4][e][h] = ovw[h][e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q_st16b<NT>(prs, pvo, (uint32_t)((16 * i + e) * g.ldc * 2),
+                          q_u32x4{ovw[0][e], ovw[1][e], ovw[2][e], ovw[3][e]});
+          }
         }
       } else {
         q_mfma<H>(acc[i][j], a1[i], b1[j]);
+      }
+      if constexpr (DEF && n < 16) {
+        constexpr int di = n >> 2, de = n & 3;
+        q_st16b<NT>(prs, pvo, (uint32_t)((16 * (4 + di) + de) * g.ldc * 2),
+                    q_u32x4{ovd[di][de][0], ovd[di][de][1], ovd[di][de][2], ovd[di][de][3]});
       }
       // two barriers per K-tile: both k-step-1 image reads first, then all 16 pieces of
       // K-tile t+2 spread one per DS MFMAs, then K-tile t+1's k-step-0 fragments
@@ -810,7 +833,11 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         }
       }
       constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
-      if constexpr (n == VMS && PROBE != 2) q_vmw<dv ? issued : 0, EPI>(FIRST && (pend || OVL));
+      if constexpr (n == VMS && PROBE != 2) {
+        // every store an OVL2 K-tile issued before this wait is younger than the pieces it waits for
+        if constexpr (OV2 || DEF) q_vmwait<(dv ? issued : 0) + 16>();
+        else q_vmw<dv ? issued : 0, EPI>(FIRST && (pend || OVL));
+      }
       if constexpr (n == VMS + 1 && PROBE != 3) q_barrier();
       if constexpr (n >= VMS + 2 && n < VMS + 2 + 16 * NSA_NT4_RS && (n - VMS - 2) % NSA_NT4_RS == 0) {
         constexpr int s = (n - VMS - 2) / NSA_NT4_RS;
@@ -832,8 +859,13 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     int last;
     while (true) {
-      ktile(std::true_type{}, std::true_type{});
-      for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{});
+      ktile(std::true_type{}, std::true_type{}, std::false_type{});
+      if constexpr (NSA_NT4_OVL2) {
+        ktile(std::false_type{}, std::false_type{}, std::true_type{});  // nk >= 2 (host check)
+        for (int kt = 2; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{}, std::false_type{});
+      } else {
+        for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{}, std::false_type{});
+      }
       last = seq;
       seq += G;
       if (seq >= g.tiles) break;
@@ -847,8 +879,8 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     return;
   }
   while (true) {
-    ktile(std::true_type{}, std::false_type{});
-    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{});
+    ktile(std::true_type{}, std::false_type{}, std::false_type{});
+    for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{}, std::false_type{});
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
@@ -962,7 +994,8 @@ hipError_t gemm_nt4_entry(int epi, const void* A, int lda, const void* B, int ld
   switch (epi) {
     case Q_EPI_BF16:
       if (bias) nt4_launch<Q_EPI_BF16, true, H>(a, gr, nt, probe, s);
-      else nt4_launch<Q_EPI_BF16, false, H>(a, gr, nt, probe, s, ovp == 1 || (ovp == 0 && K >= Q_OVL_MIN_K));
+      else nt4_launch<Q_EPI_BF16, false, H>(a, gr, nt, probe, s,
+                                            (ovp == 1 || (ovp == 0 && K >= Q_OVL_MIN_K)) && (!NSA_NT4_OVL2 || K >= 2 * Q_BK));
       break;
     case Q_EPI_GELU:
       if (bias) nt4_launch<Q_EPI_GELU, true, H>(a, gr, nt, probe, s);

@@ -81,7 +81,8 @@ def wgrad_supported(n_out, n_in, tokens) -> bool:
 
 
 NT_VAR = int(os.environ.get("NSA_NT_STORE", "0"))  # epilogue stores: 0 auto, 1 nontemporal, 2 plain
-# plain bf16 outputs: a tile's stores inside the next tile's first K-tile (0 from K = 3072, 1 always, 2 never)
+# plain bf16 outputs: a tile's stores inside the next tile's first two K-tiles (0 automatic: from
+# K = 128, 1 forced on where possible, 2 never; csrc/kernels/gemm_nt4.hip OVL)
 NT_OVL = int(os.environ.get("NSA_NT_OVL", "0"))
 
 

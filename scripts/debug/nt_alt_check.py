@@ -27,7 +27,7 @@ def main():
         ref = gemm.nt(x, w)
         for grid in (gemm.num_cus(x.device), 7, 1):
             c = torch.full((m, n), float("nan"), device="cuda", dtype=torch.bfloat16)
-            err = alt(0, _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c), c.stride(0), None, None,
+            err = alt(int(os.environ.get("ALT_EPI", "0")), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c), c.stride(0), None, None,
                       None, m, n, k, grid, _lib.stream())
             assert err == 0, err
             torch.cuda.synchronize()

@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--xent", action="store_true", help="lm_head: also time the fused cross-entropy (XENT) GEMM")
     ap.add_argument("--ovls", default="", help="overlapped-epilogue policies to time beside auto, e.g. 1,2")
     ap.add_argument("--alt-lib", default="")
+    ap.add_argument("--alt-ovl", type=int, default=0, help="overlapped-epilogue policy bits for the --alt-lib calls")
     a = ap.parse_args()
     alt = alt_xent = None
     if a.alt_lib:
@@ -71,7 +72,7 @@ def main():
         c2 = torch.empty(M_, N_, device=x.device, dtype=torch.bfloat16) if epi == gemm.NT_EPI_GELU else None
         if epi == gemm.NT_EPI_GELU:
             u = gemm.gelu_table(x.device)
-        err = alt(epi | (gemm.NT_VAR << 12), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c),
+        err = alt(epi | (gemm.NT_VAR << 12) | (a.alt_ovl << 14), _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c),
                   c.stride(0), _lib.ptr(c2), _lib.ptr(u), None, M_, N_, K_, gemm.num_cus(x.device), _lib.stream())
         assert err == 0, err
         return (c, c2) if epi == gemm.NT_EPI_GELU else c
