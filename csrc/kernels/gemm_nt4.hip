@@ -68,7 +68,7 @@ constexpr int Q_SMEM = 2 * Q_BUF;       // 128 KiB, two buffers
 
 enum { Q_EPI_BF16 = 0, Q_EPI_GELU = 1, Q_EPI_DGELU = 2, Q_EPI_XENT = 3, Q_EPI_XDX = 4 };
 
-// Overlapped epilogue (OVL, plain bf16 outputs only): each tile's stores ride in the next
+// Overlapped epilogue (OVL, plain bf16 / fp16 outputs without bias): each tile's stores ride in the next
 // tile's first two K-tiles instead of stalling the MFMA pipe between tiles.  In the first
 // K-tile, k-step 0 runs fragment row by fragment row; each accumulator tile is copied out just
 // before the MFMA that restarts it, rows 0-3 go out as 256-byte row stores after their eighth
@@ -176,16 +176,19 @@ __device__ __forceinline__ void q_acc_rd(float (&t)[4], const f32x4& a) {
       : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
 }
 // the next accumulator tile's copy-out packed with the previous one's values (lo = t, hi = a):
-// w[e] = bf16x2 {t[e], a[e]}
+// w[e] = {t[e], a[e]} as bf16x2 (H: fp16x2; both RNE, the instructions pk2 compiles to)
+template <bool H>
 __device__ __forceinline__ void q_acc_rdpk(uint32_t (&w)[4], const float (&t)[4], const f32x4& a) {
   float x0, x1, x2, x3;
-  asm volatile(
-      "v_accvgpr_read_b32 %4, %12\n\tv_accvgpr_read_b32 %5, %13\n\t"
-      "v_accvgpr_read_b32 %6, %14\n\tv_accvgpr_read_b32 %7, %15\n\t"
-      "v_cvt_pk_bf16_f32 %0, %8, %4\n\tv_cvt_pk_bf16_f32 %1, %9, %5\n\t"
-      "v_cvt_pk_bf16_f32 %2, %10, %6\n\tv_cvt_pk_bf16_f32 %3, %11, %7"
-      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-      : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
+#define Q_RDPK(CVT)                                                                                              \
+  asm volatile("v_accvgpr_read_b32 %4, %12\n\tv_accvgpr_read_b32 %5, %13\n\t"                                \
+               "v_accvgpr_read_b32 %6, %14\n\tv_accvgpr_read_b32 %7, %15\n\t" CVT " %0, %8, %4\n\t" CVT        \
+               " %1, %9, %5\n\t" CVT " %2, %10, %6\n\t" CVT " %3, %11, %7"                                      \
+               : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3) \
+               : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]))
+  if constexpr (H) Q_RDPK("v_cvt_pk_f16_f32");
+  else Q_RDPK("v_cvt_pk_bf16_f32");
+#undef Q_RDPK
 }
 template <int OFF>
 __device__ __forceinline__ void q_rd(bf16x8& d, uint32_t addr) {
@@ -632,7 +635,7 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
 // arithmetic without its stores
 template <int EPI, bool NT, int PROBE, bool BIAS = false, bool H = false, bool OVLE = false>
 __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
-  static_assert(!OVLE || (EPI == Q_EPI_BF16 && !BIAS && PROBE == 0 && !H), "OVL: plain bf16 outputs only");
+  static_assert(!OVLE || (EPI == Q_EPI_BF16 && !BIAS && PROBE == 0), "OVL: plain 16-bit outputs only");
   __shared__ __attribute__((aligned(16))) char smem[Q_SMEM + (EPI == Q_EPI_GELU && !H ? Q_GTAB_BYTES : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -779,7 +782,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
           // copies ahead of the K-tile; odd j packs with the even j before it (bf16 pairs of
           // adjacent columns, as one 16-byte row store wants them)
           if constexpr (j % 2 == 0) q_acc_rd(ovt, acc[i][j]);
-          else q_acc_rdpk(ovw[j >> 1], ovt, acc[i][j]);
+          else q_acc_rdpk<H>(ovw[j >> 1], ovt, acc[i][j]);
           q_mfma0t<H>(acc[i][j], a0[i], b0[j]);
         } else if constexpr (FIRST) {
           q_mfma0<H>(acc[i][j], a0[i], b0[j]);
@@ -929,10 +932,10 @@ void nt4_geometry(Nt4Args& a, int gmsel) {
 
 template <int E, bool B, bool H = false>
 void nt4_launch(const Nt4Args& a, dim3 gr, bool nt, int probe, hipStream_t s, bool ovl = false) {
-  if constexpr (E == Q_EPI_BF16 && !B && !H) {
+  if constexpr (E == Q_EPI_BF16 && !B) {
     if (ovl && probe == 0) {
-      if (nt) gemm_nt4_kernel<E, true, 0, false, false, true><<<gr, Q_THR, 0, s>>>(a);
-      else gemm_nt4_kernel<E, false, 0, false, false, true><<<gr, Q_THR, 0, s>>>(a);
+      if (nt) gemm_nt4_kernel<E, true, 0, false, H, true><<<gr, Q_THR, 0, s>>>(a);
+      else gemm_nt4_kernel<E, false, 0, false, H, true><<<gr, Q_THR, 0, s>>>(a);
       return;
     }
   }

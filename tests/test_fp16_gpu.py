@@ -49,6 +49,9 @@ def test_nt4_fp16(kernels, M, N, K):
     y = gemm.nt(x, w, out=nanbuf(M, N))
     assert y.dtype == H16
     check(y, ref, absab, name="nt4 fp16")
+    # the overlapped epilogue (fp16 packs with v_cvt_pk_f16_f32, as pk2) forced on / off
+    for ov, grid in ((1, None), (2, None), (1, 7)):
+        assert torch.equal(gemm.nt(x, w, ovl=ov, grid=grid, out=nanbuf(M, N)), y), (ov, grid)
     yb = gemm.nt(x, w, bias=b, out=nanbuf(M, N))
     check(yb, ref + b.float(), absab + b.float().abs(), name="nt4 fp16 bias")
     gp, g = gemm.nt(x, w, epi=gemm.NT_EPI_GELU, bias=b, out=nanbuf(M, N), out2=nanbuf(M, N))
@@ -69,6 +72,7 @@ def test_nt4_fp16_exact_permutation(kernels):
     a[torch.arange(M, device=DEV), idx] = 1
     bm = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K).remainder(1021).sub(510).to(H16)
     assert torch.equal(gemm.nt(a, bm, out=nanbuf(M, N)).float(), bm.float()[:, idx].t())
+    assert torch.equal(gemm.nt(a, bm, ovl=2, out=nanbuf(M, N)).float(), bm.float()[:, idx].t())
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 192, 64), (100, 72, 40), (17, 300, 128)])
