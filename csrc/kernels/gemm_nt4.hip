@@ -93,6 +93,9 @@ constexpr int Q_GTAB_LO = 14208, Q_GTAB_N = 2560, Q_GTAB_BYTES = 2 * Q_GTAB_N * 
 #ifndef NSA_NT4_GTAB
 #define NSA_NT4_GTAB 1  // 0 (A/B builds only): the arithmetic GELU for every row
 #endif
+#ifndef NSA_NT4_XDEF
+#define NSA_NT4_XDEF 1  // 0 (A/B builds only): the XENT epilogue stores all its rows itself
+#endif
 #ifndef NSA_NT4_GROW
 #define NSA_NT4_GROW 1  // 0 (A/B builds only): the lookups row by row (one ballot and LDS round trip per row)
 #endif
@@ -156,15 +159,19 @@ __device__ __forceinline__ void q_mfma0t(f32x4& acc, const bf16x8& a, const bf16
 }
 // a 16-byte row store pinned between the MFMAs (asm volatile statements keep their order):
 // buffer resource over the previous tile (num_records 0 before the first tile: dropped),
-// lane offset + row offset; the trailing nop keeps the next instruction off its data
-// registers until the store has read them
+// lane offset + row offset.  The leading nop covers an SGPR operand fresh from a VALU write
+// (hipcc restores spilled SGPRs with v_readlane right before the asm, and pads nothing for an
+// asm reader: without it the store took a stale row offset); the trailing one keeps the next
+// instruction off its data registers until the store has read them
 template <bool NT>
 __device__ __forceinline__ void q_st16b(q_i32x4 rsrc, uint32_t voff, uint32_t soff, q_u32x4 v) {
   if constexpr (NT)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc), "s"(soff)
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc),
+                 "s"(soff)
                  : "memory");
   else
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc), "s"(soff)
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc),
+                 "s"(soff)
                  : "memory");
 }
 // copy-out of one accumulator tile (four AGPRs) into VGPRs, pinned between the MFMAs
@@ -357,9 +364,9 @@ __device__ __forceinline__ float q_rowsum16(float v) {
 //       columns into part[2 tile_n + wn][row] (plain stores, one writer per slot: no atomics);
 //  XDX  (dX = dlogits · W): out = g (acc / S_row - W[t_row]) in fp32 before the one rounding,
 //       i.e. (softmax - onehot) · W without a dlogits tensor (ignored rows: 1/S = 0, no W row).
-template <int EPI, bool NT, bool BIAS, bool NOSTORE = false, bool H = false>
+template <int EPI, bool NT, bool BIAS, bool NOSTORE = false, bool H = false, bool DEFER = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
-                                           int lane, const char* tab) {
+                                           int lane, const char* tab, uint32_t (&defer)[4][4][4]) {
   int m0, n0, mlo, nlo;
   q_tile_coords(g, seq, m0, n0, mlo, nlo);
   const bool full = (m0 == mlo) & (n0 == nlo);
@@ -532,7 +539,12 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           // sum is made inf, so nsa_xent_combine sends it to the exact fix-up
           if constexpr (H) s = mx > 65504.0f ? __builtin_inff() : s;
           rs[e] = q_rowsum16(col < nlo ? 0.0f : s);
-          if (!skip) {
+          if (DEFER && i >= 4) {
+            // XDEF: fragment rows 4-7 go out from the next tile's first K-tile (every row:
+            // rows another tile also covers get the same bits)
+#pragma unroll
+            for (int h = 0; h < 4; ++h) defer[i - 4][e][h] = w[h];
+          } else if (!skip) {
             if constexpr (NOSTORE) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
             else q_st16<NT>(cb + off, w[0], w[1], w[2], w[3]);
           }
@@ -767,7 +779,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     constexpr bool OVL = decltype(OVL_)::value;
     constexpr bool DEF = decltype(DEF_)::value;  // OVL2: this K-tile stores the deferred rows
     static_assert(!OVL || FIRST, "the overlapped epilogue rides in a tile's first K-tile");
-    static_assert(!DEF || !FIRST, "the deferred rows go out in a tile's second K-tile");
+    static_assert(!DEF || !FIRST || (EPI == Q_EPI_XENT && !OVL), "OVL2's deferred rows go out in a tile's second K-tile");
     constexpr bool OV2 = OVL && NSA_NT4_OVL2;
     constexpr bool dv = PROBE != 1;
     const uint32_t nb = buf ^ (uint32_t)Q_BUF;
@@ -837,8 +849,11 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       }
       constexpr int issued = (VMS - D0) / DS + 1 < 16 ? (VMS - D0) / DS + 1 : 16;
       if constexpr (n == VMS && PROBE != 2) {
-        // every store an OVL2 K-tile issued before this wait is younger than the pieces it waits for
-        if constexpr (OV2 || DEF) q_vmwait<(dv ? issued : 0) + 16>();
+        // every store an OVL2 K-tile issued before this wait is younger than the pieces it waits
+        // for; XDEF (XENT's first K-tile): the previous epilogue left 32 operations and this
+        // K-tile's 16 deferred stores, 48 = q_epi_vm<XENT> (a tail tile's epilogue drained)
+        if constexpr (EPI == Q_EPI_XENT && DEF) q_vmw<dv ? issued : 0, EPI>(pend);
+        else if constexpr (OV2 || DEF) q_vmwait<(dv ? issued : 0) + 16>();
         else q_vmw<dv ? issued : 0, EPI>(FIRST && (pend || OVL));
       }
       if constexpr (n == VMS + 1 && PROBE != 3) q_barrier();
@@ -877,17 +892,24 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
       prs = q_rsrc(g.C + (int64_t)m0 * g.ldc + n0, 0x7fffffffu);
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    q_epilogue<EPI, NT, BIAS, false, H>(g, acc, last, wm, wn, lane, smem);
+    q_epilogue<EPI, NT, BIAS, false, H>(g, acc, last, wm, wn, lane, smem, ovd);
     q_vmwait<0>();
     return;
   }
+  constexpr bool XDEF = EPI == Q_EPI_XENT && NSA_NT4_XDEF && PROBE == 0;
   while (true) {
-    ktile(std::true_type{}, std::false_type{}, std::false_type{});
+    if constexpr (XDEF) ktile(std::true_type{}, std::false_type{}, std::true_type{});
+    else ktile(std::true_type{}, std::false_type{}, std::false_type{});
     for (int kt = 1; kt < nk; ++kt) ktile(std::false_type{}, std::false_type{}, std::false_type{});
     // MFMA results -> VALU reads: let the last MFMAs drain (hazard not tracked through asm)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (PROBE != 4) {
-      q_epilogue<EPI, NT, BIAS, PROBE == 5, H>(g, acc, seq, wm, wn, lane, smem);
+      q_epilogue<EPI, NT, BIAS, PROBE == 5, H, XDEF>(g, acc, seq, wm, wn, lane, smem, ovd);
+      if constexpr (XDEF) {
+        int m0, n0, mlo, nlo;
+        q_tile_coords(g, seq, m0, n0, mlo, nlo);
+        prs = q_rsrc(g.C + (int64_t)m0 * g.ldc + n0, 0x7fffffffu);  // the next tile's first K-tile stores rows 4-7
+      }
       int m0, n0, mlo, nlo;
       q_tile_coords(g, seq, m0, n0, mlo, nlo);
       if ((m0 == mlo) & (n0 == nlo)) {
@@ -906,6 +928,14 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     }
     seq += G;
     if (seq >= g.tiles) break;
+  }
+  if constexpr (XDEF) {  // the last tile's deferred rows
+#pragma unroll
+    for (int di = 0; di < 4; ++di)
+#pragma unroll
+      for (int de = 0; de < 4; ++de)
+        q_st16b<NT>(prs, pvo, (uint32_t)((16 * (4 + di) + de) * g.ldc * 2),
+                    q_u32x4{ovd[di][de][0], ovd[di][de][1], ovd[di][de][2], ovd[di][de][3]});
   }
   q_vmwait<0>();
 }
