@@ -93,6 +93,9 @@ constexpr int Q_GTAB_LO = 14208, Q_GTAB_N = 2560, Q_GTAB_BYTES = 2 * Q_GTAB_N * 
 #ifndef NSA_NT4_GTAB
 #define NSA_NT4_GTAB 1  // 0 (A/B builds only): the arithmetic GELU for every row
 #endif
+#ifndef NSA_NT4_DDEF
+#define NSA_NT4_DDEF 1  // 0 (A/B builds only): the GELU' epilogue stores all its rows itself
+#endif
 #ifndef NSA_NT4_XDEF
 #define NSA_NT4_XDEF 1  // 0 (A/B builds only): the XENT epilogue stores all its rows itself
 #endif
@@ -430,6 +433,13 @@ __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[
           w[e][h] = pk2<H>(a.x, a.y);
         }
       if (i + 2 < 8) load_u(i + 2, uv[i & 1]);
+      if (DEFER && i >= 4) {  // DDEF: rows 4-7 go out from the next tile's first K-tile
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) defer[i - 4][e][h] = w[e][h];
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool skip = !full && (row0 + 16 * i + e < mlo || col < nlo);
@@ -779,7 +789,8 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     constexpr bool OVL = decltype(OVL_)::value;
     constexpr bool DEF = decltype(DEF_)::value;  // OVL2: this K-tile stores the deferred rows
     static_assert(!OVL || FIRST, "the overlapped epilogue rides in a tile's first K-tile");
-    static_assert(!DEF || !FIRST || (EPI == Q_EPI_XENT && !OVL), "OVL2's deferred rows go out in a tile's second K-tile");
+    static_assert(!DEF || !FIRST || ((EPI == Q_EPI_XENT || EPI == Q_EPI_DGELU) && !OVL),
+                  "OVL2's deferred rows go out in a tile's second K-tile");
     constexpr bool OV2 = OVL && NSA_NT4_OVL2;
     constexpr bool dv = PROBE != 1;
     const uint32_t nb = buf ^ (uint32_t)Q_BUF;
@@ -852,7 +863,7 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
         // every store an OVL2 K-tile issued before this wait is younger than the pieces it waits
         // for; XDEF (XENT's first K-tile): the previous epilogue left 32 operations and this
         // K-tile's 16 deferred stores, 48 = q_epi_vm<XENT> (a tail tile's epilogue drained)
-        if constexpr (EPI == Q_EPI_XENT && DEF) q_vmw<dv ? issued : 0, EPI>(pend);
+        if constexpr ((EPI == Q_EPI_XENT || EPI == Q_EPI_DGELU) && DEF) q_vmw<dv ? issued : 0, EPI>(pend);
         else if constexpr (OV2 || DEF) q_vmwait<(dv ? issued : 0) + 16>();
         else q_vmw<dv ? issued : 0, EPI>(FIRST && (pend || OVL));
       }
@@ -896,7 +907,10 @@ __global__ __launch_bounds__(Q_THR, 1) void gemm_nt4_kernel(Nt4Args g) {
     q_vmwait<0>();
     return;
   }
-  constexpr bool XDEF = EPI == Q_EPI_XENT && NSA_NT4_XDEF && PROBE == 0;
+  // XDEF (XENT) / DDEF (GELU'): the epilogue leaves fragment rows 4-7 (16 row stores) to the
+  // next tile's first K-tile, where the write path drains them under the MFMAs
+  constexpr bool XDEF = PROBE == 0 && ((EPI == Q_EPI_XENT && NSA_NT4_XDEF) ||
+                                       (EPI == Q_EPI_DGELU && !H && NSA_NT4_GROW && NSA_NT4_DDEF));
   while (true) {
     if constexpr (XDEF) ktile(std::true_type{}, std::false_type{}, std::true_type{});
     else ktile(std::true_type{}, std::false_type{}, std::false_type{});
