@@ -93,6 +93,9 @@ constexpr int Q_GTAB_LO = 14208, Q_GTAB_N = 2560, Q_GTAB_BYTES = 2 * Q_GTAB_N * 
 #ifndef NSA_NT4_GTAB
 #define NSA_NT4_GTAB 1  // 0 (A/B builds only): the arithmetic GELU for every row
 #endif
+#ifndef NSA_NT4_XLANE
+#define NSA_NT4_XLANE 1  // 1: the XDX and fp16 GELU' epilogues re-derive the lane id (q_lane_now)
+#endif
 #ifndef NSA_NT4_DDEF
 #define NSA_NT4_DDEF 1  // 0 (A/B builds only): the GELU' epilogue stores all its rows itself
 #endif
@@ -367,12 +370,21 @@ __device__ __forceinline__ float q_rowsum16(float v) {
 //       columns into part[2 tile_n + wn][row] (plain stores, one writer per slot: no atomics);
 //  XDX  (dX = dlogits · W): out = g (acc / S_row - W[t_row]) in fp32 before the one rounding,
 //       i.e. (softmax - onehot) · W without a dlogits tensor (ignored rows: 1/S = 0, no W row).
+// The lane id, re-derived where it is used: opaque to the compiler, so the lane-derived row and
+// column offsets are not kept live across the K-loop (the XDX epilogue spilled two of them).
+__device__ __forceinline__ int q_lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 template <int EPI, bool NT, bool BIAS, bool NOSTORE = false, bool H = false, bool DEFER = false>
 __device__ __forceinline__ void q_epilogue(const Nt4Args& g, const f32x4 (&acc)[8][8], int seq, int wm, int wn,
                                            int lane, const char* tab, uint32_t (&defer)[4][4][4]) {
   int m0, n0, mlo, nlo;
   q_tile_coords(g, seq, m0, n0, mlo, nlo);
   const bool full = (m0 == mlo) & (n0 == nlo);
+  if constexpr ((EPI == Q_EPI_XDX || (EPI == Q_EPI_DGELU && H)) && NSA_NT4_XLANE) lane = q_lane_now();
   const int r = lane & 15, q = lane >> 4;
   const int col = n0 + wn * 128 + 8 * r;
   const int row0 = m0 + wm * 128 + 4 * q;

@@ -52,11 +52,12 @@ def main():
     ap.add_argument("--vars", default="0", help="epilogue store policies to time (0 auto, 1 nontemporal, 2 plain)")
     ap.add_argument("--small", action="store_true", help="also time the bounds-checked small-tile kernel")
     ap.add_argument("--xent", action="store_true", help="lm_head: also time the fused cross-entropy (XENT) GEMM")
+    ap.add_argument("--xdx", action="store_true", help="lm_head.dx: also time the fused cross-entropy dX (XDX) GEMM")
     ap.add_argument("--ovls", default="", help="overlapped-epilogue policies to time beside auto, e.g. 1,2")
     ap.add_argument("--alt-lib", default="")
     ap.add_argument("--alt-ovl", type=int, default=0, help="overlapped-epilogue policy bits for the --alt-lib calls")
     a = ap.parse_args()
-    alt = alt_xent = None
+    alt = alt_xent = alt_xdx = None
     if a.alt_lib:
         alt = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4
         alt.argtypes = _lib._SIGNATURES["nsa_gemm_nt4"]
@@ -64,6 +65,9 @@ def main():
         alt_xent = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4_xent
         alt_xent.argtypes = _lib._SIGNATURES["nsa_gemm_nt4_xent"]
         alt_xent.restype = ctypes.c_int
+        alt_xdx = ctypes.CDLL(a.alt_lib).nsa_gemm_nt4_xdx
+        alt_xdx.argtypes = _lib._SIGNATURES["nsa_gemm_nt4_xdx"]
+        alt_xdx.restype = ctypes.c_int
 
     def nt_alt(x, w, epi=0, u=None):
         M_, K_ = x.shape
@@ -124,6 +128,22 @@ def main():
                                   "part_maxrel": ((part2 - part_ref).abs() / part_ref.abs().clamp_min(1e-30)).max().item()}),
                       flush=True)
                 cands["nt4_alt_xent"] = xent_alt
+        if a.xdx and name == "lm_head.dx":
+            wrows = uni(M, N)
+            coef = torch.rand(M, 2, device=x.device)
+            c_ref = gemm.nt_xdx(x, w, wrows, coef)
+            cands["nt4_xdx"] = lambda: gemm.nt_xdx(x, w, wrows, coef, out=c_ref)
+            if a.alt_lib:
+                c2 = torch.empty_like(c_ref)
+
+                def xdx_alt():
+                    err = alt_xdx(_lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(c2), c2.stride(0),
+                                  _lib.ptr(wrows), _lib.ptr(coef), M, N, K, gemm.num_cus(x.device), _lib.stream())
+                    assert err == 0, err
+                xdx_alt()
+                torch.cuda.synchronize()
+                print(json.dumps({"check": "lm_head.dx/xdx_vs_alt", "equal": torch.equal(c2, c_ref)}), flush=True)
+                cands["nt4_alt_xdx"] = xdx_alt
         for ov in [int(t) for t in a.ovls.split(",") if t]:
             cands[f"nt4_ovl{ov}"] = lambda ov=ov: gemm.nt(x, w, ovl=ov)
             assert torch.equal(gemm.nt(x, w, ovl=ov), got), ov
