@@ -42,25 +42,37 @@ __global__ __launch_bounds__(256) void seg_row_kernel(const int64_t* __restrict_
   if (v >= V) return;
   const int64_t beg = seg[v], end = seg[v + 1];
   if (beg == end || end - beg > kSegLong) return;  // empty, or the chunk kernels' segment
-  for (int c = lane * 8; c < C; c += 512) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // one walk of the segment covers two 512-column halves (C = 768: one walk instead of two,
+  // so the dependent seg -> order -> row loads run once per id); per column the rows are
+  // still added in sorted order, so the sums are bitwise those of one walk per half
+  for (int c = lane * 8; c < C; c += 1024) {
+    const bool two = c + 512 < C;
+    float acc[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
     for (int64_t k = beg; k < end; k += 4) {
       const int n = (int)min((int64_t)4, end - k);
       int64_t rw[4];
-      float x[4][8];
+      float x[4][2][8];
 #pragma unroll
       for (int u = 0; u < 4; ++u) rw[u] = u < n ? order[k + u] : 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (u < n) f.load(rw[u], (int64_t)v, c, x[u]);
+        if (u < n) {
+          f.load(rw[u], (int64_t)v, c, x[u][0]);
+          if (two) f.load(rw[u], (int64_t)v, c + 512, x[u][1]);
+        }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (u < n) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += x[u][j];
+          for (int j = 0; j < 8; ++j) acc[0][j] += x[u][0][j];
+          if (two) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[1][j] += x[u][1][j];
+          }
         }
     }
-    seg_rmw8(out + (int64_t)v * ldo + c, acc);
+    seg_rmw8(out + (int64_t)v * ldo + c, acc[0]);
+    if (two) seg_rmw8(out + (int64_t)v * ldo + c + 512, acc[1]);
   }
 }
 
